@@ -1,0 +1,123 @@
+/*
+ * mpss.h -- C ABI of libmpss, the MI355X-native multipole subsurface-scattering path for
+ * pbrt-v2-skin (Thomi6York/pbrt-v2-skin).  Plain C: no C++ or torch types cross it.
+ *
+ * It replaces, one for one, the pieces of pbrt's SurfaceIntegrator plugin surface for
+ * "multipolesubsurface" + "layeredskin" (reference paths relative to /root/reference):
+ *
+ *   mpss_create / mpss_destroy      CreateMultipoleSubsurfaceIntegrator + dtor
+ *                                   (src/integrators/multipolesubsurface.cpp:306-320 [file 390-404],
+ *                                    src/integrators/multipolesubsurface.h:46-63)
+ *   mpss_add_layeredskin            CreateLayeredSkinMaterial + LayeredSkin::LayeredSkin parse-time
+ *                                   precompute (src/materials/layeredskin.cpp:39-123, 222-262;
+ *                                   src/core/multipole.cpp:241-295, 371-406, 466-549)
+ *   mpss_set_material_tables        MultipoleBSSRDFData(pData, rhoData) for externally built tables
+ *                                   (src/core/multipole.h:44-59)
+ *   mpss_get_material_tables        read back Profile::data / rcpDsqSpacing / RhoData::hd
+ *   mpss_set_irradiance_points      the octree build at the end of Preprocess
+ *                                   (multipolesubsurface.cpp:301-321 [file], diffusionutil.h:94-173)
+ *   mpss_mo_batch                   SubsurfaceOctreeNode::Mo over a batch of shading points
+ *                                   (diffusionutil.h:175-210 via multipolesubsurface.cpp:364)
+ *
+ * Error convention: every entry point returns MPSS_OK (0) or a negative MPSS_ERR_* code and
+ * records a message retrievable with mpss_last_error() (thread-local). No exception ever
+ * crosses the boundary; the reference's Severe()/abort() paths become error returns.
+ * Pointers named *_dev are HIP device pointers (e.g. torch CUDA tensors' data_ptr());
+ * all other arrays are caller-owned host memory that is copied in.
+ * stream: a hipStream_t (NULL = legacy default stream).
+ */
+#ifndef MPSS_H
+#define MPSS_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPSS_NBANDS 30 /* nSpectralSamples, src/core/spectrum.h:46 */
+
+enum {
+    MPSS_OK = 0,
+    MPSS_ERR_INVALID = -1,   /* bad argument / state */
+    MPSS_ERR_INTERNAL = -2,  /* algorithmic failure (e.g. degenerate point cloud) */
+    MPSS_ERR_HIP = -3,       /* HIP runtime error */
+    MPSS_ERR_NOMEM = -4
+};
+
+typedef struct mpss_ctx mpss_ctx;
+
+/* Integrator parameters, defaults as CreateMultipoleSubsurfaceIntegrator (file lines 393-401). */
+typedef struct {
+    int device;                /* HIP device ordinal */
+    int max_depth;             /* "maxdepth" = 5 */
+    float max_error;           /* "maxerror" = .05 */
+    float min_sample_distance; /* "minsampledistance" = .25 */
+    float mix;                 /* "mix" = .5 */
+    int show_irradiance_points;/* "showirradiancepoints" = false */
+    int incenter;              /* "incenter" = false */
+    int quick_render;          /* PbrtOptions.quickRender: maxError *= 4, minDist *= 4 */
+} mpss_config;
+
+void mpss_config_defaults(mpss_config *cfg);
+int mpss_create(const mpss_config *cfg, mpss_ctx **out);
+void mpss_destroy(mpss_ctx *ctx);
+const char *mpss_last_error(void);
+int mpss_abi_version(void);
+
+/* LayeredSkin parameters, defaults as CreateLayeredSkinMaterial (layeredskin.cpp:234-257). */
+typedef struct {
+    float roughness;      /* 0.4 */
+    float nmperunit;      /* 100e6 */
+    float f_mel, f_eu, f_blood, f_ohg;  /* 0.15, 1, 0.002, 0.3 */
+    float ga_epi, ga_derm, b_derm;      /* 0.9, 0.8, 0.4 (carried, unused by the multipole path) */
+    float layer_thickness_nm[2];        /* "skinlayer layers" thickness (nm) */
+    float layer_ior[2];                 /* "skinlayer layers" ior */
+    float albedo[MPSS_NBANDS];          /* constant "albedo" texture value (default Spectrum(1)) */
+    int desired_length;   /* "desiredlength" = 512 */
+    int lerp_on_thin_slab;/* "lerponthinslab" = true */
+    int double_ref_sslf;  /* "doublerefsslf" = false (FixedFresnelDielectric) */
+} mpss_layeredskin;
+
+void mpss_layeredskin_defaults(mpss_layeredskin *m);
+/* Builds the 30-band multipole profile and the 1025-entry rho_hd table; returns a material id. */
+int mpss_add_layeredskin(mpss_ctx *ctx, const mpss_layeredskin *m, uint32_t *material_id);
+/* Install precomputed tables: rd_table is channel-major [30][length]; rcp[30] = rcpDsqSpacing;
+ * rho_hd[n_rho] (scalar, replicated over bands); albedo[30]. */
+int mpss_set_material_tables(mpss_ctx *ctx, const float *rd_table, uint32_t length, const float *rcp,
+                             const float *rho_hd, uint32_t n_rho, const float *albedo, int is_monte_carlo,
+                             uint32_t *material_id);
+/* Query sizes first with NULL buffers: *length and *n_rho are always written. */
+int mpss_get_material_tables(mpss_ctx *ctx, uint32_t material_id, float *rd_table, uint32_t *length, float *rcp,
+                             float *rho_hd, uint32_t *n_rho, float *total_reflectance);
+
+/* Irradiance points (IrradiancePoint p, n, E, area; irradiancepoint.h:36-45) -> device octree. */
+int mpss_set_irradiance_points(mpss_ctx *ctx, uint32_t n, const float *p, const float *nrm, const float *E,
+                               const float *area);
+/* Octree statistics: node count, max depth, point count. */
+int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint32_t *n_points);
+
+/* Mo for q shading points (p_dev: q*3 floats) with material's Rd profile; mo_dev: q*30 floats.
+ * counters_dev (nullable): q*2 int32 {octree nodes entered, leaf points evaluated}. */
+int mpss_mo_batch(mpss_ctx *ctx, uint32_t material_id, uint32_t q, const float *p_dev, float *mo_dev,
+                  int32_t *counters_dev, void *stream);
+
+/* ---- host-side utilities (no HIP device needed): the product's own parse-time builders,
+ * exposed so their results can be checked on a CPU-only machine. ---- */
+/* LayeredSkin -> per-layer 30-band mua/musp [2][30], thickness[2], eta[2] (layeredskin.cpp:47-89). */
+int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta);
+/* Multipole profile from layer params; rd_table: [30][*length] (query *length with rd_table NULL). */
+int mpss_host_build_profile(const float *mua, const float *musp, const float *thickness, const float *eta,
+                            int desired_length, int lerp_on_thin_slab, float *rd_table, uint32_t *length,
+                            float *rcp, float *total_reflectance);
+/* rho_hd table (n entries, sqrt_samples^2 samples each) and rho_hh. */
+int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, int sqrt_samples, float *hd,
+                        float *hh);
+/* Octree build + pre-order export (sizes first with NULL outputs). */
+int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
+                            uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,
+                            int32_t *skip, int32_t *leaf_first, int32_t *leaf_count, int32_t *point_order);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,96 @@
+/*
+ * oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, single precision where the reference is single
+ * precision, double where it is double) of pbrt-v2-skin's multipole
+ * subsurface-scattering hot path.  It is the parity checker for the HIP product
+ * in pbrt-v2-skin_amd/; nothing outside tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.
+ *
+ * Parity status: the reference ships no golden vectors for this path and its
+ * binary cannot be built or run here (SURVEY.md section 8c records the denial),
+ * so this restatement is "parity unpinned" against reference outputs.  It is
+ * pinned instead by the reference's own physics self-checks, restated as tests:
+ *   - kissfft vs brute-force DFT   (libkissfft/test/test_vs_dft.c)
+ *   - MPC profile integral vs totalReflectance (src/multipole/test/test.cpp:74-75)
+ *   - Mo() at maxError -> 0 equals the brute-force point sum (diffusionutil.h:175-210)
+ *   - analytic single dipole (diffusionutil.h:38-83) as a closed-form Rd
+ * Every function cites the reference file:line it follows.
+ *
+ * Build: make -C oracle  (gcc -O2 -ffp-contract=off, no -ffast-math)
+ */
+#ifndef MPSS_ORACLE_H
+#define MPSS_ORACLE_H
+#include <stdint.h>
+
+#define O_NB 30 /* nSpectralSamples, src/core/spectrum.h:46 */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- spectrum (src/core/spectrum.h:291-393, spectrum.cpp:60-193) ---- */
+float o_average_spectrum_samples(const float *lambda, const float *vals, int n, float l0, float l1);
+void o_from_sampled(const float *lambda, const float *vals, int n, float out[O_NB]);
+void o_from_rgb(const float rgb[3], int illuminant, float out[O_NB]);
+float o_y(const float s[O_NB]);
+void o_to_xyz(const float s[O_NB], float xyz[3]);
+
+/* ---- skin coefficients (materials/skincoeffs.h:38-158, layeredskin.cpp:39-89) ---- */
+typedef struct {
+    float roughness, nmperunit;
+    float f_mel, f_eu, f_blood, f_ohg;
+    float layer_thickness_nm[2];
+    float layer_ior[2];
+} o_skin_params;
+void o_skin_layers(const o_skin_params *p, float mua[2][O_NB], float musp[2][O_NB],
+                   float thickness[2], float eta[2]);
+
+/* ---- kissfft v1.3.0 restated, kiss_fft_scalar = double ---- */
+typedef struct { double r, i; } o_cpx;
+void o_kiss_fft(int nfft, int inverse, const o_cpx *fin, o_cpx *fout);
+void o_kiss_fftndr2(int rows, int cols, const double *in, o_cpx *out);   /* forward */
+void o_kiss_fftndri2(int rows, int cols, const o_cpx *in, double *out);  /* inverse (unscaled) */
+
+/* ---- MPC (MultipoleProfileCalculator.cpp:151-426, DipoleCalculator.cpp:38-91) ---- */
+typedef struct { float ior, thickness, mua, musp; } o_layer_spec;
+/* Returns number of (dsq, R, T) entries written before resampling; caller frees *out arrays via o_free. */
+int o_mpc_profile(int nlayers, const o_layer_spec *specs, float step, int desired_length,
+                  int lerp_on_thin_slab, int resample, float **dsq, float **refl, float **trans,
+                  float *total_r, float *total_t);
+void o_free(void *p);
+float o_dipole_rd(float eta0, float etad, float d, float mua, float musp, int zi, int lerp, float dsq);
+
+/* Per-channel profile (multipole.cpp:241-295). table: [O_NB][*len] floats (channel-major). */
+int o_compute_profile(const float mua[2][O_NB], const float musp[2][O_NB], const float eta[2],
+                      const float thickness[2], int desired_length, int lerp_on_thin_slab,
+                      int nthreads, float **table, float rcp[O_NB], float spacing[O_NB],
+                      float total_r[O_NB]);
+/* sampleProfile (multipole.cpp:60-73) for one channel */
+float o_sample_profile(const float *data, int len, float rcp, float dsq);
+
+/* ---- rho table (multipole.cpp:466-549; reflection.cpp:132-153,228-240,391-403,548-580,623-652) ---- */
+void o_rho_table(float roughness, float eta, int n_entries /*1025*/, int sqrt_samples /*256*/,
+                 int nthreads, float *hd, float *hh);
+uint32_t o_mt_first(uint32_t seed, int n, uint32_t *out); /* MT19937 stream check */
+
+/* ---- octree + Mo (diffusionutil.h:86-234; multipolesubsurface.cpp:301-321) ---- */
+typedef struct o_octree o_octree;
+o_octree *o_octree_build(int n, const float *p /*n*3*/, const float *n_ /*n*3*/, const float *E /*n*O_NB*/,
+                         const float *area /*n*/);
+void o_octree_free(o_octree *t);
+int o_octree_num_nodes(const o_octree *t);
+/* Mo for q queries; rd_table channel-major [O_NB][len]; counters (nullable): per query nodes, points */
+void o_mo_batch(const o_octree *t, int q, const float *pts /*q*3*/, const float *rd_table, int len,
+                const float rcp[O_NB], float max_error, float *mo /*q*O_NB*/, int32_t *n_nodes,
+                int32_t *n_points, int nthreads);
+/* Flatten for inspection: pre-order nodes (same order as the product's layout contract) */
+int o_octree_export(const o_octree *t, float *node_p /*N*3*/, float *node_area, float *node_et /*N*O_NB*/,
+                    float *bmin /*N*3*/, float *bmax /*N*3*/, int32_t *depth, int32_t *skip,
+                    int32_t *leaf_first, int32_t *leaf_count, int32_t *point_order);
+void o_octree_bounds(const o_octree *t, float bmin[3], float bmax[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,552 @@
+// material.cpp -- LayeredSkin parse-time precompute (host, multithreaded). See material.h
+// for the reference functions followed. The layer grids and their frequency-domain
+// combination are FP64 exactly as the reference's MPC; the 2-D transforms use this
+// file's own radix-2 FFT (not kissfft), so tables agree with the oracle to FP64
+// rounding, which tests/test_profile.py bounds.
+#include "material.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <thread>
+
+#include "spectral.h"
+
+namespace mpss {
+
+// ------------------------------------------------------------ skin coefficients
+namespace {
+constexpr int WLD_N = 61;  // core/material.h:96
+inline float wld_lambda(int i) { return 400.f + 5.f * (float)i; }
+
+const float kOxy[WLD_N] = {  // skincoeffs.cpp:44-52
+    266200, 331450, 466800, 523100, 480400, 351100, 246100, 149050, 102600, 78880, 62820, 51525,
+    44480, 38440, 33210, 29480, 26630, 24925, 23680, 22155, 20930, 20185, 20040, 20715, 24200,
+    30885, 39960, 48335, 53240, 50985, 43020, 35650, 32610, 35210, 44500, 54425, 50100, 30620,
+    14400, 6681.5f, 3200, 1958.5f, 1506, 1166.5f, 942, 740.8f, 610, 495.6f, 442, 397.7f, 368,
+    340.3f, 319.6f, 305.6f, 294, 283.8f, 277.6f, 273.6f, 276, 280.6f, 290};
+const float kDeoxy[WLD_N] = {  // skincoeffs.cpp:64-72
+    223300, 261950, 304000, 353200, 407600, 471500, 528600, 549600, 413300, 259950, 103300,
+    33435, 23390, 18700, 16160, 14920, 14550, 15375, 16680, 18650, 20860, 23285, 25770, 28680,
+    31590, 35170, 39040, 42840, 46590, 50490, 53410, 54530, 53790, 49700, 45070, 40905, 37020,
+    33590, 28320, 21185, 14680, 12040, 9444, 7553.5f, 6510, 5763.5f, 5149, 4666.5f, 4345,
+    4026.5f, 3750, 3481.5f, 3227, 3011, 2795, 2591, 2408, 2224.5f, 2052, 1923.5f, 1794};
+
+// WLDValue::FromSampled (core/material.h:118-141): piecewise-linear resampling onto the WLD grid
+void wld_resample(const float *vals, float out[WLD_N]) {
+    int idx = 0;
+    float l0 = 0.f, l1 = wld_lambda(0), v0 = vals[0], v1 = vals[0];
+    for (int i = 0; i < WLD_N; ++i) {
+        const float lam = wld_lambda(i);
+        while (lam > l1 && idx < WLD_N - 1) {
+            ++idx;
+            l0 = l1;
+            l1 = wld_lambda(idx);
+            v0 = v1;
+            v1 = vals[idx];
+        }
+        out[i] = (lam <= l1) ? lerpf_((lam - l0) / (l1 - l0), v0, v1) : v1;
+    }
+}
+
+void wld_to_bands(const float w[WLD_N], float out[NB]) {
+    float lam[WLD_N];
+    for (int i = 0; i < WLD_N; ++i) lam[i] = wld_lambda(i);
+    spectrum_from_sampled(lam, w, WLD_N, out);
+}
+}  // namespace
+
+void skin_layer_params(const SkinParams &p, LayerParams &out) {
+    float base[WLD_N], eu[WLD_N], pheo[WLD_N], sct[WLD_N];
+    for (int i = 0; i < WLD_N; ++i) {
+        const float wl = wld_lambda(i);
+        base[i] = 0.244f + 85.3f * expf(-(wl - 154.f) / 66.2f);            // skincoeffs.h:46-50
+        eu[i] = 6.6e11f * powf(wl, -3.33f);                                 // :54-58
+        pheo[i] = 2.9e15f * powf(wl, -4.75f);                               // :60-64
+        sct[i] = 2e12f * powf(wl, -4.f) + 147.4f * powf(wl, (float)-0.22);  // :79-81,119-130
+    }
+    float oxy[WLD_N], deo[WLD_N];
+    wld_resample(kOxy, oxy);
+    wld_resample(kDeoxy, deo);
+    const float unit = p.nmperunit / 1e7f;  // layeredskin.cpp:47
+    const float kblood = 2.303f / 64500.f * 150.f;
+    float ea[WLD_N], es[WLD_N], da[WLD_N], ds[WLD_N];
+    for (int i = 0; i < WLD_N; ++i) {
+        const float mel = eu[i] * p.f_eu + pheo[i] * (1 - p.f_eu);
+        ea[i] = (mel * p.f_mel + base[i] * (1 - p.f_mel)) * unit;                    // mua_epi
+        es[i] = sct[i] * unit;                                                        // musp_epi
+        const float blood = (oxy[i] * p.f_ohg + deo[i] * (1.f - p.f_ohg)) * kblood;  // mua_blood
+        da[i] = (blood * p.f_blood + base[i] * (1 - p.f_blood)) * unit;               // mua_derm
+        ds[i] = (sct[i] * 0.5f) * unit;                                               // musp_derm
+    }
+    wld_to_bands(ea, out.mua[0]);
+    wld_to_bands(es, out.musp[0]);
+    wld_to_bands(da, out.mua[1]);
+    wld_to_bands(ds, out.musp[1]);
+    for (int l = 0; l < 2; ++l) {
+        out.thickness[l] = p.thickness_nm[l] / p.nmperunit;
+        out.eta[l] = p.ior[l];
+    }
+}
+
+// ------------------------------------------------------------ multipole profile
+namespace {
+
+constexpr float kPiMPC = 3.141592654f;  // numutil.h:45 (the MPC's own PI)
+
+float fresnel_diffuse(float eta) {  // DipoleCalculator.cpp:38-46
+    if (eta >= 1.f) return -1.4399f / (eta * eta) + 0.7099f / eta + 0.6681f + 0.0636f * eta;
+    const float e2 = eta * eta;
+    return -0.4399f + 0.7099f / eta - 0.3319f / e2 + 0.0636f / (e2 * eta);
+}
+
+struct Dipole {  // DipoleCalculator.cpp:52-91
+    float d, zpos, zneg, str, alphap;
+    Dipole(float eta0, float etad, float thick, float sa, float sps, int zi, bool lerp) {
+        d = thick;
+        const float spt = sa + sps;
+        str = sqrtf(3 * sa * spt);
+        alphap = sps / spt;
+        const float F0 = fresnel_diffuse(eta0), Fd = fresnel_diffuse(etad);
+        const float A0 = (1.f + F0) / (1.f - F0), Ad = (1.f + Fd) / (1.f - Fd);
+        const float D = 1.f / (3.f * spt);
+        const float zb0 = 2.f * A0 * D, zbd = 2.f * Ad * D;
+        float l = 1.f / spt;
+        if (lerp && l > d * .5f) l = d * .5f;
+        zpos = 2.f * (float)zi * (d + zb0 + zbd) + l;
+        zneg = zpos - 2.f * (l + zb0);
+    }
+    float term(float z, float dsq) const {
+        const float r = sqrtf(dsq + z * z);
+        return z * (1 + str * r) * expf(-str * r) / (r * r * r);
+    }
+    float Rd(float dsq) const { return alphap * (0.25f / kPiMPC) * (term(zpos, dsq) - term(zneg, dsq)); }
+    float Td(float dsq) const {
+        return alphap * (0.25f / kPiMPC) * (term(d - zpos, dsq) - term(d - zneg, dsq));
+    }
+};
+
+// Layer grid: N x N doubles, centre (N-1)/2 (MultipoleProfileCalculator.cpp:151-230)
+void layer_grid(float ior_up, float ior_lo, float thick, float mua, float musp, float step, bool lerp_thin, int N,
+                std::vector<double> &R, std::vector<double> &T) {
+    R.assign((size_t)N * N, 0.0);
+    T.assign((size_t)N * N, 0.0);
+    const double mfp2 = 2. / (mua + musp);
+    double lerp = 1.;
+    if (lerp_thin) {
+        lerp = (thick < mfp2) ? (1. - exp(-thick * 2. / mfp2)) / (1. - exp(-2.)) : 1.;
+        if (thick < 0.01 * mfp2) thick = (float)(0.01 * mfp2);
+    }
+    const int c = (N - 1) / 2, ext = c;
+    std::vector<Dipole> dips;
+    for (int pair = -5; pair <= 5; ++pair) dips.emplace_back(ior_up, ior_lo, thick, mua, musp, pair, lerp_thin);
+    const float s2 = step * step;
+    const double nf = s2;
+    auto at = [&](std::vector<double> &M, int r, int col) -> double & { return M[(size_t)r * N + col]; };
+    for (int i = 0; i <= ext; ++i)
+        for (int j = i; j <= ext; ++j) {
+            const double r2 = ((double)((unsigned)i * (unsigned)i) + (double)((unsigned)j * (unsigned)j)) * s2;
+            double &rr = at(R, c + i, c + j), &tt = at(T, c + i, c + j);
+            for (const Dipole &dp : dips) {
+                rr += dp.Rd((float)r2) * nf;
+                tt += dp.Td((float)r2) * nf;
+            }
+        }
+    if (lerp < 1.) {
+        for (int i = 0; i <= ext; ++i)
+            for (int j = i; j <= ext; ++j) {
+                at(R, c + i, c + j) *= lerp;
+                at(T, c + i, c + j) *= lerp;
+            }
+        at(T, c, c) += 1. - lerp;
+    }
+    for (int i = 1; i <= ext; ++i)
+        for (int j = 0; j < i; ++j) {
+            at(R, c + i, c + j) = at(R, c + j, c + i);
+            at(T, c + i, c + j) = at(T, c + j, c + i);
+        }
+    for (int i = 0; i <= ext; ++i)
+        for (int j = 0; j <= ext; ++j) {
+            const double rv = at(R, c + i, c + j), tv = at(T, c + i, c + j);
+            at(R, c - i, c + j) = rv; at(R, c + i, c - j) = rv; at(R, c - i, c - j) = rv;
+            at(T, c - i, c + j) = tv; at(T, c + i, c - j) = tv; at(T, c - i, c - j) = tv;
+        }
+}
+
+using cd = std::complex<double>;
+
+// In-place iterative radix-2 DIT FFT over n points with stride 1.
+struct FFT1 {
+    int n, logn;
+    std::vector<cd> tw;       // e^{-2 pi i k / n}
+    std::vector<int> rev;
+    explicit FFT1(int n_) : n(n_) {
+        logn = 0;
+        while ((1 << logn) < n) ++logn;
+        tw.resize(n / 2);
+        for (int k = 0; k < n / 2; ++k) {
+            const double ph = -2.0 * M_PI * (double)k / (double)n;
+            tw[k] = cd(cos(ph), sin(ph));
+        }
+        rev.resize(n);
+        for (int i = 0; i < n; ++i) {
+            int r = 0;
+            for (int b = 0; b < logn; ++b)
+                if (i & (1 << b)) r |= 1 << (logn - 1 - b);
+            rev[i] = r;
+        }
+    }
+    void run(cd *a, bool inverse) const {
+        for (int i = 0; i < n; ++i)
+            if (i < rev[i]) std::swap(a[i], a[rev[i]]);
+        for (int len = 2; len <= n; len <<= 1) {
+            const int half = len >> 1, step = n / len;
+            for (int i = 0; i < n; i += len)
+                for (int j = 0; j < half; ++j) {
+                    cd w = tw[(size_t)j * step];
+                    if (inverse) w = std::conj(w);
+                    const cd u = a[i + j], v = a[i + j + half] * w;
+                    a[i + j] = u + v;
+                    a[i + j + half] = u - v;
+                }
+        }
+    }
+};
+
+// 2-D FFT of an M x M complex array (rows, then columns through a column buffer).
+void fft2(const FFT1 &f, std::vector<cd> &A, int M, bool inverse) {
+    for (int r = 0; r < M; ++r) f.run(&A[(size_t)r * M], inverse);
+    std::vector<cd> col(M);
+    for (int c = 0; c < M; ++c) {
+        for (int r = 0; r < M; ++r) col[r] = A[(size_t)r * M + c];
+        f.run(col.data(), inverse);
+        for (int r = 0; r < M; ++r) A[(size_t)r * M + c] = col[r];
+    }
+}
+
+// Circularly centre an N x N grid (centre (N-1)/2) on the origin of a 2N x 2N array and transform
+// (ToFrequencyDomain + ScaleAndShift, MultipoleProfileCalculator.cpp:233-240, numutil.h:201-213).
+void to_freq(const FFT1 &f, const std::vector<double> &P, int N, std::vector<cd> &out) {
+    const int M = 2 * N, c = (N - 1) / 2;
+    out.assign((size_t)M * M, cd(0, 0));
+    for (int i = 0; i < N; ++i) {
+        const int ii = (M - c + i) % M;
+        for (int j = 0; j < N; ++j) out[(size_t)ii * M + (M - c + j) % M] = cd(P[(size_t)i * N + j], 0);
+    }
+    fft2(f, out, M, false);
+}
+
+// Inverse transform, 1/M^2 scaling and un-centring (ToTimeDomain, :243-250; numutil.h:214-226).
+void to_time(const FFT1 &f, std::vector<cd> &F, int N, std::vector<double> &out) {
+    const int M = 2 * N, c = (N - 1) / 2;
+    fft2(f, F, M, true);
+    const double s = 1.0 / ((double)M * (double)M);
+    out.assign((size_t)N * N, 0.0);
+    for (int i = 0; i < N; ++i) {
+        const int ii = (M - c + i) % M;
+        for (int j = 0; j < N; ++j) out[(size_t)i * N + j] = F[(size_t)ii * M + (M - c + j) % M].real() * s;
+    }
+}
+
+double kahan(const std::vector<double> &v) {  // numutil.h:236-246
+    double sum = 0, comp = 0;
+    for (double x : v) {
+        const double y = x - comp, t = sum + y;
+        comp = (t - sum) - y;
+        sum = t;
+    }
+    return sum;
+}
+
+// resample (MultipoleProfileCalculator.cpp:355-402)
+float resample_at(const std::vector<float> &d, const std::vector<float> &R, float dsq) {
+    const unsigned len = (unsigned)d.size();
+    if (dsq > d[len - 1]) return 0.f;
+    unsigned lo = 0, hi = len - 1;
+    float d2lo = d[lo];
+    if (lo + 32 < hi) {
+        float d2hi = d[hi];
+        do {
+            int m = (int)((dsq - d2lo) / (d2hi - d2lo) * (float)(hi - lo));
+            m = std::min(std::max(m, 0), (int)(hi - lo - 1));
+            const unsigned mid = (unsigned)m + lo;
+            const float d2mid = d[mid];
+            if (dsq > d2mid) {
+                lo = mid + 1;
+                d2lo = d[lo];
+            } else {
+                hi = mid;
+                d2hi = d2mid;
+            }
+        } while (lo + 32 < hi);
+    }
+    while (lo < hi && dsq > d2lo) d2lo = d[++lo];
+    if (!lo) return R[0];
+    float t = (dsq - d[lo - 1]) / (d[lo] - d[lo - 1]);
+    t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+    if (t != t) t = 0.5f;
+    return (1.f - t) * R[lo - 1] + t * R[lo];
+}
+
+unsigned round_up_pow2(unsigned v) {
+    v--;
+    v |= v >> 1; v |= v >> 2; v |= v >> 4; v |= v >> 8; v |= v >> 16;
+    return v + 1;
+}
+
+// One spectral channel (MultipoleProfileTask::Run, multipole.cpp:241-295)
+void channel_profile(const LayerParams &lp, int sc, int desired, bool lerp_thin, std::vector<float> &table,
+                     float &rcp, float &spacing, float &total) {
+    float mfp_total = 0.f;
+    for (int l = 0; l < 2; ++l) mfp_total += 1.f / (lp.mua[l][sc] + lp.musp[l][sc]);
+    const float mfp = mfp_total / (float)2;
+    const float step = 12.f * mfp / (float)desired;
+    const int length = (int)round_up_pow2((unsigned)desired);
+    const int N = 2 * length;
+    std::vector<double> R0, T0, R1, T1;
+    // MPC_ComputeDiffusionProfile, :294-314 (two layers)
+    layer_grid(lp.eta[0], lp.eta[0] / lp.eta[1], lp.thickness[0], lp.mua[0][sc], lp.musp[0][sc], step, lerp_thin, N,
+               R0, T0);
+    layer_grid(lp.eta[1] / lp.eta[0], lp.eta[1], lp.thickness[1], lp.mua[1][sc], lp.musp[1][sc], step, lerp_thin, N,
+               R1, T1);
+    {  // CombineLayerProfiles, :253-280: R12 = R1 + T1 R2 T1 / (1 - R2 R1)
+        FFT1 f(2 * N);
+        std::vector<cd> fR1, fR2, fT1, fT2;
+        to_freq(f, R0, N, fR1);
+        to_freq(f, R1, N, fR2);
+        to_freq(f, T0, N, fT1);
+        to_freq(f, T1, N, fT2);
+        T1.clear();
+        R1.clear();
+        std::vector<cd> fR12(fR1.size()), &fT12 = fT2;
+        for (size_t k = 0; k < fR1.size(); ++k) {
+            const cd one = cd(1, 0) - fR2[k] * fR1[k];
+            fR12[k] = fT1[k] * fR2[k] * fT1[k] / one + fR1[k];
+            fT12[k] = fT1[k] * fT2[k] / one;
+        }
+        fR1.clear(); fR2.clear(); fT1.clear();
+        to_time(f, fR12, N, R0);
+        to_time(f, fT12, N, T0);
+    }
+    // unique d^2 = (i^2 + j^2) step^2 entries, i <= j, first insertion wins (:316-330)
+    const unsigned c = (unsigned)length - 1, ext = c;
+    const float denorm = 1.f / (step * step);
+    std::vector<uint8_t> seen((size_t)ext * ext * 2 + 1, 0);
+    std::vector<std::pair<unsigned, float>> ents;
+    for (unsigned i = 0; i <= ext; ++i)
+        for (unsigned j = i; i * i + j * j <= ext * ext; ++j) {
+            const unsigned nsq = i * i + j * j;
+            if (seen[nsq]) continue;
+            seen[nsq] = 1;
+            ents.emplace_back(nsq, (float)R0[(size_t)(c + i) * N + (c + j)] * denorm);
+        }
+    std::sort(ents.begin(), ents.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::vector<float> d(ents.size()), r(ents.size());
+    for (size_t k = 0; k < ents.size(); ++k) {
+        d[k] = (float)ents[k].first * step * step;
+        r[k] = ents[k].second;
+    }
+    total = (float)kahan(R0);
+    // MPC_ResampleForUniformDistanceSquaredDistribution (:404-426), target = 2 * length
+    const unsigned tl = (unsigned)d.size() * 2;
+    const float extent = d.back();
+    table.resize(tl);
+    std::vector<float> nd(tl);
+    for (unsigned i = 0; i < tl; ++i) {
+        const float q = (float)i * extent / (float)(tl - 1);
+        nd[i] = q;
+        table[i] = resample_at(d, r, q);
+    }
+    spacing = nd[tl - 1] / (float)(tl - 1);   // multipole.cpp:274-275
+    rcp = (float)(tl - 1) / nd[tl - 1];
+}
+
+template <class F>
+void parallel_for(int n, int nthreads, F &&fn) {
+    if (nthreads <= 0) nthreads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::atomic<int> next{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::min(nthreads, n); ++t)
+        th.emplace_back([&] {
+            for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+        });
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+void build_profile(const LayerParams &lp, int desired_length, bool lerp_thin, ProfileTables &out, int nthreads) {
+    std::vector<std::vector<float>> tabs(NB);
+    parallel_for(NB, nthreads, [&](int sc) {
+        channel_profile(lp, sc, desired_length, lerp_thin, tabs[sc], out.rcp[sc], out.spacing[sc],
+                        out.total_reflectance[sc]);
+    });
+    out.length = (int)tabs[0].size();
+    for (int c = 1; c < NB; ++c)
+        if ((int)tabs[c].size() != out.length) throw Error(-2, "profile channel lengths differ");
+    out.table.resize((size_t)NB * out.length);
+    for (int c = 0; c < NB; ++c) memcpy(&out.table[(size_t)c * out.length], tabs[c].data(), sizeof(float) * out.length);
+}
+
+// ------------------------------------------------------------ rho_hd table
+namespace {
+constexpr float kPi = 3.14159265358979323846f;  // pbrt.h:196 (float)
+constexpr float kOneMinusEps = 0x1.fffffep-1f;  // montecarlo.h:48-50
+
+struct MT {  // MT19937 (core/rng.cpp)
+    uint32_t mt[624];
+    int i;
+    explicit MT(uint32_t s) {
+        mt[0] = s;
+        for (i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+    }
+    uint32_t next() {
+        if (i >= 624) {
+            for (int k = 0; k < 624; ++k) {
+                const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+                mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            i = 0;
+        }
+        uint32_t y = mt[i++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+    float uniform() { return (float)(next() & 0xffffff) / (float)(1 << 24); }
+};
+
+struct V3 { float x, y, z; };
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+struct Beckmann {
+    float rms2, rcp;
+    float D(V3 wh) const {  // reflection.h:514-521
+        const float ct = fabsf(wh.z), c2 = ct * ct, d = c2 * c2 * kPi;
+        if (d == 0.f) return 0.f;
+        return rcp * expf((c2 - 1) * rcp / c2) / d;
+    }
+};
+
+float fr_dielectric(float cosi, float ei, float et, bool fixed) {  // reflection.cpp:132-153; reflection.h:315-324
+    cosi = std::min(std::max(cosi, -1.f), 1.f);
+    if (!(cosi > 0.)) std::swap(ei, et);
+    const float sint = ei / et * sqrtf(std::max(0.f, 1.f - cosi * cosi));
+    float F;
+    if (sint >= 1.)
+        F = 1.f;
+    else {
+        const float cost = sqrtf(std::max(0.f, 1.f - sint * sint)), ci = fabsf(cosi);
+        const float par = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
+        const float per = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
+        F = (par * par + per * per) / 2.f;
+    }
+    if (fixed) F = F + F * (1.f - F) * (1.f - F);
+    return F;
+}
+
+struct MicrofacetR1 {  // Microfacet(R = 1, FresnelDielectric(1, eta), Beckmann)
+    Beckmann dist;
+    float eta;
+    bool fixed;
+    float G(V3 wo, V3 wi, V3 wh) const {
+        const float a = fabsf(wh.z), wowh = fabsf(dot(wo, wh));
+        return std::min(1.f, std::min(2.f * a * fabsf(wo.z) / wowh, 2.f * a * fabsf(wi.z) / wowh));
+    }
+    float f(V3 wo, V3 wi) const {  // reflection.cpp:228-240
+        const float co = fabsf(wo.z), ci = fabsf(wi.z);
+        if (ci == 0.f || co == 0.f) return 0.f;
+        V3 wh = {wi.x + wo.x, wi.y + wo.y, wi.z + wo.z};
+        if (wh.x == 0. && wh.y == 0. && wh.z == 0.) return 0.f;
+        const float inv = 1.f / sqrtf(wh.x * wh.x + wh.y * wh.y + wh.z * wh.z);
+        wh = {wh.x * inv, wh.y * inv, wh.z * inv};
+        const float F = fr_dielectric(dot(wi, wh), 1.f, eta, fixed);
+        return 1.f * dist.D(wh) * G(wo, wi, wh) * F / (4.f * ci * co);
+    }
+    float sample_f(V3 wo, V3 &wi, float u1, float u2, float &pdf) const {  // reflection.cpp:548-570, 391-397
+        const float th = atanf(sqrtf(-dist.rms2 * logf(1.f - u1)));
+        const float ct = cosf(th), st = sinf(th), phi = u2 * 2.f * kPi;
+        V3 wh = {st * cosf(phi), st * sinf(phi), ct};
+        if (!(wo.z * wh.z > 0.f)) wh = {-wh.x, -wh.y, -wh.z};
+        const float dw = dot(wo, wh);
+        wi = {-wo.x + 2.f * dw * wh.x, -wo.y + 2.f * dw * wh.y, -wo.z + 2.f * dw * wh.z};
+        float bp = dist.D(wh) * ct / (4.f * dot(wo, wh));
+        if (dot(wo, wh) <= 0.f || bp < 1e-20f) bp = 0.f;
+        pdf = bp;
+        if (!(wo.z * wi.z > 0.f)) return 0.f;
+        return f(wo, wi);
+    }
+};
+
+void stratified(std::vector<float> &s, int n, MT &rng) {  // montecarlo.cpp:158-168
+    s.resize((size_t)2 * n * n);
+    const float dx = 1.f / n;
+    float *p = s.data();
+    for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) {
+            const float jx = rng.uniform(), jy = rng.uniform();
+            *p++ = std::min((x + jx) * dx, kOneMinusEps);
+            *p++ = std::min((y + jy) * dx, kOneMinusEps);
+        }
+}
+
+struct Kahan {
+    float sum = 0.f, c = 0.f;
+    void add(float v) {
+        const float y = v - c, t = sum + y;
+        c = (t - sum) - y;
+        sum = t;
+    }
+};
+}  // namespace
+
+void build_rho_table(float roughness, float eta, bool fixed, int n_entries, int sqrt_samples, RhoTable &out,
+                     int nthreads) {
+    MicrofacetR1 bx;
+    const float rms = roughness < 1e-3f ? 1e-3f : roughness;
+    bx.dist.rms2 = rms * rms;
+    bx.dist.rcp = 1 / bx.dist.rms2;
+    bx.eta = eta;
+    bx.fixed = fixed;
+    out.hd.assign(n_entries, 0.f);
+    const int n = sqrt_samples * sqrt_samples;
+    parallel_for(n_entries, nthreads, [&](int id) {  // RhoTask::Run, multipole.cpp:506-518
+        MT rng((uint32_t)(6428263u * (uint32_t)id));
+        std::vector<float> s;
+        stratified(s, sqrt_samples, rng);
+        float ct = (float)id / (float)(n_entries - 1);
+        if (ct == 0.f) ct = 0.01f / (float)(n_entries - 1);
+        const float st = sqrtf(1 - ct * ct);
+        const V3 wo = {st * cosf(0.f), st * sinf(0.f), ct};
+        Kahan k;
+        for (int i = 0; i < n; ++i) {
+            V3 wi;
+            float pdf = 0.f;
+            const float f = bx.sample_f(wo, wi, s[2 * i], s[2 * i + 1], pdf);
+            if (pdf > 0.) k.add(f * fabsf(wi.z) / pdf);
+        }
+        out.hd[id] = k.sum / (float)n;
+    });
+    {  // ComputeRhoHHFromBxDF, multipole.cpp:466-480; BxDF::rho(n, s1, s2), reflection.cpp:637-652
+        MT rng(6428263u * 3u * 7u);
+        std::vector<float> s1, s2;
+        stratified(s1, sqrt_samples, rng);
+        stratified(s2, sqrt_samples, rng);
+        Kahan k;
+        for (int i = 0; i < n; ++i) {
+            const float z = s1[2 * i], r = sqrtf(std::max(0.f, 1.f - z * z)), phi = 2 * kPi * s1[2 * i + 1];
+            const V3 wo = {r * cosf(phi), r * sinf(phi), z};
+            V3 wi;
+            float pdf = 0.f;
+            const float f = bx.sample_f(wo, wi, s2[2 * i], s2[2 * i + 1], pdf);
+            if (pdf > 0.) k.add(f * fabsf(wi.z) * fabsf(wo.z) / (0.15915494309189533577f * pdf));
+        }
+        out.hh = k.sum / (kPi * n);
+    }
+}
+
+}  // namespace mpss

@@ -1,0 +1,47 @@
+// material.h -- LayeredSkin material preparation (host side).
+//
+// Follows the reference's parse-time precompute for `Material "layeredskin"`:
+//   CreateLayeredSkinMaterial / LayeredSkin::LayeredSkin  (src/materials/layeredskin.cpp:39-123, 222-262)
+//   SkinCoefficients                                       (src/materials/skincoeffs.h:38-158)
+//   ComputeMultipoleProfile -> MultipoleProfileTask::Run   (src/core/multipole.cpp:241-295, 371-406)
+//   MPC_ComputeDiffusionProfile + resample                 (MultipoleProfileCalculator.cpp:151-426)
+//   ComputeRhoDataFromBxDF                                 (src/core/multipole.cpp:466-549)
+// The product's Rd table is channel-major: table[c * length + k].
+#pragma once
+#include <vector>
+#include "common.h"
+
+namespace mpss {
+
+struct SkinParams {
+    float roughness = 0.4f, nmperunit = 100e6f;
+    float f_mel = 0.15f, f_eu = 1.f, f_blood = 0.002f, f_ohg = 0.3f;
+    float thickness_nm[2] = {0.25e6f, 20e6f};
+    float ior[2] = {1.4f, 1.4f};
+    int desired_length = 512;
+    bool lerp_on_thin_slab = true;
+    bool double_ref_sslf = false;
+};
+
+struct LayerParams {
+    float mua[2][NB], musp[2][NB], thickness[2], eta[2];
+};
+
+struct ProfileTables {
+    int length = 0;                   // entries per channel (resampled)
+    std::vector<float> table;         // [NB][length]
+    float rcp[NB], spacing[NB], total_reflectance[NB];
+};
+
+struct RhoTable {
+    std::vector<float> hd;  // [n] scalar rho_hd(cos theta) (all channels equal for this BxDF)
+    float hh = 0.f;
+};
+
+void skin_layer_params(const SkinParams &p, LayerParams &out);
+void build_profile(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
+                   int nthreads = 0);
+void build_rho_table(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
+                     RhoTable &out, int nthreads = 0);
+
+}  // namespace mpss

@@ -1,0 +1,29 @@
+// mo_kernel.h -- device-resident octree / profile and the Mo() gather launcher.
+#pragma once
+#include "common.h"
+#include "octree.h"
+
+namespace mpss {
+
+struct DeviceOctree {
+    DevBuf<NodeHdr> nodes;
+    DevBuf<float> node_et;
+    DevBuf<float4> pt_hdr;
+    DevBuf<float> pt_e;
+    int n_nodes = 0, n_points = 0, max_depth = 0;
+    void upload(const FlatOctree &t);
+};
+
+struct DeviceProfile {
+    DevBuf<float> table;  // [NB][L] channel-major
+    DevBuf<float> rcp;    // [NB]
+    int L = 0;
+    void upload(const float *table, int L, const float *rcp);
+};
+
+// queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
+// counters (nullable): per query {nodes entered, points evaluated}.
+void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream);
+
+}  // namespace mpss

@@ -1,0 +1,189 @@
+// mo_kernel.hip -- the Mo() hierarchical irradiance gather on CDNA4 (gfx950).
+//
+// Computes, for each query point p, SubsurfaceOctreeNode::Mo(octreeBounds, p, ...)
+// (reference src/integrators/diffusionutil.h:175-210) with the multipole profile
+// Rd(d^2) of MultipoleProfileData::reflectance (src/core/multipole.cpp:60-113).
+//
+// Mapping: one wave64 = two queries; each 32-lane half-wave owns one query and lane
+// c = lane & 31 owns spectral band c (30 bands, lanes 30/31 idle). The traversal is
+// stackless over the pre-order node array (skip pointers, octree.h), so control flow is
+// uniform inside a half-wave. Every node record and every spectral row is read by the
+// half-wave as one coalesced 128-B line (Et/E) plus one broadcast 64-B header.
+//
+// Summation order is the reference's recursion order: S[d][lane] in LDS holds the
+// running sum of the children of the open node at depth d-1; a finished subtree is
+// folded into its parent level on the way back up. With FP contraction disabled
+// (-ffp-contract=off) every product and sum rounds exactly as the reference's scalar
+// code, so the result is bit-identical to the CPU oracle.
+#include "mo_kernel.h"
+
+namespace mpss {
+
+namespace {
+
+struct MoArgs {
+    const NodeHdr *__restrict__ nodes;
+    const float *__restrict__ node_et;
+    const float4 *__restrict__ pt_hdr;
+    const float *__restrict__ pt_e;
+    const float *__restrict__ table;  // [NB][L]
+    const float *__restrict__ rcp;    // [NB]
+    const float *__restrict__ queries;  // q * 3
+    float *__restrict__ out;          // q * out_stride
+    int32_t *__restrict__ counters;   // optional: q * 2 (nodes entered, points evaluated)
+    int L, n_nodes, nq, out_stride;
+    float max_error;
+};
+
+// sampleProfile (multipole.cpp:60-73): f = d2 * rcp in float; 0 at/after the last entry.
+__device__ __forceinline__ bool rd_in_range(float f, float lm1) { return f < lm1; }
+
+__device__ __forceinline__ float rd_lerp(const float *__restrict__ tb, float f) {
+    const uint32_t s = (uint32_t)f;
+    const float t = f - (float)s;
+    const float a = tb[s], b = tb[s + 1];
+    return (1.f - t) * a + t * b;
+}
+
+template <int MAXD, bool COUNT>
+__global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
+    __shared__ float S[4][MAXD + 1][64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int c = lane & 31;
+    const int q = ((int)blockIdx.x * 4 + wave) * 2 + (lane >> 5);
+    const bool active = q < a.nq;
+    float (*St)[64] = S[wave];
+
+    float px = 0.f, py = 0.f, pz = 0.f;
+    if (active) {
+        px = a.queries[3 * (size_t)q];
+        py = a.queries[3 * (size_t)q + 1];
+        pz = a.queries[3 * (size_t)q + 2];
+    }
+    const float rcp = c < NB ? a.rcp[c] : INFINITY;
+    const float lm1 = (float)(a.L - 1);
+    const float *__restrict__ tb = a.table + (size_t)(c < NB ? c : 0) * a.L;
+
+    int node = active ? 0 : a.n_nodes;
+    int dlast = 0;
+    St[0][lane] = 0.f;
+    int n_nodes = 0, n_pts = 0;
+
+    while (node < a.n_nodes) {
+        const NodeHdr h = a.nodes[node];
+        const int d = h.depth;
+        while (dlast > d) {  // close finished subtrees (return from the recursion)
+            St[dlast - 1][lane] += St[dlast][lane];
+            --dlast;
+        }
+        int next = h.skip;
+        if (COUNT) ++n_nodes;
+        if (!(h.flags & NODE_BLACK)) {
+            const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
+            const float d2 = dx * dx + dy * dy + dz * dz;
+            const float dw = h.sum_area / d2;
+            const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
+                                pz >= h.bminz && pz <= h.bmaxz;
+            if (dw < a.max_error && !inside) {
+                const float f = d2 * rcp;
+                if (rd_in_range(f, lm1)) {
+                    const float rd = rd_lerp(tb, f);
+                    St[d][lane] += rd * a.node_et[(size_t)node * ROW + c];
+                }
+            } else if (h.leaf_first >= 0) {
+                float acc = 0.f;
+                for (int i = 0; i < h.leaf_count; ++i) {
+                    const int k = h.leaf_first + i;
+                    const float4 ph = a.pt_hdr[k];
+                    if (__builtin_signbit(ph.w)) continue;  // E is black
+                    if (COUNT) ++n_pts;
+                    const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
+                    const float f = (ex * ex + ey * ey + ez * ez) * rcp;
+                    if (rd_in_range(f, lm1)) {
+                        const float rd = rd_lerp(tb, f);
+                        acc += rd * a.pt_e[(size_t)k * ROW + c] * ph.w;
+                    }
+                }
+                St[d][lane] += acc;
+            } else {  // open the node: recurse into its children
+                next = node + 1;
+                St[d + 1][lane] = 0.f;
+                dlast = d + 1;
+            }
+        }
+        node = next;
+    }
+    while (dlast > 0) {
+        St[dlast - 1][lane] += St[dlast][lane];
+        --dlast;
+    }
+    if (active && c < NB) a.out[(size_t)q * a.out_stride + c] = St[0][lane];
+    if (COUNT && active && c == 0) {
+        a.counters[2 * (size_t)q] = n_nodes;
+        a.counters[2 * (size_t)q + 1] = n_pts;
+    }
+}
+
+template <int MAXD>
+void launch_t(const MoArgs &a, bool count, hipStream_t s) {
+    const int waves = (a.nq + 1) / 2;
+    const int blocks = (waves + 3) / 4;
+    if (blocks == 0) return;
+    if (count)
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, true>), dim3(blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, false>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+void DeviceOctree::upload(const FlatOctree &t) {
+    nodes.upload(t.hdr.data(), t.hdr.size());
+    node_et.upload(t.node_et.data(), t.node_et.size());
+    pt_hdr.upload(reinterpret_cast<const float4 *>(t.pt_hdr.data()), t.pt_hdr.size() / 4);
+    pt_e.upload(t.pt_e.data(), t.pt_e.size());
+    n_nodes = (int)t.hdr.size();
+    n_points = (int)t.pt_index.size();
+    max_depth = t.max_depth;
+}
+
+void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
+    table.upload(tab, (size_t)NB * len);
+    rcp.upload(rcp_, NB);
+    L = len;
+}
+
+void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (t.n_nodes <= 0) throw Error(-1, "launch_mo_gather: octree is empty");
+    if (p.L < 2) throw Error(-1, "launch_mo_gather: profile table has fewer than 2 entries");
+    MoArgs a;
+    a.nodes = t.nodes.ptr;
+    a.node_et = t.node_et.ptr;
+    a.pt_hdr = t.pt_hdr.ptr;
+    a.pt_e = t.pt_e.ptr;
+    a.table = p.table.ptr;
+    a.rcp = p.rcp.ptr;
+    a.queries = queries;
+    a.out = out;
+    a.counters = counters;
+    a.L = p.L;
+    a.n_nodes = t.n_nodes;
+    a.nq = nq;
+    a.out_stride = out_stride;
+    a.max_error = max_error;
+    const bool count = counters != nullptr;
+    if (t.max_depth < 16)
+        launch_t<16>(a, count, stream);
+    else if (t.max_depth < 32)
+        launch_t<32>(a, count, stream);
+    else if (t.max_depth < 64)
+        launch_t<64>(a, count, stream);
+    else
+        throw Error(-2, "octree deeper than 63 levels is not supported by the gather kernel");
+    MPSS_HIP(hipGetLastError());
+}
+
+}  // namespace mpss

@@ -1,0 +1,229 @@
+// mpss_abi.cpp -- the extern "C" boundary of libmpss (include/mpss.h).
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mpss.h"
+#include "context.h"
+
+using namespace mpss;
+
+namespace {
+thread_local std::string g_last_error;
+
+template <class F>
+int guarded(F &&fn) {
+    try {
+        fn();
+        return MPSS_OK;
+    } catch (const Error &e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_last_error = "out of memory";
+        return MPSS_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+        return MPSS_ERR_INTERNAL;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return MPSS_ERR_INTERNAL;
+    }
+}
+
+void require(bool ok, const char *msg) {
+    if (!ok) throw Error(MPSS_ERR_INVALID, msg);
+}
+}  // namespace
+
+extern "C" {
+
+int mpss_abi_version(void) { return 1; }
+const char *mpss_last_error(void) { return g_last_error.c_str(); }
+
+void mpss_config_defaults(mpss_config *c) {
+    if (!c) return;
+    c->device = 0;
+    c->max_depth = 5;
+    c->max_error = .05f;
+    c->min_sample_distance = .25f;
+    c->mix = .5f;
+    c->show_irradiance_points = 0;
+    c->incenter = 0;
+    c->quick_render = 0;
+}
+
+int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
+    return guarded([&] {
+        require(cfg && out, "mpss_create: null argument");
+        *out = nullptr;
+        auto ctx = std::make_unique<Context>(*cfg);
+        *out = reinterpret_cast<mpss_ctx *>(ctx.release());
+    });
+}
+
+void mpss_destroy(mpss_ctx *ctx) { delete reinterpret_cast<Context *>(ctx); }
+
+void mpss_layeredskin_defaults(mpss_layeredskin *m) {
+    if (!m) return;
+    m->roughness = 0.4f;
+    m->nmperunit = 100e6f;
+    m->f_mel = 0.15f;
+    m->f_eu = 1.f;
+    m->f_blood = 0.002f;
+    m->f_ohg = 0.3f;
+    m->ga_epi = 0.9f;
+    m->ga_derm = 0.8f;
+    m->b_derm = 0.4f;
+    m->layer_thickness_nm[0] = 0.25e6f;
+    m->layer_thickness_nm[1] = 20e6f;
+    m->layer_ior[0] = m->layer_ior[1] = 1.4f;
+    for (int i = 0; i < MPSS_NBANDS; ++i) m->albedo[i] = 1.f;
+    m->desired_length = 512;
+    m->lerp_on_thin_slab = 1;
+    m->double_ref_sslf = 0;
+}
+
+int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {
+    return guarded([&] {
+        require(c && m && id, "mpss_add_layeredskin: null argument");
+        require(m->desired_length >= 2 && m->desired_length <= 4096, "desiredlength out of range [2, 4096]");
+        require(m->nmperunit > 0.f, "nmperunit must be positive");
+        *id = reinterpret_cast<Context *>(c)->add_layeredskin(*m);
+    });
+}
+
+int mpss_set_material_tables(mpss_ctx *c, const float *rd, uint32_t len, const float *rcp, const float *rho,
+                             uint32_t n_rho, const float *albedo, int is_mc, uint32_t *id) {
+    return guarded([&] {
+        require(c && rd && rcp && rho && id, "mpss_set_material_tables: null argument");
+        require(len >= 2 && n_rho >= 2, "tables need at least 2 entries");
+        *id = reinterpret_cast<Context *>(c)->set_material_tables(rd, len, rcp, rho, n_rho, albedo, is_mc != 0);
+    });
+}
+
+int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len, float *rcp, float *rho,
+                             uint32_t *n_rho, float *total) {
+    return guarded([&] {
+        require(c && len && n_rho, "mpss_get_material_tables: null argument");
+        const Material &m = reinterpret_cast<Context *>(c)->material(id);
+        *len = (uint32_t)m.profile.length;
+        *n_rho = (uint32_t)m.rho.hd.size();
+        if (rd) memcpy(rd, m.profile.table.data(), sizeof(float) * m.profile.table.size());
+        if (rcp) memcpy(rcp, m.profile.rcp, sizeof(float) * NB);
+        if (rho) memcpy(rho, m.rho.hd.data(), sizeof(float) * m.rho.hd.size());
+        if (total) memcpy(total, m.profile.total_reflectance, sizeof(float) * NB);
+    });
+}
+
+int mpss_set_irradiance_points(mpss_ctx *c, uint32_t n, const float *p, const float *nrm, const float *E,
+                               const float *area) {
+    return guarded([&] {
+        require(c && p && nrm && E && area, "mpss_set_irradiance_points: null argument");
+        require(n > 0, "mpss_set_irradiance_points: empty point set");
+        reinterpret_cast<Context *>(c)->set_irradiance_points((int)n, p, nrm, E, area);
+    });
+}
+
+int mpss_octree_info(mpss_ctx *c, uint32_t *nn, uint32_t *md, uint32_t *np) {
+    return guarded([&] {
+        require(c, "mpss_octree_info: null ctx");
+        const DeviceOctree &t = reinterpret_cast<Context *>(c)->octree();
+        if (nn) *nn = (uint32_t)t.n_nodes;
+        if (md) *md = (uint32_t)t.max_depth;
+        if (np) *np = (uint32_t)t.n_points;
+    });
+}
+
+int mpss_mo_batch(mpss_ctx *c, uint32_t id, uint32_t q, const float *p_dev, float *mo_dev, int32_t *counters_dev,
+                  void *stream) {
+    return guarded([&] {
+        require(c && (q == 0 || (p_dev && mo_dev)), "mpss_mo_batch: null argument");
+        Context &ctx = *reinterpret_cast<Context *>(c);
+        const Material &m = ctx.material(id);
+        launch_mo_gather(ctx.octree(), m.dev_profile, ctx.max_error(), (int)q, p_dev, mo_dev, NB, counters_dev,
+                         (hipStream_t)stream);
+    });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- host-side utilities
+extern "C" {
+
+int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta) {
+    return guarded([&] {
+        require(m && mua && musp && thickness && eta, "mpss_host_skin_layers: null argument");
+        SkinParams sp;
+        sp.roughness = m->roughness;
+        sp.nmperunit = m->nmperunit;
+        sp.f_mel = m->f_mel;
+        sp.f_eu = m->f_eu;
+        sp.f_blood = m->f_blood;
+        sp.f_ohg = m->f_ohg;
+        for (int l = 0; l < 2; ++l) {
+            sp.thickness_nm[l] = m->layer_thickness_nm[l];
+            sp.ior[l] = m->layer_ior[l];
+        }
+        LayerParams lp;
+        skin_layer_params(sp, lp);
+        memcpy(mua, lp.mua, sizeof(lp.mua));
+        memcpy(musp, lp.musp, sizeof(lp.musp));
+        memcpy(thickness, lp.thickness, sizeof(lp.thickness));
+        memcpy(eta, lp.eta, sizeof(lp.eta));
+    });
+}
+
+int mpss_host_build_profile(const float *mua, const float *musp, const float *thickness, const float *eta,
+                            int desired_length, int lerp, float *rd, uint32_t *length, float *rcp, float *total) {
+    return guarded([&] {
+        require(mua && musp && thickness && eta && length, "mpss_host_build_profile: null argument");
+        require(desired_length >= 2 && desired_length <= 4096, "desired_length out of range");
+        LayerParams lp;
+        memcpy(lp.mua, mua, sizeof(lp.mua));
+        memcpy(lp.musp, musp, sizeof(lp.musp));
+        memcpy(lp.thickness, thickness, sizeof(lp.thickness));
+        memcpy(lp.eta, eta, sizeof(lp.eta));
+        ProfileTables pt;
+        build_profile(lp, desired_length, lerp != 0, pt);
+        *length = (uint32_t)pt.length;
+        if (rd) memcpy(rd, pt.table.data(), sizeof(float) * pt.table.size());
+        if (rcp) memcpy(rcp, pt.rcp, sizeof(pt.rcp));
+        if (total) memcpy(total, pt.total_reflectance, sizeof(pt.total_reflectance));
+    });
+}
+
+int mpss_host_rho_table(float roughness, float eta, int fixed, int n, int sq, float *hd, float *hh) {
+    return guarded([&] {
+        require(hd && n >= 2 && sq >= 1, "mpss_host_rho_table: bad argument");
+        RhoTable rt;
+        build_rho_table(roughness, eta, fixed != 0, n, sq, rt);
+        memcpy(hd, rt.hd.data(), sizeof(float) * n);
+        if (hh) *hh = rt.hh;
+    });
+}
+
+int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
+                            uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,
+                            int32_t *skip, int32_t *leaf_first, int32_t *leaf_count, int32_t *order) {
+    return guarded([&] {
+        require(p && nrm && E && area && n_nodes && n > 0, "mpss_host_octree_export: bad argument");
+        FlatOctree t;
+        build_octree((int)n, p, nrm, E, area, t);
+        *n_nodes = (uint32_t)t.hdr.size();
+        for (size_t i = 0; i < t.hdr.size(); ++i) {
+            const NodeHdr &h = t.hdr[i];
+            if (node_p) { node_p[3 * i] = h.px; node_p[3 * i + 1] = h.py; node_p[3 * i + 2] = h.pz; }
+            if (node_area) node_area[i] = h.sum_area;
+            if (node_et) memcpy(node_et + i * NB, &t.node_et[i * ROW], sizeof(float) * NB);
+            if (depth) depth[i] = h.depth;
+            if (skip) skip[i] = h.skip;
+            if (leaf_first) leaf_first[i] = h.leaf_first;
+            if (leaf_count) leaf_count[i] = h.leaf_count;
+        }
+        if (order) memcpy(order, t.pt_index.data(), sizeof(int32_t) * t.pt_index.size());
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,211 @@
+"""mpss -- Python host binding of libmpss (the MI355X-native multipole subsurface path).
+
+Thin ctypes layer over the C ABI in include/mpss.h.  Device buffers are passed as raw
+HIP pointers (torch CUDA tensors' ``data_ptr()``); torch is plumbing here, not the product.
+The HIP library is mandatory: importing this module raises if libmpss.so is missing, and
+there is no CPU fallback anywhere in the product path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+NB = 30
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmpss.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("libmpss.so not built (%s): run __graft_entry__.build() or make -C pbrt-v2-skin_amd/csrc"
+                      % LIB_PATH)
+
+_lib = C.CDLL(LIB_PATH)
+
+f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+vp = C.c_void_p
+u32 = C.c_uint32
+u32p = C.POINTER(C.c_uint32)
+
+
+class Config(C.Structure):
+    """mpss_config (CreateMultipoleSubsurfaceIntegrator params, multipolesubsurface.cpp:393-401)."""
+    _fields_ = [("device", C.c_int), ("max_depth", C.c_int), ("max_error", C.c_float),
+                ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
+                ("incenter", C.c_int), ("quick_render", C.c_int)]
+
+
+class LayeredSkin(C.Structure):
+    """mpss_layeredskin (CreateLayeredSkinMaterial params, layeredskin.cpp:234-257)."""
+    _fields_ = [("roughness", C.c_float), ("nmperunit", C.c_float), ("f_mel", C.c_float), ("f_eu", C.c_float),
+                ("f_blood", C.c_float), ("f_ohg", C.c_float), ("ga_epi", C.c_float), ("ga_derm", C.c_float),
+                ("b_derm", C.c_float), ("layer_thickness_nm", C.c_float * 2), ("layer_ior", C.c_float * 2),
+                ("albedo", C.c_float * NB), ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
+                ("double_ref_sslf", C.c_int)]
+
+
+def _sig(name, res, args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+_sig("mpss_abi_version", C.c_int, [])
+_sig("mpss_last_error", C.c_char_p, [])
+_sig("mpss_config_defaults", None, [C.POINTER(Config)])
+_sig("mpss_create", C.c_int, [C.POINTER(Config), C.POINTER(vp)])
+_sig("mpss_destroy", None, [vp])
+_sig("mpss_layeredskin_defaults", None, [C.POINTER(LayeredSkin)])
+_sig("mpss_add_layeredskin", C.c_int, [vp, C.POINTER(LayeredSkin), u32p])
+_sig("mpss_set_material_tables", C.c_int, [vp, f32p, u32, f32p, f32p, u32, vp, C.c_int, u32p])
+_sig("mpss_get_material_tables", C.c_int, [vp, u32, vp, u32p, vp, vp, u32p, vp])
+_sig("mpss_set_irradiance_points", C.c_int, [vp, u32, f32p, f32p, f32p, f32p])
+_sig("mpss_octree_info", C.c_int, [vp, u32p, u32p, u32p])
+_sig("mpss_mo_batch", C.c_int, [vp, u32, u32, vp, vp, vp, vp])
+_sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
+_sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
+_sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
+_sig("mpss_host_octree_export", C.c_int, [u32, f32p, f32p, f32p, f32p, u32p] + [vp] * 8)
+
+
+class MpssError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        raise MpssError("libmpss error %d: %s" % (rc, _lib.mpss_last_error().decode()))
+
+
+def lib():
+    return _lib
+
+
+def exported_symbols():
+    """Names declared in include/mpss.h (checked by tests/test_abi.py)."""
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "mpss.h")
+    txt = open(hdr).read()
+    return sorted(set(re.findall(r"\b(mpss_[a-z0-9_]+)\s*\(", txt)))
+
+
+def default_config(**kw):
+    c = Config()
+    _lib.mpss_config_defaults(C.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def default_skin(**kw):
+    m = LayeredSkin()
+    _lib.mpss_layeredskin_defaults(C.byref(m))
+    for k, v in kw.items():
+        if k in ("layer_thickness_nm", "layer_ior"):
+            setattr(m, k, (C.c_float * 2)(*v))
+        elif k == "albedo":
+            setattr(m, k, (C.c_float * NB)(*v))
+        else:
+            setattr(m, k, v)
+    return m
+
+
+# ------------------------------------------------------------------ host utilities
+def host_skin_layers(skin):
+    mua = np.zeros((2, NB), np.float32)
+    musp = np.zeros((2, NB), np.float32)
+    th = np.zeros(2, np.float32)
+    eta = np.zeros(2, np.float32)
+    check(_lib.mpss_host_skin_layers(C.byref(skin), mua, musp, th, eta))
+    return mua, musp, th, eta
+
+
+def host_build_profile(mua, musp, thickness, eta, desired_length=512, lerp=True):
+    args = [np.ascontiguousarray(x, np.float32) for x in (mua, musp, thickness, eta)]
+    n = C.c_uint32()
+    check(_lib.mpss_host_build_profile(*args, desired_length, int(lerp), None, C.byref(n), None, None))
+    # the length query above ran the whole build; run once more into buffers
+    tab = np.zeros((NB, n.value), np.float32)
+    rcp = np.zeros(NB, np.float32)
+    tot = np.zeros(NB, np.float32)
+    check(_lib.mpss_host_build_profile(*args, desired_length, int(lerp), tab.ctypes.data, C.byref(n),
+                                       rcp.ctypes.data, tot.ctypes.data))
+    return tab, rcp, tot
+
+
+def host_rho_table(roughness, eta, n=1025, sqrt_samples=256, double_ref_sslf=False):
+    hd = np.zeros(n, np.float32)
+    hh = C.c_float()
+    check(_lib.mpss_host_rho_table(roughness, eta, int(double_ref_sslf), n, sqrt_samples, hd, C.byref(hh)))
+    return hd, hh.value
+
+
+def host_octree_export(p, n, E, area):
+    p, n, E, area = [np.ascontiguousarray(x, np.float32) for x in (p, n, E, area)]
+    nn = C.c_uint32()
+    check(_lib.mpss_host_octree_export(len(p), p, n, E, area, C.byref(nn), *([None] * 8)))
+    N = nn.value
+    d = dict(p=np.zeros((N, 3), np.float32), area=np.zeros(N, np.float32), Et=np.zeros((N, NB), np.float32),
+             depth=np.zeros(N, np.int32), skip=np.zeros(N, np.int32), leaf_first=np.zeros(N, np.int32),
+             leaf_count=np.zeros(N, np.int32), order=np.zeros(len(p), np.int32))
+    check(_lib.mpss_host_octree_export(len(p), p, n, E, area, C.byref(nn),
+                                       *[d[k].ctypes.data for k in ("p", "area", "Et", "depth", "skip",
+                                                                    "leaf_first", "leaf_count", "order")]))
+    return d
+
+
+# ------------------------------------------------------------------ device context
+class Context:
+    """One MultipoleSubsurfaceIntegrator instance (multipolesubsurface.h:36-80) on one GPU."""
+
+    def __init__(self, **cfg):
+        self.cfg = default_config(**cfg)
+        h = vp()
+        check(_lib.mpss_create(C.byref(self.cfg), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.mpss_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def add_layeredskin(self, skin):
+        mid = C.c_uint32()
+        check(_lib.mpss_add_layeredskin(self.h, C.byref(skin), C.byref(mid)))
+        return mid.value
+
+    def set_material_tables(self, table, rcp, rho_hd, albedo=None, is_mc=False):
+        table = np.ascontiguousarray(table, np.float32)
+        al = None if albedo is None else np.ascontiguousarray(albedo, np.float32)
+        mid = C.c_uint32()
+        check(_lib.mpss_set_material_tables(self.h, table, table.shape[1], np.ascontiguousarray(rcp, np.float32),
+                                            np.ascontiguousarray(rho_hd, np.float32), len(rho_hd),
+                                            None if al is None else al.ctypes.data, int(is_mc), C.byref(mid)))
+        return mid.value
+
+    def material_tables(self, mid):
+        L = C.c_uint32()
+        nr = C.c_uint32()
+        check(_lib.mpss_get_material_tables(self.h, mid, None, C.byref(L), None, None, C.byref(nr), None))
+        tab = np.zeros((NB, L.value), np.float32)
+        rcp = np.zeros(NB, np.float32)
+        rho = np.zeros(nr.value, np.float32)
+        tot = np.zeros(NB, np.float32)
+        check(_lib.mpss_get_material_tables(self.h, mid, tab.ctypes.data, C.byref(L), rcp.ctypes.data,
+                                            rho.ctypes.data, C.byref(nr), tot.ctypes.data))
+        return tab, rcp, rho, tot
+
+    def set_irradiance_points(self, p, n, E, area):
+        p, n, E, area = [np.ascontiguousarray(x, np.float32) for x in (p, n, E, area)]
+        check(_lib.mpss_set_irradiance_points(self.h, len(p), p, n, E, area))
+
+    def octree_info(self):
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(_lib.mpss_octree_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return dict(n_nodes=a.value, max_depth=b.value, n_points=c.value)
+
+    def mo_batch(self, mid, q, p_dev, mo_dev, counters_dev=None, stream=None):
+        check(_lib.mpss_mo_batch(self.h, mid, q, p_dev, mo_dev, counters_dev, stream))

@@ -1,0 +1,45 @@
+"""Seeded synthetic inputs shared by the parity tests and bench.py."""
+import numpy as np
+
+NB = 30
+
+
+def smooth_spectra(n, seed=1, black_frac=0.0):
+    """E_c = s * (0.5 + 0.5 sin(0.1 c + phi)), s ~ U[0,1)."""
+    rng = np.random.default_rng(seed)
+    s = rng.random(n, dtype=np.float32)
+    phi = rng.random(n, dtype=np.float32) * np.float32(6.2831853)
+    c = np.arange(NB, dtype=np.float32)
+    E = (s[:, None] * (np.float32(0.5) + np.float32(0.5) * np.sin(np.float32(0.1) * c[None, :] + phi[:, None])))
+    E = E.astype(np.float32)
+    if black_frac > 0:
+        E[rng.random(n) < black_frac] = 0.0
+    return E
+
+
+def ellipsoid_cloud(n, radii=(0.25, 0.3, 0.35), seed=7, black_frac=0.05):
+    """Irradiance points on an ellipsoid surface: p, n, E, area."""
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal((n, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    r = np.asarray(radii)
+    p = (v * r).astype(np.float32)
+    nrm = v / (r * r)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    area_total = 4 * np.pi * (np.prod(r) ** (2 / 3))
+    area = np.full(n, area_total / n, np.float32) * (0.5 + rng.random(n).astype(np.float32))
+    return p, nrm.astype(np.float32), smooth_spectra(n, seed + 1, black_frac), area.astype(np.float32)
+
+
+def surface_queries(q, radii=(0.25, 0.3, 0.35), seed=11, jitter=0.0, sort=True):
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal((q, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    p = v * np.asarray(radii)
+    if jitter:
+        p += rng.standard_normal((q, 3)) * jitter
+    p = p.astype(np.float32)
+    if sort:  # neighbouring queries in a wave take similar octree paths (camera-sample order)
+        key = np.lexsort((np.round(p[:, 2] * 64), np.round(p[:, 1] * 64), np.round(p[:, 0] * 8)))
+        p = p[key]
+    return np.ascontiguousarray(p)

@@ -1,0 +1,119 @@
+"""Mo() gather on the GPU (libmpss HIP kernel) vs the CPU oracle: bit-exact.
+
+The kernel follows the reference recursion's summation order (diffusionutil.h:175-210) and
+rounds every product/sum like the scalar code, so equality is exact, not a tolerance.
+Counters (octree nodes entered, leaf points evaluated) must match the oracle's
+instrumented recursion too (they feed the algorithmic-bytes figure).
+"""
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+RADII = (0.25, 0.3, 0.35)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def skin_profile(oracle):
+    mua, musp, th, eta = oracle.skin_layers(0.3, 40e6, 0.5, 0.5, 0.5, 0.5, (0.25e6, 20e6), (1.4, 1.4))
+    tab, rcp, _, _ = oracle.compute_profile(mua, musp, eta, th, desired_length=512)
+    return tab, rcp
+
+
+@pytest.fixture(scope="module")
+def wide_profile():
+    """A synthetic smooth profile whose extent spans many octree levels (stresses Rd lookups)."""
+    L = 4096
+    x = np.linspace(0, 1, L, dtype=np.float32)
+    tab = np.stack([(np.exp(-x * (4 + 0.2 * c)) * (1 + 0.01 * c)).astype(np.float32) for c in range(30)])
+    rcp = np.array([(L - 1) / (0.004 * (1 + 0.03 * c)) for c in range(30)], np.float32)
+    return tab, rcp
+
+
+def run_gpu(mpss, torch, cloud, table, rcp, q, max_error):
+    p, n, E, area = cloud
+    ctx = mpss.Context(max_error=max_error)
+    mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
+    ctx.set_irradiance_points(p, n, E, area)
+    qd = torch.from_numpy(q).cuda()
+    out = torch.zeros((len(q), 30), dtype=torch.float32, device="cuda")
+    cnt = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+    ctx.mo_batch(mid, len(q), qd.data_ptr(), out.data_ptr(), cnt.data_ptr())
+    torch.cuda.synchronize()
+    mo_plain = torch.zeros_like(out)
+    ctx.mo_batch(mid, len(q), qd.data_ptr(), mo_plain.data_ptr())
+    torch.cuda.synchronize()
+    info = ctx.octree_info()
+    ctx.close()
+    return out.cpu().numpy(), cnt.cpu().numpy(), mo_plain.cpu().numpy(), info
+
+
+@pytest.mark.parametrize("max_error", [0.05, 0.1, 0.5])
+def test_mo_bit_exact_skin_profile(oracle, mpss, torch_dev, skin_profile, max_error):
+    cloud = synth.ellipsoid_cloud(200000, radii=RADII, seed=7, black_frac=0.05)
+    q = synth.surface_queries(6000, radii=RADII, seed=13)
+    table, rcp = skin_profile
+    mo, cnt, mo_plain, info = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error)
+    t = oracle.Octree(*cloud)
+    ref, nn, npt = t.mo(q, table, rcp, max_error, counters=True)
+    assert info["n_nodes"] == t.num_nodes()
+    assert np.array_equal(mo, ref)
+    assert np.array_equal(mo_plain, ref)  # the counting variant changes nothing
+    assert np.array_equal(cnt[:, 0], nn) and np.array_equal(cnt[:, 1], npt)
+    assert np.any(ref > 0)
+
+
+@pytest.mark.parametrize("jitter", [0.0, 0.01])
+def test_mo_bit_exact_wide_profile(oracle, mpss, torch_dev, wide_profile, jitter):
+    cloud = synth.ellipsoid_cloud(50000, radii=RADII, seed=17, black_frac=0.1)
+    q = synth.surface_queries(4001, radii=RADII, seed=19, jitter=jitter)  # odd count: half-wave tail
+    table, rcp = wide_profile
+    mo, cnt, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1)
+    ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.1, counters=True)
+    assert np.array_equal(mo, ref)
+    assert np.array_equal(cnt[:, 0], nn) and np.array_equal(cnt[:, 1], npt)
+    assert (ref > 0).mean() > 0.5
+
+
+def test_mo_edge_cases(oracle, mpss, torch_dev, wide_profile):
+    table, rcp = wide_profile
+    # tiny clouds: single point, exactly 8 points (one leaf), 9 points (first split)
+    for npts in (1, 8, 9, 100):
+        cloud = synth.ellipsoid_cloud(npts, radii=(0.002, 0.002, 0.002), seed=npts, black_frac=0.0)
+        q = np.concatenate([synth.surface_queries(63, radii=(0.002, 0.002, 0.002), seed=5, sort=False),
+                            cloud[0][:1],                        # query exactly on a point (d2 = 0)
+                            np.float32([[10.0, 10.0, 10.0]])])   # far outside every node
+        mo, cnt, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, np.ascontiguousarray(q), 0.05)
+        ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.05, counters=True)
+        assert np.array_equal(mo, ref), npts
+        assert np.array_equal(cnt[:, 0], nn)
+    # all-black cloud: root is black, Mo = 0 after one node visit
+    p, n, E, area = synth.ellipsoid_cloud(64, seed=3)
+    mo, cnt, _, _ = run_gpu(mpss, torch_dev, (p, n, np.zeros_like(E), area), table, rcp,
+                            synth.surface_queries(16, seed=2), 0.05)
+    assert np.all(mo == 0) and np.all(cnt[:, 0] == 1)
+
+
+def test_layeredskin_material_on_device(oracle, mpss, torch_dev):
+    """mpss_add_layeredskin builds the tables itself; they must match the oracle's."""
+    ctx = mpss.Context(max_error=0.1)
+    skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5,
+                             desired_length=64)
+    mid = ctx.add_layeredskin(skin)
+    tab, rcp, rho, tot = ctx.material_tables(mid)
+    ctx.close()
+    mua, musp, th, eta = oracle.skin_layers(0.3, 40e6, 0.5, 0.5, 0.5, 0.5, (0.25e6, 20e6), (1.4, 1.4))
+    tab_o, rcp_o, _, tot_o = oracle.compute_profile(mua, musp, eta, th, desired_length=64)
+    assert np.array_equal(rcp, rcp_o)
+    assert np.abs(tab - tab_o).max() <= 1e-6 * np.abs(tab_o).max()
+    hd_o, _ = oracle.rho_table(0.3, 1.4)
+    assert np.array_equal(rho, hd_o)
