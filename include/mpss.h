@@ -97,7 +97,8 @@ int mpss_set_irradiance_points(mpss_ctx *ctx, uint32_t n, const float *p, const 
 int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint32_t *n_points);
 
 /* Mo for q shading points (p_dev: q*3 floats) with material's Rd profile; mo_dev: q*30 floats.
- * counters_dev (nullable): q*2 int32 {octree nodes entered, leaf points evaluated}. */
+ * counters_dev (nullable): q*4 int32 {nodes entered, leaf points evaluated} by the reference
+ * recursion, then the same two counts for the kernel's exactly-pruned traversal. */
 int mpss_mo_batch(mpss_ctx *ctx, uint32_t material_id, uint32_t q, const float *p_dev, float *mo_dev,
                   int32_t *counters_dev, void *stream);
 

@@ -17,12 +17,14 @@ struct DeviceOctree {
 struct DeviceProfile {
     DevBuf<float> table;  // [NB][L] channel-major
     DevBuf<float> rcp;    // [NB]
+    float rcp_min = 0.f;  // min over bands (exact subtree pruning, mo_kernel.hip)
     int L = 0;
     void upload(const float *table, int L, const float *rcp);
 };
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
-// counters (nullable): per query {nodes entered, points evaluated}.
+// counters (nullable, q*4 int32): per query {reference-traversal nodes entered, points evaluated,
+// pruned-kernel nodes entered, points evaluated}.
 void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
                       float *out, int out_stride, int32_t *counters, hipStream_t stream);
 

@@ -15,6 +15,14 @@
 // folded into its parent level on the way back up. With FP contraction disabled
 // (-ffp-contract=off) every product and sum rounds exactly as the reference's scalar
 // code, so the result is bit-identical to the CPU oracle.
+//
+// Exact pruning: sampleProfile returns exactly 0 once d^2 * rcpDsqSpacing >= L-1
+// (multipole.cpp:63-66). Every point of a subtree and its clusters' centroids lie inside the
+// node's box, so if the box's squared distance to p times the smallest rcp over bands is past
+// L-1 (with a 1e-4 relative margin that dominates float rounding of the two distances), the
+// whole subtree adds only +0 terms in the reference and is skipped here without changing a
+// bit of the result. The COUNT variant reports both the reference traversal's visits and the
+// pruned traversal's visits (SURVEY.md 8d counters).
 #include "mo_kernel.h"
 
 namespace mpss {
@@ -26,23 +34,28 @@ struct MoArgs {
     const float *__restrict__ node_et;
     const float4 *__restrict__ pt_hdr;
     const float *__restrict__ pt_e;
-    const float *__restrict__ table;  // [NB][L]
-    const float *__restrict__ rcp;    // [NB]
+    const float *__restrict__ table;    // [NB][L]
+    const float *__restrict__ rcp;      // [NB]
     const float *__restrict__ queries;  // q * 3
-    float *__restrict__ out;          // q * out_stride
-    int32_t *__restrict__ counters;   // optional: q * 2 (nodes entered, points evaluated)
+    float *__restrict__ out;            // q * out_stride
+    int32_t *__restrict__ counters;     // COUNT: q * 4
     int L, n_nodes, nq, out_stride;
-    float max_error;
+    float max_error, prune_f;           // prune when d2box * rcp_min >= prune_f
+    float rcp_min;
 };
-
-// sampleProfile (multipole.cpp:60-73): f = d2 * rcp in float; 0 at/after the last entry.
-__device__ __forceinline__ bool rd_in_range(float f, float lm1) { return f < lm1; }
 
 __device__ __forceinline__ float rd_lerp(const float *__restrict__ tb, float f) {
     const uint32_t s = (uint32_t)f;
     const float t = f - (float)s;
     const float a = tb[s], b = tb[s + 1];
     return (1.f - t) * a + t * b;
+}
+
+__device__ __forceinline__ float box_d2(float px, float py, float pz, const NodeHdr &h) {
+    const float bx = fmaxf(fmaxf(h.bminx - px, px - h.bmaxx), 0.f);
+    const float by = fmaxf(fmaxf(h.bminy - py, py - h.bmaxy), 0.f);
+    const float bz = fmaxf(fmaxf(h.bminz - pz, pz - h.bmaxz), 0.f);
+    return bx * bx + by * by + bz * bz;
 }
 
 template <int MAXD, bool COUNT>
@@ -53,7 +66,7 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
     const int c = lane & 31;
     const int q = ((int)blockIdx.x * 4 + wave) * 2 + (lane >> 5);
     const bool active = q < a.nq;
-    float (*St)[64] = S[wave];
+    float(*St)[64] = S[wave];
 
     float px = 0.f, py = 0.f, pz = 0.f;
     if (active) {
@@ -68,7 +81,8 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
     int node = active ? 0 : a.n_nodes;
     int dlast = 0;
     St[0][lane] = 0.f;
-    int n_nodes = 0, n_pts = 0;
+    // COUNT: reference visits (no pruning) and pruned-kernel visits
+    int ref_nodes = 0, ref_pts = 0, k_nodes = 0, k_pts = 0, pruned_until = 0;
 
     while (node < a.n_nodes) {
         const NodeHdr h = a.nodes[node];
@@ -78,7 +92,17 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
             --dlast;
         }
         int next = h.skip;
-        if (COUNT) ++n_nodes;
+        const bool prune = box_d2(px, py, pz, h) * a.rcp_min >= a.prune_f;
+        if (COUNT) {
+            ++ref_nodes;
+            if (node >= pruned_until) {
+                ++k_nodes;
+                if (prune) pruned_until = h.skip;
+            }
+        } else if (prune) {
+            node = next;
+            continue;
+        }
         if (!(h.flags & NODE_BLACK)) {
             const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
             const float d2 = dx * dx + dy * dy + dz * dz;
@@ -87,23 +111,20 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
                                 pz >= h.bminz && pz <= h.bmaxz;
             if (dw < a.max_error && !inside) {
                 const float f = d2 * rcp;
-                if (rd_in_range(f, lm1)) {
-                    const float rd = rd_lerp(tb, f);
-                    St[d][lane] += rd * a.node_et[(size_t)node * ROW + c];
-                }
+                if (f < lm1) St[d][lane] += rd_lerp(tb, f) * a.node_et[(size_t)node * ROW + c];
             } else if (h.leaf_first >= 0) {
                 float acc = 0.f;
                 for (int i = 0; i < h.leaf_count; ++i) {
                     const int k = h.leaf_first + i;
                     const float4 ph = a.pt_hdr[k];
                     if (__builtin_signbit(ph.w)) continue;  // E is black
-                    if (COUNT) ++n_pts;
+                    if (COUNT) {
+                        ++ref_pts;
+                        if (node >= pruned_until) ++k_pts;
+                    }
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
                     const float f = (ex * ex + ey * ey + ez * ez) * rcp;
-                    if (rd_in_range(f, lm1)) {
-                        const float rd = rd_lerp(tb, f);
-                        acc += rd * a.pt_e[(size_t)k * ROW + c] * ph.w;
-                    }
+                    if (f < lm1) acc += rd_lerp(tb, f) * a.pt_e[(size_t)k * ROW + c] * ph.w;
                 }
                 St[d][lane] += acc;
             } else {  // open the node: recurse into its children
@@ -120,8 +141,8 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
     }
     if (active && c < NB) a.out[(size_t)q * a.out_stride + c] = St[0][lane];
     if (COUNT && active && c == 0) {
-        a.counters[2 * (size_t)q] = n_nodes;
-        a.counters[2 * (size_t)q + 1] = n_pts;
+        int4 v = {ref_nodes, ref_pts, k_nodes, k_pts};
+        reinterpret_cast<int4 *>(a.counters)[q] = v;
     }
 }
 
@@ -152,6 +173,8 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
     table.upload(tab, (size_t)NB * len);
     rcp.upload(rcp_, NB);
     L = len;
+    rcp_min = rcp_[0];
+    for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
 }
 
 void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
@@ -174,6 +197,8 @@ void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_e
     a.nq = nq;
     a.out_stride = out_stride;
     a.max_error = max_error;
+    a.rcp_min = p.rcp_min > 0.f ? p.rcp_min : 0.f;  // rcp_min <= 0 disables pruning
+    a.prune_f = (a.rcp_min > 0.f) ? (float)(p.L - 1) * 1.0001f : INFINITY;
     const bool count = counters != nullptr;
     if (t.max_depth < 16)
         launch_t<16>(a, count, stream);

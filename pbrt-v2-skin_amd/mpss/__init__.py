@@ -18,6 +18,14 @@ if not os.path.exists(LIB_PATH):
     raise ImportError("libmpss.so not built (%s): run __graft_entry__.build() or make -C pbrt-v2-skin_amd/csrc"
                       % LIB_PATH)
 
+# torch-ROCm ships its own libamdhip64/libhsa-runtime64 (same SONAME, different NEEDED spelling).
+# Loading libmpss first would pull /opt/rocm's runtime in beside torch's and leave two HSA
+# runtimes fighting over /dev/kfd; importing torch first makes libmpss bind to torch's copy.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pure C/ctypes use without torch: /opt/rocm's runtime is used
+    torch = None
+
 _lib = C.CDLL(LIB_PATH)
 
 f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")

@@ -46,7 +46,7 @@ def run_gpu(mpss, torch, cloud, table, rcp, q, max_error):
     ctx.set_irradiance_points(p, n, E, area)
     qd = torch.from_numpy(q).cuda()
     out = torch.zeros((len(q), 30), dtype=torch.float32, device="cuda")
-    cnt = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros((len(q), 4), dtype=torch.int32, device="cuda")
     ctx.mo_batch(mid, len(q), qd.data_ptr(), out.data_ptr(), cnt.data_ptr())
     torch.cuda.synchronize()
     mo_plain = torch.zeros_like(out)

@@ -45,7 +45,7 @@ def main():
     q = synth.surface_queries(args.queries, radii=radii, seed=13)
     qd = torch.from_numpy(q).cuda()
     out = torch.empty((len(q), 30), dtype=torch.float32, device="cuda")
-    cnt = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros((len(q), 4), dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream()
     ctx.mo_batch(mid, len(q), qd.data_ptr(), out.data_ptr(), cnt.data_ptr(), s.cuda_stream)
     torch.cuda.synchronize()
@@ -60,9 +60,12 @@ def main():
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) / 1e3)
     t = float(np.median(times))
-    algo = 136.0 * float(visits.sum())
+    algo = 136.0 * float(visits[2] + visits[3])      # pruned kernel traversal
+    algo_ref = 136.0 * float(visits[0] + visits[1])  # reference recursion (same result)
     res = dict(points=args.points, queries=args.queries, info=ctx.octree_info(),
-               nodes_per_query=float(visits[0]) / len(q), points_per_query=float(visits[1]) / len(q),
+               ref_nodes_per_query=float(visits[0]) / len(q), ref_points_per_query=float(visits[1]) / len(q),
+               nodes_per_query=float(visits[2]) / len(q), points_per_query=float(visits[3]) / len(q),
+               ref_equiv_GBps=algo_ref / t / 1e9,
                kernel_s=t, all_s=times, mqueries_per_s=len(q) / t / 1e6, algo_GBps=algo / t / 1e9,
                frac_of_8TBps=algo / t / 8e12, profile_build_s=t1 - t0, octree_build_s=t2 - t1,
                mo_mean=float(out.mean().item()))
