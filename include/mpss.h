@@ -56,6 +56,8 @@ typedef struct {
     int show_irradiance_points;/* "showirradiancepoints" = false */
     int incenter;              /* "incenter" = false */
     int quick_render;          /* PbrtOptions.quickRender: maxError *= 4, minDist *= 4 */
+    int exact_mo;              /* 1: Mo sums in the reference recursion order (bit-exact, slower);
+                                  0: packet kernel, same terms, one running sum per band (default) */
 } mpss_config;
 
 void mpss_config_defaults(mpss_config *cfg);
@@ -98,7 +100,7 @@ int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint
 
 /* Mo for q shading points (p_dev: q*3 floats) with material's Rd profile; mo_dev: q*30 floats.
  * counters_dev (nullable): q*4 int32 {nodes entered, leaf points evaluated} by the reference
- * recursion, then the same two counts for the kernel's exactly-pruned traversal. */
+ * recursion (exact_mo = 1 only; else 0), then the same two counts for the kernel's pruned traversal. */
 int mpss_mo_batch(mpss_ctx *ctx, uint32_t material_id, uint32_t q, const float *p_dev, float *mo_dev,
                   int32_t *counters_dev, void *stream);
 

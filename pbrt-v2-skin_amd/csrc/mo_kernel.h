@@ -16,6 +16,7 @@ struct DeviceOctree {
 
 struct DeviceProfile {
     DevBuf<float> table;  // [NB][L] channel-major
+    DevBuf<float2> pairs; // [NB][L] (T[s], T[s+1]) for the packet kernel
     DevBuf<float> rcp;    // [NB]
     float rcp_min = 0.f;  // min over bands (exact subtree pruning, mo_kernel.hip)
     int L = 0;
@@ -24,8 +25,9 @@ struct DeviceProfile {
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
 // counters (nullable, q*4 int32): per query {reference-traversal nodes entered, points evaluated,
-// pruned-kernel nodes entered, points evaluated}.
+// pruned-kernel nodes entered, points evaluated}. The packet kernel (exact=false)
+// reports only the last two (the first two are 0); exact=true follows the reference summation order.
 void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
-                      float *out, int out_stride, int32_t *counters, hipStream_t stream);
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream, bool exact);
 
 }  // namespace mpss

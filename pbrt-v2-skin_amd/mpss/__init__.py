@@ -39,7 +39,7 @@ class Config(C.Structure):
     """mpss_config (CreateMultipoleSubsurfaceIntegrator params, multipolesubsurface.cpp:393-401)."""
     _fields_ = [("device", C.c_int), ("max_depth", C.c_int), ("max_error", C.c_float),
                 ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
-                ("incenter", C.c_int), ("quick_render", C.c_int)]
+                ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int)]
 
 
 class LayeredSkin(C.Structure):

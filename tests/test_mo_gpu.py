@@ -4,6 +4,10 @@ The kernel follows the reference recursion's summation order (diffusionutil.h:17
 rounds every product/sum like the scalar code, so equality is exact, not a tolerance.
 Counters (octree nodes entered, leaf points evaluated) must match the oracle's
 instrumented recursion too (they feed the algorithmic-bytes figure).
+The default packet kernel (exact_mo=0) evaluates the same terms with one running sum per
+band; it is held to 2e-6 relative of the reference order (all terms are >= 0, so the
+reassociation error is bounded by n*eps of the result) and must visit exactly the same
+pruned node/point sets as the exact kernel.
 """
 import numpy as np
 import pytest
@@ -39,9 +43,9 @@ def wide_profile():
     return tab, rcp
 
 
-def run_gpu(mpss, torch, cloud, table, rcp, q, max_error):
+def run_gpu(mpss, torch, cloud, table, rcp, q, max_error, exact=True):
     p, n, E, area = cloud
-    ctx = mpss.Context(max_error=max_error)
+    ctx = mpss.Context(max_error=max_error, exact_mo=int(exact))
     mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
     ctx.set_irradiance_points(p, n, E, area)
     qd = torch.from_numpy(q).cuda()
@@ -117,3 +121,34 @@ def test_layeredskin_material_on_device(oracle, mpss, torch_dev):
     assert np.abs(tab - tab_o).max() <= 1e-6 * np.abs(tab_o).max()
     hd_o, _ = oracle.rho_table(0.3, 1.4)
     assert np.array_equal(rho, hd_o)
+
+
+def _rel_close(got, ref, tol):
+    scale = np.maximum(np.abs(ref), np.abs(ref).max(axis=1, keepdims=True) * 1e-3)
+    return np.all(np.abs(got - ref) <= tol * scale + 1e-30)
+
+
+@pytest.mark.parametrize("max_error", [0.05, 0.1])
+def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile, wide_profile, max_error):
+    for (table, rcp), npts in ((skin_profile, 200000), (wide_profile, 50000)):
+        cloud = synth.ellipsoid_cloud(npts, radii=RADII, seed=23, black_frac=0.05)
+        q = synth.surface_queries(6001, radii=RADII, seed=29)
+        fast, cnt_f, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=False)
+        exact, cnt_e, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=True)
+        ref = oracle.Octree(*cloud).mo(q, table, rcp, max_error)
+        assert np.array_equal(exact, ref)
+        assert _rel_close(fast, ref, 2e-6), np.abs(fast - ref).max()
+        assert np.array_equal(cnt_f[:, 2:], cnt_e[:, 2:])  # same pruned traversal per query
+        assert np.array_equal(fast == 0, ref == 0)
+
+
+def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
+    table, rcp = wide_profile
+    for npts in (1, 9, 100):
+        cloud = synth.ellipsoid_cloud(npts, radii=(0.002, 0.002, 0.002), seed=npts, black_frac=0.0)
+        q = np.ascontiguousarray(np.concatenate([
+            synth.surface_queries(61, radii=(0.002, 0.002, 0.002), seed=5, sort=False),
+            cloud[0][:1], np.float32([[10.0, 10.0, 10.0]])]))  # 63 queries: ragged last packet
+        fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, exact=False)
+        ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
+        assert _rel_close(fast, ref, 2e-6), npts
