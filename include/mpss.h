@@ -75,6 +75,9 @@ typedef struct {
     float layer_thickness_nm[2];        /* "skinlayer layers" thickness (nm) */
     float layer_ior[2];                 /* "skinlayer layers" ior */
     float albedo[MPSS_NBANDS];          /* constant "albedo" texture value (default Spectrum(1)) */
+    float Kr[MPSS_NBANDS];              /* "Kr" (default Spectrum(1)): Microfacet reflection */
+    float Kt[MPSS_NBANDS];              /* "Kt" (default Spectrum(1)); non-black is rejected for now
+                                           (MicrofacetTransmission not ported; skin scenes set [0 0 0]) */
     int desired_length;   /* "desiredlength" = 512 */
     int lerp_on_thin_slab;/* "lerponthinslab" = true */
     int double_ref_sslf;  /* "doublerefsslf" = false (FixedFresnelDielectric) */
@@ -103,6 +106,30 @@ int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint
  * recursion (exact_mo = 1 only; else 0), then the same two counts for the kernel's pruned traversal. */
 int mpss_mo_batch(mpss_ctx *ctx, uint32_t material_id, uint32_t q, const float *p_dev, float *mo_dev,
                   int32_t *counters_dev, void *stream);
+
+/* ---- scene slice of the per-pixel path (the renderer feeds pbrt's parsed scene through these) ---- */
+/* TriangleMesh (shapes/trianglemesh.cpp:43-73): P already in world space (the ctor's ObjectToWorld),
+ * N / S in object space (nullable), uv (nullable), o2w / w2o = ObjectToWorld and its inverse
+ * (row-major 4x4). */
+int mpss_add_mesh(mpss_ctx *ctx, uint32_t nverts, const float *P, const float *N, const float *S, const float *uv,
+                  uint32_t ntris, const int32_t *indices, const float *obj_to_world, const float *world_to_obj,
+                  int reverse_orientation, uint32_t material_id);
+/* AreaLightSource "area" + Shape "sphere" placed by a translation (lights/diffuse.cpp:45-67). */
+int mpss_add_sphere_light(mpss_ctx *ctx, const float *center, float radius, const float *Lemit, int nsamples);
+/* PerspectiveCamera (cameras/perspective.cpp): RasterToCamera and CameraToWorld, row-major 4x4. */
+int mpss_set_camera(mpss_ctx *ctx, const float *raster_to_camera, const float *camera_to_world, int xres, int yres);
+/* SurfacePoint records (44 B: p[3] n[3] u v materialId area rayEpsilon, renderers/surfacepoints.h:45-55),
+ * the "pointsfile" format; set before mpss_preprocess to skip tessellation. */
+int mpss_set_surface_points(mpss_ctx *ctx, uint32_t n, const void *records);
+int mpss_get_surface_points(mpss_ctx *ctx, void *records, uint32_t *n);
+/* Irradiance E[n][30] of the last Preprocess. */
+int mpss_get_irradiance(mpss_ctx *ctx, float *E, uint32_t *n);
+/* MultipoleSubsurfaceIntegrator::Preprocess: tessellation, irradiance (GPU), octree. */
+int mpss_preprocess(mpss_ctx *ctx, uint32_t seed);
+/* Render pixels [x0,x1) x [y0,y1) at spp samples per pixel; xyzw_dev receives
+ * (y1-y0)*(x1-x0) float4 {sum X, sum Y, sum Z, sum of filter weights} (ImageFilm::Pixel). */
+int mpss_render_tile(mpss_ctx *ctx, int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *xyzw_dev,
+                     void *stream);
 
 /* ---- host-side utilities (no HIP device needed): the product's own parse-time builders,
  * exposed so their results can be checked on a CPU-only machine. ---- */

@@ -48,6 +48,13 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
     build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
     memcpy(mat->albedo, m.albedo, sizeof(mat->albedo));
+    memcpy(mat->Kr, m.Kr, sizeof(mat->Kr));
+    for (int c = 0; c < NB; ++c)
+        if (m.Kt[c] != 0.f)
+            throw Error(MPSS_ERR_INVALID, "layeredskin: a non-black Kt (MicrofacetTransmission) is not supported yet");
+    mat->roughness = m.roughness;
+    mat->ior = m.layer_ior[0];
+    mat->double_ref_sslf = m.double_ref_sslf != 0;
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));
@@ -66,7 +73,10 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
         mat->profile.total_reflectance[c] = 0.f;
     }
     mat->rho.hd.assign(rho, rho + n_rho);
-    for (int c = 0; c < NB; ++c) mat->albedo[c] = albedo ? albedo[c] : 1.f;
+    for (int c = 0; c < NB; ++c) {
+        mat->albedo[c] = albedo ? albedo[c] : 1.f;
+        mat->Kr[c] = 1.f;
+    }
     mat->is_monte_carlo = is_mc;
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());

@@ -9,13 +9,19 @@
 #include "material.h"
 #include "mo_kernel.h"
 #include "octree.h"
+#include "scene.h"
 
 namespace mpss {
+
+struct RenderScene;
 
 struct Material {
     ProfileTables profile;
     RhoTable rho;
     float albedo[NB];
+    float Kr[NB];              // Microfacet reflectance (layeredskin "Kr"); Kt must be black
+    float roughness = 0.4f, ior = 1.4f;
+    bool double_ref_sslf = false;
     bool is_monte_carlo = false;
     DeviceProfile dev_profile;
     DevBuf<float> dev_rho;  // [n_rho]
@@ -34,8 +40,38 @@ public:
     float max_error() const { return max_error_; }
     const mpss_config &config() const { return cfg_; }
 
+    // scene + per-pixel path (render_host.cpp)
+    void add_mesh(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
+                  const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material);
+    void add_sphere_light(const float *c, float r, const float *Lemit, int nsamples);
+    void set_camera(const float *r2c, const float *c2w, int xres, int yres);
+    void set_surface_points(uint32_t n, const SurfacePoint *pts);
+    void preprocess(uint32_t seed);
+    void render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, hipStream_t stream);
+    const std::vector<SurfacePoint> &surface_points() const { return points_; }
+    const std::vector<float> &irradiance() const { return irradiance_; }
+    bool has_octree() const { return have_octree_; }
+
 private:
     void activate() const;
+    void upload_scene();
+    RenderScene render_scene() const;
+    int first_bssrdf_material() const;
+    SceneData scene_;
+    bool scene_dirty_ = true, have_points_ = false;
+    std::vector<SurfacePoint> points_;
+    std::vector<float> irradiance_;
+    DevBuf<BvhNode> d_bvh_;
+    DevBuf<TriRec> d_tris_;
+    DevBuf<int32_t> d_tri_mesh_, d_tri_local_;
+    std::vector<std::unique_ptr<DevBuf<float>>> d_mesh_bufs_;
+    DevBuf<struct RenderMesh> d_meshes_;
+    DevBuf<struct RenderLight> d_lights_;
+    DevBuf<struct RenderMaterial> d_materials_;
+    DevBuf<uint32_t> ws_flags_;
+    DevBuf<float4> ws_pq_;
+    DevBuf<float> ws_ld_, ws_xyz_;
+    int64_t ws_n_ = 0;
     mpss_config cfg_;
     float max_error_, min_dist_;
     std::vector<std::unique_ptr<Material>> materials_;

@@ -16,7 +16,6 @@ struct DeviceOctree {
 
 struct DeviceProfile {
     DevBuf<float> table;  // [NB][L] channel-major
-    DevBuf<float2> pairs; // [NB][L] (T[s], T[s+1]) for the packet kernel
     DevBuf<float> rcp;    // [NB]
     float rcp_min = 0.f;  // min over bands (exact subtree pruning, mo_kernel.hip)
     int L = 0;

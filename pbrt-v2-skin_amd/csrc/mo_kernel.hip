@@ -24,6 +24,7 @@
 // bit of the result. The COUNT variant reports both the reference traversal's visits and the
 // pruned traversal's visits (SURVEY.md 8d counters).
 #include "mo_kernel.h"
+#include "mo_packet.h"
 
 #include <vector>
 
@@ -158,111 +159,26 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
 // Per query the visited node set, the decisions and every product are those of the
 // reference; only the order of the final float additions differs (one running sum per
 // band instead of the recursion's per-level sums), so results agree with the reference
-// order to float reassociation (tests bound it at 2e-6 relative).
+// order to float reassociation (tests bound it at 2e-5 relative; north star: 1e-4).
 // ---------------------------------------------------------------------------------------
 template <bool COUNT>
-__global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, const float2 *__restrict__ pairs, int nblocks) {
-    // XCD-aware remap: consecutive logical blocks (neighbouring queries) share one XCD's L2
-    const int b = (int)blockIdx.x, xcd = b & 7, qn = nblocks >> 3, rn = nblocks & 7;
-    const int lb = (xcd < rn ? xcd * (qn + 1) : rn * (qn + 1) + (xcd - rn) * qn) + (b >> 3);
+__global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
+    const int lb = xcd_remap((int)blockIdx.x, nblocks);
     const int lane = threadIdx.x & 63;
-    const int g = lane >> 3;           // query slot in the packet
-    const int k = lane & 7;            // band group: bands 4k .. 4k+3
+    const int g = lane >> 3, k = lane & 7;
     const int q = (lb * 4 + (int)(threadIdx.x >> 6)) * 8 + g;
     const bool valid = q < a.nq;
-
     float px = 0.f, py = 0.f, pz = 0.f;
     if (valid) {
         px = a.queries[3 * (size_t)q];
         py = a.queries[3 * (size_t)q + 1];
         pz = a.queries[3 * (size_t)q + 2];
     }
-    float rcp[4];
-    const float2 *tb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = 4 * k + j;
-        rcp[j] = c < NB ? a.rcp[c] : INFINITY;
-        tb[j] = pairs + (size_t)(c < NB ? c : 0) * a.L;
-    }
-    const float lm1 = (float)(a.L - 1);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    int resume = valid ? 0 : 0x7fffffff;
-    int k_nodes = 0, k_pts = 0;
-
-    int node = 0;
-    while (node < a.n_nodes) {
-        node = __builtin_amdgcn_readfirstlane(node);
-        const NodeHdr h = a.nodes[node];
-        const int skip = h.skip;
-        bool open = false;
-        if (node >= resume) {
-            if (COUNT) ++k_nodes;
-            const bool prune = box_d2(px, py, pz, h) * a.rcp_min >= a.prune_f;
-            if (prune || (h.flags & NODE_BLACK)) {
-                resume = skip;
-            } else {
-                const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
-                const float d2 = dx * dx + dy * dy + dz * dz;
-                const float dw = h.sum_area / d2;
-                const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
-                                    pz >= h.bminz && pz <= h.bmaxz;
-                if (dw < a.max_error && !inside) {
-                    resume = skip;
-                    const float4 et = reinterpret_cast<const float4 *>(a.node_et + (size_t)node * ROW)[k];
-                    const float e[4] = {et.x, et.y, et.z, et.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float f = d2 * rcp[j];
-                        if (f < lm1) {
-                            const uint32_t s = (uint32_t)f;
-                            const float t = f - (float)s;
-                            const float2 ab = tb[j][s];
-                            acc[j] += ((1.f - t) * ab.x + t * ab.y) * e[j];
-                        }
-                    }
-                } else {
-                    open = true;  // leaf: evaluate points below; interior: descend
-                }
-            }
-        }
-        const bool any_open = __builtin_amdgcn_ballot_w64(open) != 0;
-        if (h.leaf_first >= 0) {
-            if (any_open) {
-                float lacc[4] = {0.f, 0.f, 0.f, 0.f};
-                for (int i = 0; i < h.leaf_count; ++i) {
-                    const int kp = h.leaf_first + i;
-                    const float4 ph = a.pt_hdr[kp];
-                    if (__builtin_signbit(ph.w)) continue;
-                    if (!open) continue;
-                    if (COUNT) ++k_pts;
-                    const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
-                    const float d2 = ex * ex + ey * ey + ez * ez;
-                    const float4 ev = reinterpret_cast<const float4 *>(a.pt_e + (size_t)kp * ROW)[k];
-                    const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float f = d2 * rcp[j];
-                        if (f < lm1) {
-                            const uint32_t s = (uint32_t)f;
-                            const float t = f - (float)s;
-                            const float2 ab = tb[j][s];
-                            lacc[j] += ((1.f - t) * ab.x + t * ab.y) * e[j] * ph.w;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += lacc[j];
-            }
-            if (open) resume = skip;
-            node = skip;
-        } else if (any_open) {
-            if (!open && node >= resume) resume = skip;
-            node = node + 1;
-        } else {
-            node = skip;
-        }
-    }
+    PacketTree t{a.nodes, a.node_et, a.pt_hdr, a.pt_e, a.table, a.rcp, a.L, a.n_nodes, a.max_error, a.prune_f,
+                 a.rcp_min};
+    float acc[4];
+    int kn = 0, kp = 0, un = 0;
+    mo_packet_traverse<COUNT>(t, px, py, pz, valid, k, acc, kn, kp, &un);
     if (valid) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -270,7 +186,7 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, const float2 *
             if (c < NB) a.out[(size_t)q * a.out_stride + c] = acc[j];
         }
         if (COUNT && k == 0) {
-            int4 v = {0, 0, k_nodes, k_pts};
+            int4 v = {un, 0, kn, kp};  // packet: wave (union) iterations, -, own nodes, own points
             reinterpret_cast<int4 *>(a.counters)[q] = v;
         }
     }
@@ -301,11 +217,6 @@ void DeviceOctree::upload(const FlatOctree &t) {
 
 void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
     table.upload(tab, (size_t)NB * len);
-    std::vector<float2> pr((size_t)NB * len);  // (T[s], T[s+1]): one 8-B gather per Rd lerp
-    for (int c = 0; c < NB; ++c)
-        for (int s = 0; s < len; ++s)
-            pr[(size_t)c * len + s] = make_float2(tab[(size_t)c * len + s], s + 1 < len ? tab[(size_t)c * len + s + 1] : 0.f);
-    pairs.upload(pr.data(), pr.size());
     rcp.upload(rcp_, NB);
     L = len;
     rcp_min = rcp_[0];
@@ -338,9 +249,9 @@ void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_e
     if (!exact) {
         const int packets = (nq + 7) / 8, blocks = (packets + 3) / 4;
         if (count)
-            hipLaunchKernelGGL((mo_packet_kernel<true>), dim3(blocks), dim3(256), 0, stream, a, p.pairs.ptr, blocks);
+            hipLaunchKernelGGL((mo_packet_kernel<true>), dim3(blocks), dim3(256), 0, stream, a, blocks);
         else
-            hipLaunchKernelGGL((mo_packet_kernel<false>), dim3(blocks), dim3(256), 0, stream, a, p.pairs.ptr, blocks);
+            hipLaunchKernelGGL((mo_packet_kernel<false>), dim3(blocks), dim3(256), 0, stream, a, blocks);
         MPSS_HIP(hipGetLastError());
         return;
     }

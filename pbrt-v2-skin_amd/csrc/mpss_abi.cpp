@@ -80,7 +80,7 @@ void mpss_layeredskin_defaults(mpss_layeredskin *m) {
     m->layer_thickness_nm[0] = 0.25e6f;
     m->layer_thickness_nm[1] = 20e6f;
     m->layer_ior[0] = m->layer_ior[1] = 1.4f;
-    for (int i = 0; i < MPSS_NBANDS; ++i) m->albedo[i] = 1.f;
+    for (int i = 0; i < MPSS_NBANDS; ++i) m->albedo[i] = m->Kr[i] = m->Kt[i] = 1.f;
     m->desired_length = 512;
     m->lerp_on_thin_slab = 1;
     m->double_ref_sslf = 0;
@@ -145,6 +145,67 @@ int mpss_mo_batch(mpss_ctx *c, uint32_t id, uint32_t q, const float *p_dev, floa
         const Material &m = ctx.material(id);
         launch_mo_gather(ctx.octree(), m.dev_profile, ctx.max_error(), (int)q, p_dev, mo_dev, NB, counters_dev,
                          (hipStream_t)stream, ctx.config().exact_mo != 0);
+    });
+}
+
+int mpss_add_mesh(mpss_ctx *c, uint32_t nv, const float *P, const float *N, const float *S, const float *uv,
+                  uint32_t nt, const int32_t *idx, const float *o2w, const float *w2o, int rev, uint32_t mat) {
+    return guarded([&] {
+        require(c && P && idx && o2w && w2o && nv > 0 && nt > 0, "mpss_add_mesh: bad argument");
+        reinterpret_cast<Context *>(c)->add_mesh(nv, P, N, S, uv, nt, idx, o2w, w2o, rev != 0, mat);
+    });
+}
+
+int mpss_add_sphere_light(mpss_ctx *c, const float *center, float r, const float *L, int ns) {
+    return guarded([&] {
+        require(c && center && L, "mpss_add_sphere_light: null argument");
+        reinterpret_cast<Context *>(c)->add_sphere_light(center, r, L, ns);
+    });
+}
+
+int mpss_set_camera(mpss_ctx *c, const float *r2c, const float *c2w, int xres, int yres) {
+    return guarded([&] {
+        require(c && r2c && c2w, "mpss_set_camera: null argument");
+        reinterpret_cast<Context *>(c)->set_camera(r2c, c2w, xres, yres);
+    });
+}
+
+int mpss_set_surface_points(mpss_ctx *c, uint32_t n, const void *rec) {
+    return guarded([&] {
+        require(c && (n == 0 || rec), "mpss_set_surface_points: null argument");
+        reinterpret_cast<Context *>(c)->set_surface_points(n, reinterpret_cast<const SurfacePoint *>(rec));
+    });
+}
+
+int mpss_get_surface_points(mpss_ctx *c, void *rec, uint32_t *n) {
+    return guarded([&] {
+        require(c && n, "mpss_get_surface_points: null argument");
+        const auto &v = reinterpret_cast<Context *>(c)->surface_points();
+        *n = (uint32_t)v.size();
+        if (rec) memcpy(rec, v.data(), sizeof(SurfacePoint) * v.size());
+    });
+}
+
+int mpss_get_irradiance(mpss_ctx *c, float *E, uint32_t *n) {
+    return guarded([&] {
+        require(c && n, "mpss_get_irradiance: null argument");
+        const auto &v = reinterpret_cast<Context *>(c)->irradiance();
+        *n = (uint32_t)(v.size() / NB);
+        if (E) memcpy(E, v.data(), sizeof(float) * v.size());
+    });
+}
+
+int mpss_preprocess(mpss_ctx *c, uint32_t seed) {
+    return guarded([&] {
+        require(c, "mpss_preprocess: null ctx");
+        reinterpret_cast<Context *>(c)->preprocess(seed);
+    });
+}
+
+int mpss_render_tile(mpss_ctx *c, int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, void *stream) {
+    return guarded([&] {
+        require(c && out, "mpss_render_tile: null argument");
+        reinterpret_cast<Context *>(c)->render_tile(spp, seed, x0, x1, y0, y1, out, (hipStream_t)stream);
     });
 }
 

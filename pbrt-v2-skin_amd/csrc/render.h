@@ -1,0 +1,78 @@
+// render.h -- device-side scene, sample records and the kernels of the per-pixel path
+// (render.hip), plus the host driver that uploads a SceneData and runs Preprocess / tiles.
+#pragma once
+#include <vector>
+
+#include "common.h"
+#include "geom.h"
+#include "mo_kernel.h"
+#include "mo_packet.h"
+#include "scene.h"
+
+namespace mpss {
+
+struct RenderMesh {
+    MeshView view;  // device pointers
+    uint32_t material;
+};
+
+struct RenderLight {
+    SphereView s;
+    float Lemit[NB];
+    int nsamples_pow2;   // RoundUpPow2(nSamples): IrradianceTask (file line 196)
+    int nsamples_round;  // LDSampler::RoundSize(nSamples): RequestSamples (file line 248)
+};
+
+struct RenderMaterial {
+    float R[NB];          // Kr (Microfacet reflectance), layeredskin.cpp:154-158
+    float alb_mix[NB];    // Pow(albedo, mix)      (IrradianceTask, file line 224)
+    float alb_1mmix[NB];  // Pow(albedo, 1 - mix)  (Li, file line 371)
+    Microfacet mf;
+    const float *rho;     // device rho_hd table
+    int n_rho, has_bssrdf, has_refl, is_mc;
+};
+
+struct RenderScene {
+    const BvhNode *bvh;
+    const TriRec *tris;
+    const int32_t *tri_mesh, *tri_local;
+    const RenderMesh *meshes;
+    const RenderLight *lights;
+    const RenderMaterial *materials;
+    int nlights, nmaterials, xres, yres;
+    float raster_to_camera[16], camera_to_world[16];
+};
+
+// A tile [x0,x1) x [y0,y1) extended by one column/row (ew x eh pixels) for samples that
+// land exactly on a pixel edge (film_kernel).
+struct TileBatch {
+    int x0, x1, y0, y1, ew, eh, spp;
+    uint32_t seed;
+    int64_t nsamples;  // ew * eh * spp
+};
+
+enum : uint32_t {
+    REC_LIVE = 1u,
+    REC_SURF = 2u,  // hit a mesh: Ld valid
+    REC_SSS = 4u,   // material has a MultipoleBSSRDF: pq valid
+    REC_LE = 8u,    // hit an area light's front face
+    REC_LIGHT_SHIFT = 8,
+    REC_MAT_SHIFT = 16
+};
+
+struct SampleRecs {
+    uint32_t *flags;
+    float4 *pq;   // p.xyz, cos(theta_o) at the shading point
+    float *ld;    // [n][ROW] UniformSampleAllLights result
+    float *xyz;   // [n][3]
+};
+
+__global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
+                                  const uint32_t *sp_mat, int n, uint32_t seed, float *E_out);
+__global__ void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
+__global__ void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples, int nblocks,
+                             int have_octree);
+__global__ void film_kernel(TileBatch tb, const uint32_t *flags, const float *xyz, float *out, int out_stride_px,
+                            int xres);
+
+}  // namespace mpss

@@ -1,0 +1,282 @@
+// render_host.cpp -- host driver of the per-pixel path: scene upload, Preprocess
+// (tessellation -> irradiance kernel -> octree) and tiled rendering (render.hip kernels).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "context.h"
+#include "render.h"
+#include "spectral.h"
+
+namespace mpss {
+
+namespace {
+int round_up_pow2(int v) {
+    int r = 1;
+    while (r < v) r <<= 1;
+    return r;
+}
+float det3(const float *m) {
+    return m[0] * (m[5] * m[10] - m[6] * m[9]) - m[1] * (m[4] * m[10] - m[6] * m[8]) +
+           m[2] * (m[4] * m[9] - m[5] * m[8]);
+}
+int bvh_depth(const std::vector<BvhNode> &n, int i) {
+    if (n[i].nprims > 0) return 1;
+    return 1 + std::max(bvh_depth(n, i + 1), bvh_depth(n, n[i].offset));
+}
+}  // namespace
+
+void Context::add_mesh(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
+                       const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material) {
+    if (material >= materials_.size()) throw Error(MPSS_ERR_INVALID, "add_mesh: unknown material id");
+    Mesh m;
+    m.P.assign(P, P + 3 * (size_t)nv);
+    if (N) m.N.assign(N, N + 3 * (size_t)nv);
+    if (S) m.S.assign(S, S + 3 * (size_t)nv);
+    if (uv) m.uv.assign(uv, uv + 2 * (size_t)nv);
+    m.idx.assign(idx, idx + 3 * (size_t)nt);
+    for (uint32_t i = 0; i < 3 * nt; ++i)
+        if (m.idx[i] < 0 || (uint32_t)m.idx[i] >= nv) throw Error(MPSS_ERR_INVALID, "add_mesh: vertex index out of range");
+    memcpy(m.o2w, o2w, sizeof(m.o2w));
+    memcpy(m.w2o, w2o, sizeof(m.w2o));
+    m.material = material;
+    m.reverse_orientation = reverse;
+    m.swaps_handedness = det3(o2w) < 0.f;  // Transform::SwapsHandedness
+    scene_.meshes.push_back(std::move(m));
+    scene_dirty_ = true;
+}
+
+void Context::add_sphere_light(const float *c, float r, const float *Lemit, int nsamples) {
+    if (!(r > 0.f)) throw Error(MPSS_ERR_INVALID, "add_sphere_light: radius must be positive");
+    if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_sphere_light: nsamples must be >= 1");
+    SphereLight l;
+    memcpy(l.center, c, sizeof(l.center));
+    l.radius = r;
+    memcpy(l.Lemit, Lemit, sizeof(l.Lemit));
+    l.nsamples = cfg_.quick_render ? std::max(1, nsamples / 4) : nsamples;  // CreateDiffuseAreaLight
+    scene_.lights.push_back(l);
+    scene_dirty_ = true;
+}
+
+void Context::set_camera(const float *r2c, const float *c2w, int xres, int yres) {
+    if (xres <= 0 || yres <= 0) throw Error(MPSS_ERR_INVALID, "set_camera: bad resolution");
+    memcpy(scene_.camera.raster_to_camera, r2c, sizeof(float) * 16);
+    memcpy(scene_.camera.camera_to_world, c2w, sizeof(float) * 16);
+    scene_.camera.xres = xres;
+    scene_.camera.yres = yres;
+    scene_dirty_ = true;
+}
+
+void Context::upload_scene() {
+    activate();
+    if (scene_.meshes.empty()) throw Error(MPSS_ERR_INVALID, "scene has no meshes");
+    build_bvh(scene_);
+    const int depth = bvh_depth(scene_.bvh, 0);
+    if (depth > 47) throw Error(MPSS_ERR_INTERNAL, "BVH deeper than the 48-entry traversal stack");
+    d_bvh_.upload(scene_.bvh.data(), scene_.bvh.size());
+    d_tris_.upload(scene_.tris.data(), scene_.tris.size());
+    d_tri_mesh_.upload(scene_.tri_mesh.data(), scene_.tri_mesh.size());
+    d_tri_local_.upload(scene_.tri_local.data(), scene_.tri_local.size());
+    d_mesh_bufs_.clear();
+    std::vector<RenderMesh> rm;
+    for (const Mesh &m : scene_.meshes) {
+        auto add = [&](const std::vector<float> &v) -> const float * {
+            if (v.empty()) return nullptr;
+            d_mesh_bufs_.emplace_back(new DevBuf<float>());
+            d_mesh_bufs_.back()->upload(v.data(), v.size());
+            return d_mesh_bufs_.back()->ptr;
+        };
+        RenderMesh r{};
+        r.view.P = add(m.P);
+        r.view.N = add(m.N);
+        r.view.S = add(m.S);
+        r.view.uv = add(m.uv);
+        std::vector<float> idxf(m.idx.size());
+        memcpy(idxf.data(), m.idx.data(), sizeof(int32_t) * m.idx.size());
+        r.view.idx = reinterpret_cast<const int32_t *>(add(idxf));
+        memcpy(r.view.o2w_store, m.o2w, sizeof(m.o2w));
+        memcpy(r.view.w2o_store, m.w2o, sizeof(m.w2o));
+        r.view.flip = (int)(m.reverse_orientation ^ m.swaps_handedness);
+        r.material = m.material;
+        rm.push_back(r);
+    }
+    // matrices live inside the device-side RenderMesh records; fix up their pointers there
+    d_meshes_.alloc(rm.size());
+    for (size_t i = 0; i < rm.size(); ++i) {
+        rm[i].view.o2w = reinterpret_cast<float *>(reinterpret_cast<char *>(d_meshes_.ptr + i) +
+                                                   offsetof(RenderMesh, view) + offsetof(MeshView, o2w_store));
+        rm[i].view.w2o = reinterpret_cast<float *>(reinterpret_cast<char *>(d_meshes_.ptr + i) +
+                                                   offsetof(RenderMesh, view) + offsetof(MeshView, w2o_store));
+    }
+    d_meshes_.upload(rm.data(), rm.size());
+    std::vector<RenderLight> rl;
+    for (const SphereLight &l : scene_.lights) {
+        RenderLight r{};
+        r.s.c = V3{l.center[0], l.center[1], l.center[2]};
+        r.s.r = l.radius;
+        r.s.phi_max = (kPiF / 180.f) * 360.f;   // Radians(Clamp(360, 0, 360))
+        r.s.theta_min = m_acos(-1.f);           // acosf(Clamp(zmin/radius))
+        r.s.theta_max = m_acos(1.f);
+        r.s.area = r.s.phi_max * l.radius * (l.radius - -l.radius);  // Sphere::Area
+        memcpy(r.Lemit, l.Lemit, sizeof(r.Lemit));
+        r.nsamples_pow2 = round_up_pow2(l.nsamples);
+        r.nsamples_round = round_up_pow2(l.nsamples);
+        rl.push_back(r);
+    }
+    d_lights_.upload(rl.data(), rl.size());
+    std::vector<RenderMaterial> rmat;
+    for (const auto &mp : materials_) {
+        const Material &m = *mp;
+        RenderMaterial r{};
+        memcpy(r.R, m.Kr, sizeof(r.R));
+        bool black = true;
+        for (int c = 0; c < NB; ++c) black = black && m.Kr[c] == 0.f;
+        r.has_refl = !black;
+        for (int c = 0; c < NB; ++c) {
+            r.alb_mix[c] = m_pow(m.albedo[c], cfg_.mix);
+            r.alb_1mmix[c] = m_pow(m.albedo[c], 1.f - cfg_.mix);
+        }
+        const float rough = m.roughness < 1e-3f ? 1e-3f : m.roughness;
+        r.mf.rms2 = rough * rough;
+        r.mf.rcp_rms2 = 1 / r.mf.rms2;
+        r.mf.eta = m.ior;
+        r.mf.fixed_fresnel = m.double_ref_sslf ? 1 : 0;
+        r.rho = m.dev_rho.ptr;
+        r.n_rho = (int)m.rho.hd.size();
+        r.has_bssrdf = 1;
+        r.is_mc = m.is_monte_carlo ? 1 : 0;
+        rmat.push_back(r);
+    }
+    d_materials_.upload(rmat.data(), rmat.size());
+    scene_dirty_ = false;
+}
+
+RenderScene Context::render_scene() const {
+    RenderScene sc{};
+    sc.bvh = d_bvh_.ptr;
+    sc.tris = d_tris_.ptr;
+    sc.tri_mesh = d_tri_mesh_.ptr;
+    sc.tri_local = d_tri_local_.ptr;
+    sc.meshes = d_meshes_.ptr;
+    sc.lights = d_lights_.ptr;
+    sc.materials = d_materials_.ptr;
+    sc.nlights = (int)scene_.lights.size();
+    sc.nmaterials = (int)materials_.size();
+    sc.xres = scene_.camera.xres;
+    sc.yres = scene_.camera.yres;
+    memcpy(sc.raster_to_camera, scene_.camera.raster_to_camera, sizeof(sc.raster_to_camera));
+    memcpy(sc.camera_to_world, scene_.camera.camera_to_world, sizeof(sc.camera_to_world));
+    return sc;
+}
+
+void Context::set_surface_points(uint32_t n, const SurfacePoint *pts) {
+    points_.assign(pts, pts + n);
+    have_points_ = n > 0;
+}
+
+// MultipoleSubsurfaceIntegrator::Preprocess (multipolesubsurface.cpp:254-322 [file lines])
+void Context::preprocess(uint32_t seed) {
+    if (scene_dirty_) upload_scene();
+    if (scene_.lights.empty()) {  // "if (scene->lights.size() == 0) return;" -> no octree, no SSS
+        have_octree_ = false;
+        irradiance_.clear();
+        return;
+    }
+    if (!have_points_) tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_);
+    const int n = (int)points_.size();
+    if (n == 0) throw Error(MPSS_ERR_INTERNAL, "tessellation produced no surface points");
+    std::vector<float> p(3 * (size_t)n), nr(3 * (size_t)n), eps(n);
+    std::vector<uint32_t> mat(n);
+    for (int i = 0; i < n; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            p[3 * (size_t)i + k] = points_[i].p[k];
+            nr[3 * (size_t)i + k] = points_[i].n[k];
+        }
+        eps[i] = points_[i].ray_eps;
+        mat[i] = points_[i].material;
+    }
+    DevBuf<float> dp, dn, de, dE;
+    DevBuf<uint32_t> dm;
+    dp.upload(p.data(), p.size());
+    dn.upload(nr.data(), nr.size());
+    de.upload(eps.data(), eps.size());
+    dm.upload(mat.data(), mat.size());
+    dE.alloc((size_t)n * NB);
+    const RenderScene sc = render_scene();
+    if (cfg_.show_irradiance_points) {  // IrradianceTask: red points instead of irradiance
+        const float red[3] = {1.f, 0.f, 0.f};
+        float s[NB];
+        spectrum_from_rgb(red, false, s);
+        irradiance_.resize((size_t)n * NB);
+        for (int i = 0; i < n; ++i) memcpy(&irradiance_[(size_t)i * NB], s, sizeof(s));
+    } else {
+        hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sc, dp.ptr, dn.ptr, de.ptr,
+                           dm.ptr, n, seed, dE.ptr);
+        MPSS_HIP(hipGetLastError());
+        irradiance_.resize((size_t)n * NB);
+        MPSS_HIP(hipMemcpy(irradiance_.data(), dE.ptr, sizeof(float) * irradiance_.size(), hipMemcpyDeviceToHost));
+    }
+    std::vector<float> area(n);
+    for (int i = 0; i < n; ++i) area[i] = points_[i].area;
+    set_irradiance_points(n, p.data(), nr.data(), irradiance_.data(), area.data());
+}
+
+// SamplerRenderer::Render restricted to the pixel rectangle [x0,x1) x [y0,y1)
+void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, hipStream_t stream) {
+    if (scene_dirty_) upload_scene();
+    const int W = scene_.camera.xres, H = scene_.camera.yres;
+    if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
+    if (spp < 1 || x0 < 0 || y0 < 0 || x1 > W || y1 > H || x0 >= x1 || y0 >= y1)
+        throw Error(MPSS_ERR_INVALID, "render_tile: bad rectangle or spp");
+    const int sss_mat = first_bssrdf_material();
+    PacketTree tree{};
+    int have_tree = 0;
+    if (have_octree_ && sss_mat >= 0) {
+        const Material &m = *materials_[sss_mat];
+        tree = PacketTree{dev_octree_.nodes.ptr, dev_octree_.node_et.ptr, dev_octree_.pt_hdr.ptr,
+                          dev_octree_.pt_e.ptr, m.dev_profile.table.ptr, m.dev_profile.rcp.ptr, m.dev_profile.L,
+                          dev_octree_.n_nodes, max_error_, (float)(m.dev_profile.L - 1) * 1.0001f,
+                          m.dev_profile.rcp_min};
+        have_tree = 1;
+    }
+    const RenderScene sc = render_scene();
+    const int tw = x1 - x0;
+    const int ew = tw + (x1 < W ? 1 : 0);
+    const int64_t max_samples = 1 << 21;
+    int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp));
+    for (int yb = y0; yb < y1; yb += rows) {
+        const int ye = std::min(y1, yb + rows);
+        TileBatch tb;
+        tb.x0 = x0;
+        tb.x1 = x1;
+        tb.y0 = yb;
+        tb.y1 = ye;
+        tb.ew = ew;
+        tb.eh = (ye - yb) + (ye < H ? 1 : 0);
+        tb.spp = spp;
+        tb.seed = seed;
+        tb.nsamples = (int64_t)tb.ew * tb.eh * spp;
+        if (ws_n_ < tb.nsamples) {
+            ws_flags_.alloc(tb.nsamples);
+            ws_pq_.alloc(tb.nsamples);
+            ws_ld_.alloc(tb.nsamples * ROW);
+            ws_xyz_.alloc(tb.nsamples * 3);
+            ws_n_ = tb.nsamples;
+        }
+        SampleRecs rec{ws_flags_.ptr, ws_pq_.ptr, ws_ld_.ptr, ws_xyz_.ptr};
+        hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
+                           sc, tb, rec);
+        const int64_t packets = (tb.nsamples + 7) / 8;
+        const int blocks = (int)((packets + 3) / 4);
+        hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples, blocks,
+                           have_tree);
+        const int npx = tw * (ye - yb);
+        hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, tb, ws_flags_.ptr,
+                           ws_xyz_.ptr, out + (size_t)(yb - y0) * tw * 4, tw, W);
+        MPSS_HIP(hipGetLastError());
+    }
+}
+
+int Context::first_bssrdf_material() const { return materials_.empty() ? -1 : 0; }
+
+}  // namespace mpss

@@ -1,0 +1,81 @@
+// scene.h -- the scene slice the multipole path needs (host side): triangle meshes in world
+// space, sphere area lights, perspective camera, the BVH over triangles, and the tessellated
+// SurfacePoint set (reference: shapes/trianglemesh.{cpp,inl}, shapes/sphere.cpp,
+// lights/diffuse.cpp, cameras/perspective.cpp, accelerators/bvh.cpp,
+// renderers/surfacepoints.cpp:301-369).
+#pragma once
+#include <vector>
+
+#include "common.h"
+#include "pbrt_math.h"
+
+namespace mpss {
+
+struct Mesh {
+    // world-space positions (TriangleMesh ctor applies ObjectToWorld, trianglemesh.cpp:43-73)
+    std::vector<float> P;        // nv*3
+    std::vector<float> N, S, uv; // object-space normals / tangents (nv*3), uv (nv*2); may be empty
+    std::vector<int32_t> idx;    // nt*3
+    float o2w[16], w2o[16];      // ObjectToWorld and its inverse (row-major)
+    uint32_t material = 0;
+    bool reverse_orientation = false, swaps_handedness = false;
+};
+
+struct SphereLight {  // AreaLightSource "area" on Shape "sphere" (translation-only placement)
+    float center[3], radius;
+    float Lemit[NB];
+    int nsamples;
+};
+
+struct Camera {
+    float raster_to_camera[16], camera_to_world[16];
+    int xres = 0, yres = 0;
+};
+
+// Linear BVH node (accelerators/bvh.cpp:113-123 layout): 32 B.
+struct alignas(16) BvhNode {
+    float bmin[3];
+    int32_t offset;  // leaf: first primitive; interior: second child index
+    float bmax[3];
+    uint16_t nprims;  // 0 for interior
+    uint16_t axis;
+};
+static_assert(sizeof(BvhNode) == 32, "BvhNode is 32 B");
+
+// Flattened triangle for the GPU: p1, e1 = p2-p1, e2 = p3-p1 (trianglemesh.inl:57-60) and its
+// global triangle id; 48 B.
+struct alignas(16) TriRec {
+    float p1[3];
+    int32_t tri;
+    float e1[3];
+    int32_t mesh;
+    float e2[3];
+    int32_t pad;
+};
+
+struct SceneData {
+    std::vector<Mesh> meshes;
+    std::vector<SphereLight> lights;
+    Camera camera;
+    // flattened (all meshes)
+    std::vector<int32_t> tri_mesh, tri_local;  // global tri -> mesh, local index
+    std::vector<BvhNode> bvh;
+    std::vector<TriRec> tris;  // in BVH leaf order
+};
+
+void build_bvh(SceneData &s);
+
+// SurfacePoint (renderers/surfacepoints.h:45-55): p, n, u, v, materialId, area, rayEpsilon.
+struct SurfacePoint {
+    float p[3], n[3], u, v;
+    uint32_t material;
+    float area, ray_eps;
+};
+static_assert(sizeof(SurfacePoint) == 44, "SurfacePoint matches the reference's 44-B pointsfile record");
+
+// TriangleMesh::TessellateSurfacePoints over every mesh in order (trianglemesh.cpp:187-257,
+// tessellator 265-318, matching 321-351; driver surfacepoints.cpp:301-333).
+void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter, std::vector<SurfacePoint> &out,
+                               int nthreads = 0);
+
+}  // namespace mpss

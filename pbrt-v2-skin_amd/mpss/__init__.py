@@ -47,7 +47,8 @@ class LayeredSkin(C.Structure):
     _fields_ = [("roughness", C.c_float), ("nmperunit", C.c_float), ("f_mel", C.c_float), ("f_eu", C.c_float),
                 ("f_blood", C.c_float), ("f_ohg", C.c_float), ("ga_epi", C.c_float), ("ga_derm", C.c_float),
                 ("b_derm", C.c_float), ("layer_thickness_nm", C.c_float * 2), ("layer_ior", C.c_float * 2),
-                ("albedo", C.c_float * NB), ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
+                ("albedo", C.c_float * NB), ("Kr", C.c_float * NB), ("Kt", C.c_float * NB),
+                ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
                 ("double_ref_sslf", C.c_int)]
 
 
@@ -70,6 +71,14 @@ _sig("mpss_get_material_tables", C.c_int, [vp, u32, vp, u32p, vp, vp, u32p, vp])
 _sig("mpss_set_irradiance_points", C.c_int, [vp, u32, f32p, f32p, f32p, f32p])
 _sig("mpss_octree_info", C.c_int, [vp, u32p, u32p, u32p])
 _sig("mpss_mo_batch", C.c_int, [vp, u32, u32, vp, vp, vp, vp])
+_sig("mpss_add_mesh", C.c_int, [vp, u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32])
+_sig("mpss_add_sphere_light", C.c_int, [vp, f32p, C.c_float, f32p, C.c_int])
+_sig("mpss_set_camera", C.c_int, [vp, f32p, f32p, C.c_int, C.c_int])
+_sig("mpss_set_surface_points", C.c_int, [vp, u32, vp])
+_sig("mpss_get_surface_points", C.c_int, [vp, vp, u32p])
+_sig("mpss_get_irradiance", C.c_int, [vp, vp, u32p])
+_sig("mpss_preprocess", C.c_int, [vp, u32])
+_sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
@@ -111,11 +120,17 @@ def default_skin(**kw):
     for k, v in kw.items():
         if k in ("layer_thickness_nm", "layer_ior"):
             setattr(m, k, (C.c_float * 2)(*v))
-        elif k == "albedo":
+        elif k in ("albedo", "Kr", "Kt"):
             setattr(m, k, (C.c_float * NB)(*v))
         else:
             setattr(m, k, v)
     return m
+
+
+# SurfacePoint record, the "pointsfile" format (renderers/surfacepoints.h:45-55), 44 B.
+SURFACE_POINT = np.dtype([("p", "<f4", 3), ("n", "<f4", 3), ("u", "<f4"), ("v", "<f4"), ("material", "<u4"),
+                          ("area", "<f4"), ("ray_eps", "<f4")])
+assert SURFACE_POINT.itemsize == 44
 
 
 # ------------------------------------------------------------------ host utilities
@@ -217,3 +232,46 @@ class Context:
 
     def mo_batch(self, mid, q, p_dev, mo_dev, counters_dev=None, stream=None):
         check(_lib.mpss_mo_batch(self.h, mid, q, p_dev, mo_dev, counters_dev, stream))
+
+    # ---- scene slice of the per-pixel path
+    def add_mesh(self, P, idx, o2w, w2o, material, N=None, S=None, uv=None, reverse=False):
+        P = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
+        idx = np.ascontiguousarray(idx, np.int32).reshape(-1, 3)
+        opt = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (N, S, uv)]
+        self._keep = opt
+        check(_lib.mpss_add_mesh(self.h, len(P), P, *[None if a is None else a.ctypes.data for a in opt],
+                                 len(idx), idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                 np.ascontiguousarray(o2w, np.float32), np.ascontiguousarray(w2o, np.float32),
+                                 int(reverse), material))
+
+    def add_sphere_light(self, center, radius, Lemit, nsamples=1):
+        check(_lib.mpss_add_sphere_light(self.h, np.ascontiguousarray(center, np.float32), radius,
+                                         np.ascontiguousarray(Lemit, np.float32), nsamples))
+
+    def set_camera(self, raster_to_camera, camera_to_world, xres, yres):
+        check(_lib.mpss_set_camera(self.h, np.ascontiguousarray(raster_to_camera, np.float32),
+                                   np.ascontiguousarray(camera_to_world, np.float32), xres, yres))
+
+    def set_surface_points(self, recs):
+        recs = np.ascontiguousarray(recs, SURFACE_POINT)
+        check(_lib.mpss_set_surface_points(self.h, len(recs), recs.ctypes.data))
+
+    def surface_points(self):
+        n = C.c_uint32()
+        check(_lib.mpss_get_surface_points(self.h, None, C.byref(n)))
+        out = np.zeros(n.value, SURFACE_POINT)
+        check(_lib.mpss_get_surface_points(self.h, out.ctypes.data, C.byref(n)))
+        return out
+
+    def irradiance(self):
+        n = C.c_uint32()
+        check(_lib.mpss_get_irradiance(self.h, None, C.byref(n)))
+        out = np.zeros((n.value, NB), np.float32)
+        check(_lib.mpss_get_irradiance(self.h, out.ctypes.data, C.byref(n)))
+        return out
+
+    def preprocess(self, seed=0):
+        check(_lib.mpss_preprocess(self.h, seed))
+
+    def render_tile(self, spp, seed, x0, x1, y0, y1, out_dev, stream=None):
+        check(_lib.mpss_render_tile(self.h, spp, seed, x0, x1, y0, y1, out_dev, stream))

@@ -39,7 +39,18 @@ def surface_queries(q, radii=(0.25, 0.3, 0.35), seed=11, jitter=0.0, sort=True):
     if jitter:
         p += rng.standard_normal((q, 3)) * jitter
     p = p.astype(np.float32)
-    if sort:  # neighbouring queries in a wave take similar octree paths (camera-sample order)
-        key = np.lexsort((np.round(p[:, 2] * 64), np.round(p[:, 1] * 64), np.round(p[:, 0] * 8)))
-        p = p[key]
+    if sort:  # Morton order: neighbouring queries share octree paths, like a pixel's samples
+        p = p[np.argsort(morton3(p), kind="stable")]
     return np.ascontiguousarray(p)
+
+
+def morton3(p, bits=10):
+    """30-bit Morton code of points quantised over their bounding box."""
+    lo = p.min(0)
+    span = np.maximum(p.max(0) - lo, 1e-30)
+    q = np.minimum(((p - lo) / span * (1 << bits)).astype(np.uint64), (1 << bits) - 1)
+    code = np.zeros(len(p), np.uint64)
+    for b in range(bits):
+        for a in range(3):
+            code |= ((q[:, a] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + a)
+    return code

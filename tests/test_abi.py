@@ -32,7 +32,7 @@ def test_defaults_match_reference_factories(mpss):
     # CreateLayeredSkinMaterial, layeredskin.cpp:234-257
     assert round(m.roughness, 6) == 0.4 and m.nmperunit == pytest.approx(100e6)
     assert m.desired_length == 512 and m.lerp_on_thin_slab == 1 and m.double_ref_sslf == 0
-    assert list(m.albedo) == [1.0] * 30
+    assert list(m.albedo) == [1.0] * 30 and list(m.Kr) == [1.0] * 30 and list(m.Kt) == [1.0] * 30
 
 
 def test_header_has_no_torch_types():

