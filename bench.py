@@ -1,0 +1,179 @@
+"""bench.py -- headline benchmark of the MI355X multipole skin path (BASELINE.json metric).
+
+A step = the pixel loop of one skin.pbrt frame per GPU (config C2: 1024x1024, 64 spp,
+MultipoleSubsurfaceIntegrator + LayeredSkin; SamplerRenderer::Render's task loop,
+samplerrenderer.cpp:177-236): every camera sample is traced, shaded (direct lighting + the
+Mo() octree gather) and splatted into the film. Frames are cut into 128x128 tiles dealt to
+ranks round-robin; rank 0 collects every rank's film tiles with one RCCL gather per step.
+Weak scaling: at N GPUs a step renders N frames (different sampler seeds).
+
+Preprocess (tessellation, irradiance kernel, octree build) runs once before timing and is
+reported separately, as SURVEY.md §8d prescribes.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-skin_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+MO_BYTES_PER_RECORD = 136  # position 12 + area 4 + 30-band E/Et 120
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"))
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--tile", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--out", default=None, help="write rank 0's first frame as .pfm/.exr")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != a.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (a.gpus, world))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mpss
+    from mpss import pbrtscene, tiles as tl
+
+    sc = pbrtscene.load(a.scene, xres=a.res, yres=a.res, spp=a.spp)
+    t0 = time.perf_counter()
+    ctx = pbrtscene.build_context(sc, device=local)
+    t_materials = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ctx.preprocess(seed=1)
+    torch.cuda.synchronize()
+    t_pre = time.perf_counter() - t0
+    n_points = ctx.octree_info()["n_points"] if ctx.surface_points().size else 0
+
+    frames = world                     # weak scaling: one frame's worth of work per GPU
+    T = a.tile
+    tiles = tl.tile_grid(sc.xres, sc.yres, T)
+    items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
+    items_by_rank = [[items_all[i] for i in tl.rank_items(len(items_all), r, world)] for r in range(world)]
+    mine = items_by_rank[rank]
+    slots = tl.slots_per_rank(len(items_all), world)
+    seeds = [a.seed + f for f in range(frames)]
+    out = torch.zeros((slots, T * T * 4), dtype=torch.float32, device="cuda")
+    gath = [torch.zeros_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        tl.render_items(ctx, mine, tiles, sc.spp, seeds, out, T, stream)
+        if world > 1:
+            dist.gather(out, gath if rank == 0 else None, dst=0)
+
+    # traversal-count pass (untimed): octree records the Mo gather reads for this workload
+    ctx.set_instrumentation(kernel_timing=False, count_traversal=True)
+    ctx.reset_render_stats()
+    tl.render_items(ctx, mine, tiles, sc.spp, seeds, out, T, stream)
+    cnt = ctx.render_stats()
+    ctx.set_instrumentation(kernel_timing=False, count_traversal=False)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ctx.set_instrumentation(kernel_timing=True, count_traversal=False)
+    ctx.reset_render_stats()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    st = ctx.render_stats()
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    samples_per_step = frames * sc.xres * sc.yres * sc.spp
+    value = samples_per_step * a.steps / dt / 1e6
+    # dominant kernel + Mo gather roofline (per-launch averages over the timed region)
+    kern = {"camera_direct": (st["ms_camera"], st["n_camera"]), "shade_mo": (st["ms_shade"], st["n_shade"]),
+            "film": (st["ms_film"], st["n_film"])}
+    dom = max(kern, key=lambda k: kern[k][0])
+    mo_bytes_step = MO_BYTES_PER_RECORD * (cnt["mo_nodes"] + cnt["mo_points"])   # this rank, one step
+    shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
+    launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
+    mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
+    roofline = {"kernel": "shade_kernel (Mo gather)", "bound": "hbm", "achieved": round(mo_gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(mo_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
+                "dominant_kernel": dom,
+                "kernel_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in kern.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(sc, ctx, a)
+
+    if rank == 0:
+        line = {"metric": "Msamples/s (skin.pbrt C2 pixel loop) + Mo()-gather HBM GB/s", "value": round(value, 3),
+                "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "f32", "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh)",
+                "config": {"workload": "skin.pbrt %dx%d %d spp per GPU (C2), %dx%d tiles, RCCL film gather"
+                           % (sc.xres, sc.yres, sc.spp, T, T), "frames_per_step": frames,
+                           "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
+                           "material_build_s": round(t_materials, 3),
+                           "mo_gbs": round(mo_gbs, 1), "mo_sss_samples": cnt["sss_samples"],
+                           "mo_records_per_sss_sample": round((cnt["mo_nodes"] + cnt["mo_points"]) /
+                                                              max(1, cnt["sss_samples"]), 2)},
+                "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if a.out and rank == 0:
+        from mpss import film
+        img = np.zeros((frames, sc.yres, sc.xres, 4), np.float32)
+        g = [x.cpu().numpy() for x in gath] if gath is not None else [out.cpu().numpy()]
+        tl.assemble(img, g, items_by_rank, tiles, T)
+        rgb = film.finalize(img[0])
+        (film.write_exr if a.out.endswith(".exr") else film.write_pfm)(a.out, rgb)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sc, ctx, a):
+    """The CPU restatement (oracle/, test infrastructure) timed on a bounded sample of the same
+    workload: whole tiles of the same frame, same points, same sampler, until the time budget is
+    spent. Reported as a baseline only; it never feeds `value`."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_render
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "unit": "Msamples/s", "cores": None, "kind": "port", "sample": "unavailable: %s" % e}
+    return oracle_render.time_cpu_baseline(sc, ctx, a.spp, a.seed, a.cpu_baseline_seconds)
+
+
+if __name__ == "__main__":
+    main()

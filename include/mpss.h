@@ -58,6 +58,8 @@ typedef struct {
     int quick_render;          /* PbrtOptions.quickRender: maxError *= 4, minDist *= 4 */
     int exact_mo;              /* 1: Mo sums in the reference recursion order (bit-exact, slower);
                                   0: packet kernel, same terms, one running sum per band (default) */
+    int kernel_timing;         /* 1: time every render kernel with HIP events (mpss_get_render_stats) */
+    int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
 } mpss_config;
 
 void mpss_config_defaults(mpss_config *cfg);
@@ -131,8 +133,26 @@ int mpss_preprocess(mpss_ctx *ctx, uint32_t seed);
 int mpss_render_tile(mpss_ctx *ctx, int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *xyzw_dev,
                      void *stream);
 
+/* Accumulated per-kernel statistics of mpss_render_tile / mpss_preprocess since the last reset.
+ * Kernel times need kernel_timing = 1; traversal counts need count_traversal = 1. Synchronizes. */
+typedef struct {
+    double ms_irradiance, ms_camera, ms_shade, ms_film;  /* summed kernel durations */
+    int64_t n_irradiance, n_camera, n_shade, n_film;     /* launches */
+    int64_t samples;      /* camera samples traced (incl. the tile's one-pixel border) */
+    int64_t sss_samples;  /* samples that evaluated Mo() */
+    int64_t mo_nodes;     /* octree nodes whose header/Et the shade kernel read (per sample) */
+    int64_t mo_points;    /* leaf points it evaluated */
+} mpss_render_stats;
+int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
+/* Switch kernel_timing / count_traversal after creation (instrumented passes). */
+int mpss_set_instrumentation(mpss_ctx *ctx, int kernel_timing, int count_traversal);
+int mpss_reset_render_stats(mpss_ctx *ctx);
+
 /* ---- host-side utilities (no HIP device needed): the product's own parse-time builders,
  * exposed so their results can be checked on a CPU-only machine. ---- */
+/* SampledSpectrum::FromRGB (spectrum.cpp:103-187); pbrt's "color"/"rgb" parameters use
+ * illuminant = 0 (ParamSet::AddRGBSpectrum, paramset.cpp:97-105). */
+int mpss_host_from_rgb(const float *rgb, int illuminant, float *out);
 /* LayeredSkin -> per-layer 30-band mua/musp [2][30], thickness[2], eta[2] (layeredskin.cpp:47-89). */
 int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta);
 /* Multipole profile from layer params; rd_table: [30][*length] (query *length with rd_table NULL). */

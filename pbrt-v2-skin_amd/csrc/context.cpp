@@ -22,6 +22,10 @@ Context::Context(const mpss_config &cfg) : cfg_(cfg) {
 
 Context::~Context() {
     (void)hipSetDevice(cfg_.device);
+    for (const Timed &t : timed_) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
 }
 
 void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }

@@ -51,6 +51,12 @@ public:
     const std::vector<SurfacePoint> &surface_points() const { return points_; }
     const std::vector<float> &irradiance() const { return irradiance_; }
     bool has_octree() const { return have_octree_; }
+    mpss_render_stats render_stats();
+    void reset_render_stats();
+    void set_instrumentation(bool timing, bool counting) {
+        cfg_.kernel_timing = timing;
+        cfg_.count_traversal = counting;
+    }
 
 private:
     void activate() const;
@@ -72,6 +78,16 @@ private:
     DevBuf<float4> ws_pq_;
     DevBuf<float> ws_ld_, ws_xyz_;
     int64_t ws_n_ = 0;
+    // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)
+    struct Timed {
+        hipEvent_t a, b;
+        int kind;
+    };
+    std::vector<Timed> timed_;
+    void time_begin(hipStream_t s, hipEvent_t &a);
+    void time_end(hipStream_t s, hipEvent_t a, int kind);
+    mpss_render_stats stats_{};
+    DevBuf<unsigned long long> d_counts_;  // [3]: sss samples, nodes, points
     mpss_config cfg_;
     float max_error_, min_dist_;
     std::vector<std::unique_ptr<Material>> materials_;

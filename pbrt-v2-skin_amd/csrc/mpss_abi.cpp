@@ -6,6 +6,7 @@
 
 #include "../../include/mpss.h"
 #include "context.h"
+#include "spectral.h"
 
 using namespace mpss;
 
@@ -53,6 +54,8 @@ void mpss_config_defaults(mpss_config *c) {
     c->incenter = 0;
     c->quick_render = 0;
     c->exact_mo = 0;
+    c->kernel_timing = 0;
+    c->count_traversal = 0;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -195,6 +198,27 @@ int mpss_get_irradiance(mpss_ctx *c, float *E, uint32_t *n) {
     });
 }
 
+int mpss_get_render_stats(mpss_ctx *c, mpss_render_stats *out) {
+    return guarded([&] {
+        require(c && out, "mpss_get_render_stats: null argument");
+        *out = reinterpret_cast<Context *>(c)->render_stats();
+    });
+}
+
+int mpss_set_instrumentation(mpss_ctx *c, int timing, int counting) {
+    return guarded([&] {
+        require(c, "mpss_set_instrumentation: null ctx");
+        reinterpret_cast<Context *>(c)->set_instrumentation(timing != 0, counting != 0);
+    });
+}
+
+int mpss_reset_render_stats(mpss_ctx *c) {
+    return guarded([&] {
+        require(c, "mpss_reset_render_stats: null ctx");
+        reinterpret_cast<Context *>(c)->reset_render_stats();
+    });
+}
+
 int mpss_preprocess(mpss_ctx *c, uint32_t seed) {
     return guarded([&] {
         require(c, "mpss_preprocess: null ctx");
@@ -213,6 +237,13 @@ int mpss_render_tile(mpss_ctx *c, int spp, uint32_t seed, int x0, int x1, int y0
 
 // ---------------------------------------------------------------- host-side utilities
 extern "C" {
+
+int mpss_host_from_rgb(const float *rgb, int illuminant, float *out) {
+    return guarded([&] {
+        require(rgb && out, "mpss_host_from_rgb: null argument");
+        spectrum_from_rgb(rgb, illuminant != 0, out);
+    });
+}
 
 int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta) {
     return guarded([&] {

@@ -70,8 +70,9 @@ struct SampleRecs {
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, int n, uint32_t seed, float *E_out);
 __global__ void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
+template <bool COUNT>
 __global__ void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples, int nblocks,
-                             int have_octree);
+                             int have_octree, unsigned long long *counts);
 __global__ void film_kernel(TileBatch tb, const uint32_t *flags, const float *xyz, float *out, int out_stride_px,
                             int xres);
 

@@ -351,8 +351,9 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
 }
 
 // ------------------------------------------------------------------ Mo term + Li assembly
+template <bool COUNT>
 __global__ __launch_bounds__(256) void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples,
-                                                    int nblocks, int have_octree) {
+                                                    int nblocks, int have_octree, unsigned long long *counts) {
     const int lb = xcd_remap((int)blockIdx.x, nblocks);
     const int lane = threadIdx.x & 63;
     const int g = lane >> 3, k = lane & 7;
@@ -363,8 +364,13 @@ __global__ __launch_bounds__(256) void shade_kernel(RenderScene sc, PacketTree t
     const bool sss = (flags & REC_SSS) && have_octree;
     float mo[4];
     int kn = 0, kp = 0;
-    mo_packet_traverse<false>(tree, pq.x, pq.y, pq.z, sss, k, mo, kn, kp);
+    mo_packet_traverse<COUNT>(tree, pq.x, pq.y, pq.z, sss, k, mo, kn, kp);
     if (!valid) return;
+    if (COUNT && k == 0 && sss) {
+        atomicAdd(&counts[0], 1ull);
+        atomicAdd(&counts[1], (unsigned long long)kn);
+        atomicAdd(&counts[2], (unsigned long long)kp);
+    }
     // L = 0 + Le; L += SSS; L += Ld   (MultipoleSubsurfaceIntegrator::Li, file lines 341-386)
     float L[4] = {0.f, 0.f, 0.f, 0.f};
     if (flags & REC_LE) {
@@ -425,6 +431,11 @@ __global__ __launch_bounds__(256) void shade_kernel(RenderScene sc, PacketTree t
         o[2] = Z;
     }
 }
+
+template __global__ void shade_kernel<false>(RenderScene, PacketTree, SampleRecs, int64_t, int, int,
+                                             unsigned long long *);
+template __global__ void shade_kernel<true>(RenderScene, PacketTree, SampleRecs, int64_t, int, int,
+                                            unsigned long long *);
 
 // ------------------------------------------------------------------ film
 __global__ __launch_bounds__(256) void film_kernel(TileBatch tb, const uint32_t *__restrict__ flags,

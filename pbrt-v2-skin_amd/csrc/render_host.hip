@@ -210,9 +210,12 @@ void Context::preprocess(uint32_t seed) {
         irradiance_.resize((size_t)n * NB);
         for (int i = 0; i < n; ++i) memcpy(&irradiance_[(size_t)i * NB], s, sizeof(s));
     } else {
+        hipEvent_t ev{};
+        time_begin(0, ev);
         hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sc, dp.ptr, dn.ptr, de.ptr,
                            dm.ptr, n, seed, dE.ptr);
         MPSS_HIP(hipGetLastError());
+        time_end(0, ev, 0);
         irradiance_.resize((size_t)n * NB);
         MPSS_HIP(hipMemcpy(irradiance_.data(), dE.ptr, sizeof(float) * irradiance_.size(), hipMemcpyDeviceToHost));
     }
@@ -264,17 +267,79 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
             ws_n_ = tb.nsamples;
         }
         SampleRecs rec{ws_flags_.ptr, ws_pq_.ptr, ws_ld_.ptr, ws_xyz_.ptr};
+        hipEvent_t ev{};
+        time_begin(stream, ev);
         hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
                            sc, tb, rec);
+        time_end(stream, ev, 1);
         const int64_t packets = (tb.nsamples + 7) / 8;
         const int blocks = (int)((packets + 3) / 4);
-        hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples, blocks,
-                           have_tree);
+        time_begin(stream, ev);
+        if (cfg_.count_traversal) {
+            if (!d_counts_.ptr) {
+                d_counts_.alloc(3);
+                MPSS_HIP(hipMemset(d_counts_.ptr, 0, 3 * sizeof(unsigned long long)));
+            }
+            hipLaunchKernelGGL(shade_kernel<true>, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples,
+                               blocks, have_tree, d_counts_.ptr);
+        } else {
+            hipLaunchKernelGGL(shade_kernel<false>, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples,
+                               blocks, have_tree, nullptr);
+        }
+        time_end(stream, ev, 2);
         const int npx = tw * (ye - yb);
+        time_begin(stream, ev);
         hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, tb, ws_flags_.ptr,
                            ws_xyz_.ptr, out + (size_t)(yb - y0) * tw * 4, tw, W);
+        time_end(stream, ev, 3);
         MPSS_HIP(hipGetLastError());
+        stats_.samples += tb.nsamples;
     }
+}
+
+void Context::time_begin(hipStream_t s, hipEvent_t &a) {
+    if (!cfg_.kernel_timing) return;
+    MPSS_HIP(hipEventCreate(&a));
+    MPSS_HIP(hipEventRecord(a, s));
+}
+
+void Context::time_end(hipStream_t s, hipEvent_t a, int kind) {
+    if (!cfg_.kernel_timing) return;
+    hipEvent_t b;
+    MPSS_HIP(hipEventCreate(&b));
+    MPSS_HIP(hipEventRecord(b, s));
+    timed_.push_back(Timed{a, b, kind});
+}
+
+mpss_render_stats Context::render_stats() {
+    activate();
+    MPSS_HIP(hipDeviceSynchronize());
+    for (const Timed &t : timed_) {
+        float ms = 0.f;
+        MPSS_HIP(hipEventElapsedTime(&ms, t.a, t.b));
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+        double *dst[4] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film};
+        int64_t *cnt[4] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film};
+        *dst[t.kind] += ms;
+        *cnt[t.kind] += 1;
+    }
+    timed_.clear();
+    mpss_render_stats out = stats_;
+    if (d_counts_.ptr) {
+        unsigned long long c[3];
+        MPSS_HIP(hipMemcpy(c, d_counts_.ptr, sizeof(c), hipMemcpyDeviceToHost));
+        out.sss_samples = (int64_t)c[0];
+        out.mo_nodes = (int64_t)c[1];
+        out.mo_points = (int64_t)c[2];
+    }
+    return out;
+}
+
+void Context::reset_render_stats() {
+    (void)render_stats();  // drain pending events
+    stats_ = mpss_render_stats{};
+    if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, 3 * sizeof(unsigned long long)));
 }
 
 int Context::first_bssrdf_material() const { return materials_.empty() ? -1 : 0; }

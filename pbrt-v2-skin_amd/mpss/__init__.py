@@ -39,7 +39,16 @@ class Config(C.Structure):
     """mpss_config (CreateMultipoleSubsurfaceIntegrator params, multipolesubsurface.cpp:393-401)."""
     _fields_ = [("device", C.c_int), ("max_depth", C.c_int), ("max_error", C.c_float),
                 ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
-                ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int)]
+                ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
+                ("kernel_timing", C.c_int), ("count_traversal", C.c_int)]
+
+
+class RenderStats(C.Structure):
+    """mpss_render_stats."""
+    _fields_ = [("ms_irradiance", C.c_double), ("ms_camera", C.c_double), ("ms_shade", C.c_double),
+                ("ms_film", C.c_double), ("n_irradiance", C.c_int64), ("n_camera", C.c_int64),
+                ("n_shade", C.c_int64), ("n_film", C.c_int64), ("samples", C.c_int64), ("sss_samples", C.c_int64),
+                ("mo_nodes", C.c_int64), ("mo_points", C.c_int64)]
 
 
 class LayeredSkin(C.Structure):
@@ -78,7 +87,11 @@ _sig("mpss_set_surface_points", C.c_int, [vp, u32, vp])
 _sig("mpss_get_surface_points", C.c_int, [vp, vp, u32p])
 _sig("mpss_get_irradiance", C.c_int, [vp, vp, u32p])
 _sig("mpss_preprocess", C.c_int, [vp, u32])
+_sig("mpss_get_render_stats", C.c_int, [vp, C.POINTER(RenderStats)])
+_sig("mpss_reset_render_stats", C.c_int, [vp])
+_sig("mpss_set_instrumentation", C.c_int, [vp, C.c_int, C.c_int])
 _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
+_sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
@@ -134,6 +147,12 @@ assert SURFACE_POINT.itemsize == 44
 
 
 # ------------------------------------------------------------------ host utilities
+def host_from_rgb(rgb, illuminant=False):
+    out = np.zeros(NB, np.float32)
+    check(_lib.mpss_host_from_rgb(np.ascontiguousarray(rgb, np.float32), int(illuminant), out))
+    return out
+
+
 def host_skin_layers(skin):
     mua = np.zeros((2, NB), np.float32)
     musp = np.zeros((2, NB), np.float32)
@@ -269,6 +288,17 @@ class Context:
         out = np.zeros((n.value, NB), np.float32)
         check(_lib.mpss_get_irradiance(self.h, out.ctypes.data, C.byref(n)))
         return out
+
+    def render_stats(self):
+        st = RenderStats()
+        check(_lib.mpss_get_render_stats(self.h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in RenderStats._fields_}
+
+    def set_instrumentation(self, kernel_timing=False, count_traversal=False):
+        check(_lib.mpss_set_instrumentation(self.h, int(kernel_timing), int(count_traversal)))
+
+    def reset_render_stats(self):
+        check(_lib.mpss_reset_render_stats(self.h))
 
     def preprocess(self, seed=0):
         check(_lib.mpss_preprocess(self.h, seed))
