@@ -110,7 +110,7 @@ def test_mo_edge_cases(oracle, mpss, torch_dev, wide_profile):
 def test_layeredskin_material_on_device(oracle, mpss, torch_dev):
     """mpss_add_layeredskin builds the tables itself; they must match the oracle's."""
     ctx = mpss.Context(max_error=0.1)
-    skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5,
+    skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5, Kt=[0.0] * 30,
                              desired_length=64)
     mid = ctx.add_layeredskin(skin)
     tab, rcp, rho, tot = ctx.material_tables(mid)

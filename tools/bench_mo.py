@@ -36,7 +36,7 @@ def main():
     radii = (0.25, 0.3, 0.35)
     t0 = time.time()
     ctx = mpss.Context(max_error=args.max_error, exact_mo=int(args.exact))
-    skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5,
+    skin = mpss.default_skin(roughness=0.3, nmperunit=40e6, f_mel=0.5, f_eu=0.5, f_blood=0.5, f_ohg=0.5, Kt=[0.0] * 30,
                              desired_length=args.desired_length)
     mid = ctx.add_layeredskin(skin)
     t1 = time.time()
