@@ -153,6 +153,11 @@ int mpss_reset_render_stats(mpss_ctx *ctx);
 /* SampledSpectrum::FromRGB (spectrum.cpp:103-187); pbrt's "color"/"rgb" parameters use
  * illuminant = 0 (ParamSet::AddRGBSpectrum, paramset.cpp:97-105). */
 int mpss_host_from_rgb(const float *rgb, int illuminant, float *out);
+/* TessellateSurfacePoints of one triangle mesh (trianglemesh.cpp:187-351); flip =
+ * ReverseOrientation ^ ObjectToWorld.SwapsHandedness(). Sizes first with records NULL. */
+int mpss_host_tessellate(uint32_t nverts, const float *P, const float *N, const float *S, const float *uv,
+                         uint32_t ntris, const int32_t *indices, const float *obj_to_world, const float *world_to_obj,
+                         int flip, uint32_t material_id, float min_dist, int incenter, void *records, uint32_t *n);
 /* LayeredSkin -> per-layer 30-band mua/musp [2][30], thickness[2], eta[2] (layeredskin.cpp:47-89). */
 int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta);
 /* Multipole profile from layer params; rd_table: [30][*length] (query *length with rd_table NULL). */

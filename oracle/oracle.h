@@ -90,6 +90,27 @@ int o_octree_export(const o_octree *t, float *node_p /*N*3*/, float *node_area, 
                     int32_t *leaf_first, int32_t *leaf_count, int32_t *point_order);
 void o_octree_bounds(const o_octree *t, float bmin[3], float bmax[3]);
 
+/* ---- per-pixel path (render.c): tessellation, irradiance, Li, film ---- */
+typedef struct {  /* SurfacePoint, renderers/surfacepoints.h:45-55 (44-byte record) */
+    float p[3], n[3], u, v;
+    uint32_t material;
+    float area, ray_eps;
+} o_surface_point;
+typedef struct o_scene o_scene;
+o_scene *o_scene_create(int xres, int yres, const float *raster_to_camera, const float *camera_to_world);
+int o_scene_add_material(o_scene *s, const float *R, const float *albedo, float mix, float roughness, float eta,
+                         int fixed_fresnel, const float *rho, int n_rho, int is_mc, const float *rd_table, int L,
+                         const float *rcp);
+int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
+                     const int32_t *idx, const float *o2w, const float *w2o, int flip, int material);
+int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples);
+long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_point *out, long cap);
+void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E);
+void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, const float *E, const float *area,
+                        float max_error);
+void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw);
+void o_scene_free(o_scene *s);
+
 #ifdef __cplusplus
 }
 #endif

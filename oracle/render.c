@@ -1,0 +1,1124 @@
+/*
+ * render.c -- TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Scalar CPU restatement of the per-pixel path of MultipoleSubsurfaceIntegrator with
+ * LayeredSkin: surface-point tessellation, irradiance Preprocess, camera rays, scene
+ * intersection, direct lighting with MIS, the Mo() term and the box-filtered film.
+ * Sample values come from the same counter-based scrambled (0,2)-sequences as the product
+ * ("replay mode"), so both sides see identical sample values.
+ *
+ * Reference files (paths under /root/reference/src):
+ *   shapes/trianglemesh.cpp:187-351   TessellateSurfacePoints / tessellator / matching
+ *   shapes/trianglemesh.inl:54-135,224-346  Triangle::Intersect, GetShadingGeometry, ...
+ *   shapes/sphere.cpp                 Sphere::Intersect / Sample / Pdf
+ *   core/light.cpp:145-172            ShapeSet::Sample / Pdf
+ *   lights/diffuse.cpp:45-87          DiffuseAreaLight::L / Sample_L / Pdf
+ *   core/integrator.cpp:47-174        UniformSampleAllLights / EstimateDirect
+ *   core/reflection.{h,cpp}           Microfacet, Beckmann, FresnelDielectric, BSDF::f/Sample_f/Pdf
+ *   integrators/multipolesubsurface.cpp:72-152 (IrradianceTask), 253-303 (Li)
+ *   renderers/samplerrenderer.cpp:100-140 (sample filter), film/image.cpp:77-137 (AddSample)
+ *   cameras/perspective.cpp (GenerateRay)
+ * Intersection uses its own median-split BVH: the closest hit does not depend on the tree
+ * (only exact t ties between triangles could differ).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+#include "../data/spectral_bands.h"
+
+#define PI_F 3.14159265358979323846f
+#define INV_PI_F 0.31830988618379067154f
+
+typedef struct { float x, y, z; } v3;
+
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+static inline v3 mul(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float absdot(v3 a, v3 b) { return fabsf(dot(a, b)); }
+static inline float lensq(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline float len(v3 a) { return sqrtf(lensq(a)); }
+/* geometry.h: v / f multiplies by the reciprocal */
+static inline v3 divf(v3 a, float f) { float inv = 1.f / f; return mk(a.x * inv, a.y * inv, a.z * inv); }
+static inline v3 nrm(v3 a) { return divf(a, len(a)); }
+/* geometry.h Cross: double intermediates */
+static inline v3 crs(v3 a, v3 b) {
+    double ax = a.x, ay = a.y, az = a.z, bx = b.x, by = b.y, bz = b.z;
+    return mk((float)((ay * bz) - (az * by)), (float)((az * bx) - (ax * bz)), (float)((ax * by) - (ay * bx)));
+}
+static inline float dsq(v3 a, v3 b) { return lensq(sub(a, b)); }
+static inline v3 ld(const float *a, int i) { return mk(a[3 * i], a[3 * i + 1], a[3 * i + 2]); }
+
+/* transcendentals: evaluated in double, rounded once (DESIGN.md "float conventions") */
+static inline float fsin(float x) { return (float)sin((double)x); }
+static inline float fcos(float x) { return (float)cos((double)x); }
+static inline float fexp(float x) { return (float)exp((double)x); }
+static inline float flog(float x) { return (float)log((double)x); }
+static inline float fatan(float x) { return (float)atan((double)x); }
+static inline float fatan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+static inline float facos(float x) { return (float)acos((double)x); }
+static inline float fpowf_(float x, float y) { return (float)pow((double)x, (double)y); }
+
+static void coord_system(v3 v1, v3 *v2, v3 *v3o) { /* geometry.h CoordinateSystem */
+    if (fabsf(v1.x) > fabsf(v1.y)) {
+        float inv = 1.f / sqrtf(v1.x * v1.x + v1.z * v1.z);
+        *v2 = mk(-v1.z * inv, 0.f, v1.x * inv);
+    } else {
+        float inv = 1.f / sqrtf(v1.y * v1.y + v1.z * v1.z);
+        *v2 = mk(0.f, v1.z * inv, -v1.y * inv);
+    }
+    *v3o = crs(v1, *v2);
+}
+
+/* Transform::operator() on points / vectors / normals (transform.h:190-237) */
+static v3 xpoint(const float *m, v3 p) {
+    float xp = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float yp = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float zp = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wp = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wp == 1.f) return mk(xp, yp, zp);
+    return divf(mk(xp, yp, zp), wp);
+}
+static v3 xvector(const float *m, v3 v) {
+    return mk(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[4] * v.x + m[5] * v.y + m[6] * v.z,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z);
+}
+static v3 xnormal(const float *mi, v3 n) {
+    return mk(mi[0] * n.x + mi[4] * n.y + mi[8] * n.z, mi[1] * n.x + mi[5] * n.y + mi[9] * n.z,
+              mi[2] * n.x + mi[6] * n.y + mi[10] * n.z);
+}
+
+/* ------------------------------------------------------------------ replay-mode sampler */
+static uint32_t mix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+    return h;
+}
+static uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) { return mix32(a ^ mix32(b ^ mix32(c + 0x9e3779b9u))); }
+#define ONE_MINUS_EPS 0x1.fffffep-1f
+static float vdc(uint32_t n, uint32_t scramble) { /* montecarlo.h VanDerCorput */
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ffu) << 8) | ((n & 0xff00ff00u) >> 8);
+    n = ((n & 0x0f0f0f0fu) << 4) | ((n & 0xf0f0f0f0u) >> 4);
+    n = ((n & 0x33333333u) << 2) | ((n & 0xccccccccu) >> 2);
+    n = ((n & 0x55555555u) << 1) | ((n & 0xaaaaaaaau) >> 1);
+    n ^= scramble;
+    float v = (float)((n >> 8) & 0xffffff) / (float)(1 << 24);
+    return v < ONE_MINUS_EPS ? v : ONE_MINUS_EPS;
+}
+static float sobol(uint32_t n, uint32_t scramble) { /* montecarlo.h Sobol2 */
+    for (uint32_t v = 1u << 31; n != 0; n >>= 1, v ^= v >> 1)
+        if (n & 1u) scramble ^= v;
+    float r = (float)((scramble >> 8) & 0xffffff) / (float)(1 << 24);
+    return r < ONE_MINUS_EPS ? r : ONE_MINUS_EPS;
+}
+/* dimension ids of one camera sample (see DESIGN.md "replay mode") */
+enum { D_IMAGE = 0, D_LIGHT_POS = 2, D_BSDF_DIR = 4, D_IRR_POS = 6, D_PERM = 9 };
+
+/* ------------------------------------------------------------------ scene */
+typedef struct {
+    int nv, nt;
+    float *P, *N, *S, *uv;
+    int *idx;
+    float o2w[16], w2o[16];
+    int flip, material;
+} o_mesh;
+
+typedef struct {
+    v3 c;
+    float r, phimax, thetamin, thetamax, area;
+    float Le[O_NB];
+    int ns_pow2;
+} o_light;
+
+typedef struct {
+    float R[O_NB], alb_mix[O_NB], alb_1mmix[O_NB];
+    float rough2, eta;
+    int fixed_fresnel, is_mc, has_refl;
+    float *rho;
+    int n_rho;
+    float *rd;
+    int L;
+    float rcp[O_NB];
+} o_mat;
+
+typedef struct { float bmin[3], bmax[3]; int left, right, first, count; } o_bnode;
+
+struct o_scene {
+    int xres, yres;
+    float r2c[16], c2w[16];
+    o_mesh *meshes; int nmeshes;
+    o_light *lights; int nlights;
+    o_mat *mats; int nmats;
+    /* flattened triangles for intersection */
+    int ntris;
+    int *tri_mesh, *tri_local;
+    float *tp1, *te1, *te2; /* p1, e1 = p2 - p1, e2 = p3 - p1 */
+    o_bnode *bvh; int nbvh;
+    int *order;
+    o_octree *octree;
+    float max_error;
+};
+
+o_scene *o_scene_create(int xres, int yres, const float *r2c, const float *c2w) {
+    o_scene *s = (o_scene *)calloc(1, sizeof(o_scene));
+    s->xres = xres;
+    s->yres = yres;
+    memcpy(s->r2c, r2c, sizeof(s->r2c));
+    memcpy(s->c2w, c2w, sizeof(s->c2w));
+    return s;
+}
+
+static float *dupf(const float *a, size_t n) {
+    if (!a) return NULL;
+    float *r = (float *)malloc(n * sizeof(float));
+    memcpy(r, a, n * sizeof(float));
+    return r;
+}
+
+int o_scene_add_material(o_scene *s, const float *R, const float *albedo, float mix, float roughness, float eta,
+                         int fixed_fresnel, const float *rho, int n_rho, int is_mc, const float *rd, int L,
+                         const float *rcp) {
+    s->mats = (o_mat *)realloc(s->mats, (s->nmats + 1) * sizeof(o_mat));
+    o_mat *m = &s->mats[s->nmats];
+    memset(m, 0, sizeof(*m));
+    m->has_refl = 0;
+    for (int c = 0; c < O_NB; ++c) {
+        m->R[c] = R[c];
+        if (R[c] != 0.f) m->has_refl = 1;
+        m->alb_mix[c] = fpowf_(albedo[c], mix);          /* Pow(albedo, mix): IrradianceTask */
+        m->alb_1mmix[c] = fpowf_(albedo[c], 1.f - mix);  /* Pow(albedo, 1 - mix): Li */
+        m->rcp[c] = rcp[c];
+    }
+    float r = roughness < 1e-3f ? 1e-3f : roughness;    /* Beckmann ctor clamps */
+    m->rough2 = r * r;
+    m->eta = eta;
+    m->fixed_fresnel = fixed_fresnel;
+    m->is_mc = is_mc;
+    m->rho = dupf(rho, (size_t)n_rho);
+    m->n_rho = n_rho;
+    m->rd = dupf(rd, (size_t)O_NB * L);
+    m->L = L;
+    return s->nmats++;
+}
+
+int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
+                     const int32_t *idx, const float *o2w, const float *w2o, int flip, int material) {
+    s->meshes = (o_mesh *)realloc(s->meshes, (s->nmeshes + 1) * sizeof(o_mesh));
+    o_mesh *m = &s->meshes[s->nmeshes];
+    m->nv = nv;
+    m->nt = nt;
+    m->P = dupf(P, 3 * (size_t)nv);
+    m->N = dupf(N, 3 * (size_t)nv);
+    m->S = dupf(S, 3 * (size_t)nv);
+    m->uv = dupf(uv, 2 * (size_t)nv);
+    m->idx = (int *)malloc(3 * (size_t)nt * sizeof(int));
+    memcpy(m->idx, idx, 3 * (size_t)nt * sizeof(int));
+    memcpy(m->o2w, o2w, sizeof(m->o2w));
+    memcpy(m->w2o, w2o, sizeof(m->w2o));
+    m->flip = flip;
+    m->material = material;
+    return s->nmeshes++;
+}
+
+static int round_up_pow2(int v) { int r = 1; while (r < v) r <<= 1; return r; }
+
+int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples) {
+    s->lights = (o_light *)realloc(s->lights, (s->nlights + 1) * sizeof(o_light));
+    o_light *l = &s->lights[s->nlights];
+    l->c = mk(c[0], c[1], c[2]);
+    l->r = r;
+    /* Sphere ctor (sphere.cpp): zmin = -r, zmax = r, phiMax = 360 degrees */
+    l->phimax = (PI_F / 180.f) * 360.f;
+    l->thetamin = facos(-1.f);
+    l->thetamax = facos(1.f);
+    l->area = l->phimax * r * (r - -r);
+    memcpy(l->Le, Le, sizeof(l->Le));
+    l->ns_pow2 = round_up_pow2(nsamples);
+    return s->nlights++;
+}
+
+/* ------------------------------------------------------------------ triangle geometry */
+typedef struct { v3 p, ng, nn, sn, tn; float u, v; } frame_t;
+
+static void tri_uvs(const o_mesh *m, int t, float uv[3][2]) { /* TriangleBase::GetUVs */
+    if (m->uv) {
+        for (int k = 0; k < 3; ++k) {
+            uv[k][0] = m->uv[2 * m->idx[3 * t + k]];
+            uv[k][1] = m->uv[2 * m->idx[3 * t + k] + 1];
+        }
+    } else {
+        uv[0][0] = 0.f; uv[0][1] = 0.f; uv[1][0] = 1.f; uv[1][1] = 0.f; uv[2][0] = 1.f; uv[2][1] = 1.f;
+    }
+}
+
+/* dg (Intersect / GetDifferentialGeometries) + GetShadingGeometry + BSDF frame */
+static frame_t tri_frame(const o_mesh *m, int t, v3 p, float b0, float b1, float b2) {
+    v3 p1 = ld(m->P, m->idx[3 * t]), p2 = ld(m->P, m->idx[3 * t + 1]), p3 = ld(m->P, m->idx[3 * t + 2]);
+    v3 e1 = sub(p2, p1), e2 = sub(p3, p1);
+    float uv[3][2];
+    tri_uvs(m, t, uv);
+    float du1 = uv[0][0] - uv[2][0], du2 = uv[1][0] - uv[2][0];
+    float dv1 = uv[0][1] - uv[2][1], dv2 = uv[1][1] - uv[2][1];
+    v3 dp1 = sub(p1, p3), dp2 = sub(p2, p3);
+    float det = du1 * dv2 - dv1 * du2;
+    v3 dpdu, dpdv;
+    if (det == 0.f) {
+        coord_system(nrm(crs(e2, e1)), &dpdu, &dpdv);
+    } else {
+        float invdet = 1.f / det;
+        dpdu = mul(sub(mul(dp1, dv2), mul(dp2, dv1)), invdet);
+        dpdv = mul(add(mul(dp1, -du2), mul(dp2, du1)), invdet);
+    }
+    frame_t f;
+    f.p = p;
+    f.u = b0 * uv[0][0] + b1 * uv[1][0] + b2 * uv[2][0];
+    f.v = b0 * uv[0][1] + b1 * uv[1][1] + b2 * uv[2][1];
+    /* DifferentialGeometry ctor: nn = Normalize(Cross(dpdu, dpdv)), flipped on RO ^ SwapsHandedness */
+    v3 ng = nrm(crs(dpdu, dpdv));
+    if (m->flip) ng = mul(ng, -1.f);
+    f.ng = ng;
+    v3 ss, ts;
+    if (!m->N && !m->S) {
+        f.nn = ng;
+        ss = dpdu;
+    } else {
+        /* GetShadingGeometry: barycentrics of (u, v) via SolveLinearSystem2x2 */
+        float b[3];
+        float A[2][2] = {{uv[1][0] - uv[0][0], uv[2][0] - uv[0][0]}, {uv[1][1] - uv[0][1], uv[2][1] - uv[0][1]}};
+        float C[2] = {f.u - uv[0][0], f.v - uv[0][1]};
+        float d = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+        int ok = !(fabsf(d) < 1e-10f);
+        if (ok) {
+            b[1] = (A[1][1] * C[0] - A[0][1] * C[1]) / d;
+            b[2] = (A[0][0] * C[1] - A[1][0] * C[0]) / d;
+            if (isnan(b[1]) || isnan(b[2])) ok = 0;
+        }
+        if (!ok) b[0] = b[1] = b[2] = 1.f / 3.f;
+        else b[0] = 1.f - b[1] - b[2];
+        v3 ns;
+        if (m->N) {
+            v3 n0 = ld(m->N, m->idx[3 * t]), n1 = ld(m->N, m->idx[3 * t + 1]), n2 = ld(m->N, m->idx[3 * t + 2]);
+            ns = nrm(xnormal(m->w2o, add(add(mul(n0, b[0]), mul(n1, b[1])), mul(n2, b[2]))));
+        } else {
+            ns = ng;
+        }
+        if (m->S) {
+            v3 s0 = ld(m->S, m->idx[3 * t]), s1 = ld(m->S, m->idx[3 * t + 1]), s2 = ld(m->S, m->idx[3 * t + 2]);
+            ss = nrm(xvector(m->o2w, add(add(mul(s0, b[0]), mul(s1, b[1])), mul(s2, b[2]))));
+        } else {
+            ss = nrm(dpdu);
+        }
+        ts = crs(ss, ns);
+        if (lensq(ts) > 0.f) {
+            ts = nrm(ts);
+            ss = crs(ts, ns);
+        } else {
+            coord_system(ns, &ss, &ts);
+        }
+        v3 nn = nrm(crs(ss, ts));
+        if (m->flip) nn = mul(nn, -1.f);
+        f.nn = nn;
+    }
+    f.sn = nrm(ss);
+    f.tn = crs(f.nn, f.sn);
+    return f;
+}
+
+/* Triangle::Intersect ray test */
+static int tri_hit(v3 o, v3 d, float mint, float maxt, v3 p1, v3 e1, v3 e2, float *tt, float *bb1, float *bb2) {
+    v3 s1 = crs(d, e2);
+    float divisor = dot(s1, e1);
+    if (divisor == 0.f) return 0;
+    float inv = 1.f / divisor;
+    v3 dd = sub(o, p1);
+    float b1 = dot(dd, s1) * inv;
+    if (b1 < 0.f || b1 > 1.f) return 0;
+    v3 s2 = crs(dd, e1);
+    float b2 = dot(d, s2) * inv;
+    if (b2 < 0.f || b1 + b2 > 1.f) return 0;
+    float t = dot(e2, s2) * inv;
+    if (t < mint || t > maxt) return 0;
+    *tt = t; *bb1 = b1; *bb2 = b2;
+    return 1;
+}
+
+/* ------------------------------------------------------------------ sphere light */
+static int quad(float A, float B, float C, float *t0, float *t1) { /* pbrt.h Quadratic */
+    float disc = B * B - 4.f * A * C;
+    if (disc < 0.f) return 0;
+    float rd = sqrtf(disc);
+    float q = (B < 0.f) ? -.5f * (B - rd) : -.5f * (B + rd);
+    *t0 = q / A;
+    *t1 = C / q;
+    if (*t0 > *t1) { float x = *t0; *t0 = *t1; *t1 = x; }
+    return 1;
+}
+
+static int sphere_hit(const o_light *s, v3 o, v3 d, float mint, float maxt, float *thit, v3 *nn) {
+    v3 ro = sub(o, s->c); /* WorldToObject of a translation */
+    float A = d.x * d.x + d.y * d.y + d.z * d.z;
+    float B = 2 * (d.x * ro.x + d.y * ro.y + d.z * ro.z);
+    float C = ro.x * ro.x + ro.y * ro.y + ro.z * ro.z - s->r * s->r;
+    float t0, t1;
+    if (!quad(A, B, C, &t0, &t1)) return 0;
+    if (t0 > maxt || t1 < mint) return 0;
+    float th = t0;
+    if (t0 < mint) {
+        th = t1;
+        if (th > maxt) return 0;
+    }
+    v3 ph = add(ro, mul(d, th));
+    if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * s->r;
+    float phi = fatan2(ph.y, ph.x);
+    if (phi < 0.f) phi += 2.f * PI_F;
+    if (phi > s->phimax) {
+        if (th == t1) return 0;
+        if (t1 > maxt) return 0;
+        th = t1;
+        ph = add(ro, mul(d, th));
+        if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * s->r;
+        phi = fatan2(ph.y, ph.x);
+        if (phi < 0.f) phi += 2.f * PI_F;
+        if (phi > s->phimax) return 0;
+    }
+    if (nn) {
+        float cz = ph.z / s->r;
+        float theta = facos(cz < -1.f ? -1.f : (cz > 1.f ? 1.f : cz));
+        float zr = sqrtf(ph.x * ph.x + ph.y * ph.y);
+        float izr = 1.f / zr;
+        float cphi = ph.x * izr, sphi = ph.y * izr;
+        v3 dpdu = mk(-s->phimax * ph.y, s->phimax * ph.x, 0.f);
+        v3 dpdv = mul(mk(ph.z * cphi, ph.z * sphi, -s->r * fsin(theta)), s->thetamax - s->thetamin);
+        *nn = nrm(crs(dpdu, dpdv));
+    }
+    *thit = th;
+    return 1;
+}
+
+static v3 sample_sphere_uniform(float u1, float u2) { /* montecarlo.cpp UniformSampleSphere */
+    float z = 1.f - 2.f * u1;
+    float r = sqrtf(fmaxf(0.f, 1.f - z * z));
+    float phi = 2.f * PI_F * u2;
+    return mk(r * fcos(phi), r * fsin(phi), z);
+}
+
+static v3 sample_cone(float u1, float u2, float ctmax, v3 x, v3 y, v3 z) { /* UniformSampleCone(frame) */
+    float ct = (1.f - u1) * ctmax + u1 * 1.f;
+    float st = sqrtf(1.f - ct * ct);
+    float phi = u2 * 2.f * PI_F;
+    return add(add(mul(x, fcos(phi) * st), mul(y, fsin(phi) * st)), mul(z, ct));
+}
+
+/* Sphere::Sample(p, u1, u2, &ns) + ShapeSet::Sample re-intersection; returns point, normal */
+static v3 light_sample_point(const o_light *s, v3 p, float u1, float u2, v3 *ns) {
+    v3 pc = s->c;
+    v3 wc = nrm(sub(pc, p)), wcx, wcy;
+    coord_system(wc, &wcx, &wcy);
+    v3 ps;
+    if (dsq(p, pc) - s->r * s->r < 1e-4f) {
+        v3 q = mul(sample_sphere_uniform(u1, u2), s->r);
+        *ns = nrm(q);
+        ps = add(q, pc);
+    } else {
+        float st2 = s->r * s->r / dsq(p, pc);
+        float ctmax = sqrtf(fmaxf(0.f, 1.f - st2));
+        v3 rd = sample_cone(u1, u2, ctmax, wcx, wcy, wc);
+        float th;
+        if (!sphere_hit(s, p, rd, 1e-3f, INFINITY, &th, NULL)) th = dot(sub(pc, p), nrm(rd));
+        ps = add(p, mul(rd, th));
+        *ns = nrm(sub(ps, pc));
+    }
+    v3 rd2 = sub(ps, p);
+    float th2 = 1.f;
+    v3 nn2;
+    if (sphere_hit(s, p, rd2, 1e-3f, INFINITY, &th2, &nn2)) *ns = nn2;
+    return add(p, mul(rd2, th2));
+}
+
+static float light_pdf(const o_light *s, v3 p, v3 wi) { /* ShapeSet::Pdf of one Sphere */
+    float pdf;
+    if (dsq(p, s->c) - s->r * s->r < 1e-4f) {
+        float th;
+        v3 nn;
+        if (!sphere_hit(s, p, wi, 1e-3f, INFINITY, &th, &nn)) pdf = 0.f;
+        else {
+            pdf = dsq(p, add(p, mul(wi, th))) / (absdot(nn, neg(wi)) * s->area);
+            if (isinf(pdf)) pdf = 0.f;
+        }
+    } else {
+        float st2 = s->r * s->r / dsq(p, s->c);
+        float ctmax = sqrtf(fmaxf(0.f, 1.f - st2));
+        pdf = 1.f / (2.f * PI_F * (1.f - ctmax));
+    }
+    return (0.f + s->area * pdf) / s->area;
+}
+
+/* DiffuseAreaLight::Sample_L: wi, pdf, shadow segment, radiance non-black flag */
+typedef struct { v3 wi, so, sd; float pdf, smint, smaxt; int nonblack; } lsamp;
+static lsamp light_sample(const o_light *L, v3 p, float peps, float u0, float u1) {
+    lsamp r;
+    v3 ns;
+    v3 ps = light_sample_point(L, p, u0, u1, &ns);
+    r.wi = nrm(sub(ps, p));
+    r.pdf = light_pdf(L, p, r.wi);
+    float dist = len(sub(p, ps));
+    r.so = p;
+    r.sd = divf(sub(ps, p), dist);
+    r.smint = peps;
+    r.smaxt = dist * (1.f - 1e-3f);
+    r.nonblack = dot(ns, neg(r.wi)) > 0.f;
+    return r;
+}
+
+/* ------------------------------------------------------------------ microfacet BSDF */
+static float beck_D(float r2, v3 wh) {
+    float ct = fabsf(wh.z), c2 = ct * ct, d = c2 * c2 * PI_F;
+    if (d == 0.f) return 0.f;
+    float irr = 1 / r2;
+    float e = (c2 - 1) * irr / c2;
+    return irr * fexp(e) / d;
+}
+static float fresnel(float cosi, float eta_i, float eta_t, int fixed) {
+    cosi = cosi < -1.f ? -1.f : (cosi > 1.f ? 1.f : cosi);
+    float ei = eta_i, et = eta_t;
+    if (!(cosi > 0.f)) { ei = eta_t; et = eta_i; }
+    float x = 1.f - cosi * cosi;
+    float sint = ei / et * sqrtf(x > 0.f ? x : 0.f);
+    float F;
+    if (sint >= 1.f) F = 1.f;
+    else {
+        float y = 1.f - sint * sint;
+        float cost = sqrtf(y > 0.f ? y : 0.f);
+        float ci = fabsf(cosi);
+        float par = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
+        float per = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
+        F = (par * par + per * per) / 2.f;
+    }
+    if (fixed) F = F + F * (1.f - F) * (1.f - F);
+    return F;
+}
+static float geomG(v3 wo, v3 wi, v3 wh) {
+    float a = fabsf(wh.z), wowh = absdot(wo, wh);
+    float g1 = 2.f * a * fabsf(wo.z) / wowh, g2 = 2.f * a * fabsf(wi.z) / wowh;
+    float m = g1 < g2 ? g1 : g2;
+    return 1.f < m ? 1.f : m;
+}
+/* Microfacet::f per band: R * D * G * F / (4 cos_i cos_o); returns 0 if the lobe is zero */
+static int mf_f(const o_mat *m, v3 wo, v3 wi, float f[O_NB]) {
+    float co = fabsf(wo.z), ci = fabsf(wi.z);
+    if (ci == 0.f || co == 0.f) return 0;
+    v3 wh = add(wi, wo);
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return 0;
+    wh = nrm(wh);
+    float F = fresnel(dot(wi, wh), 1.f, m->eta, m->fixed_fresnel);
+    float D = beck_D(m->rough2, wh), G = geomG(wo, wi, wh), den = 4.f * ci * co;
+    for (int c = 0; c < O_NB; ++c) f[c] = m->R[c] * D * G * F / den;
+    return 1;
+}
+static float mf_pdf(const o_mat *m, v3 wo, v3 wi) {
+    if (!(wo.z * wi.z > 0.f)) return 0.f;
+    v3 wh = nrm(add(wo, wi));
+    float ct = fabsf(wh.z);
+    float p = beck_D(m->rough2, wh) * ct / (4.f * dot(wo, wh));
+    if (dot(wo, wh) <= 0.f || p < 1e-20f) p = 0.f;
+    return p;
+}
+static void mf_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *pdf) {
+    float theta = fatan(sqrtf(-m->rough2 * flog(1.f - u1)));
+    float ct = fcos(theta), st = fsin(theta);
+    float phi = u2 * 2.f * PI_F;
+    v3 wh = mk(st * fcos(phi), st * fsin(phi), ct);
+    if (!(wo.z * wh.z > 0.f)) wh = neg(wh);
+    float dw = dot(wo, wh);
+    *wi = add(neg(wo), mul(wh, 2.f * dw));
+    float p = beck_D(m->rough2, wh) * ct / (4.f * dot(wo, wh));
+    if (dot(wo, wh) <= 0.f || p < 1e-20f) p = 0.f;
+    *pdf = p;
+}
+static v3 to_local(const frame_t *f, v3 v) { return mk(dot(v, f->sn), dot(v, f->tn), dot(v, f->nn)); }
+static v3 to_world(const frame_t *f, v3 v) {
+    return mk(f->sn.x * v.x + f->tn.x * v.y + f->nn.x * v.z, f->sn.y * v.x + f->tn.y * v.y + f->nn.y * v.z,
+              f->sn.z * v.x + f->tn.z * v.y + f->nn.z * v.z);
+}
+/* BSDF::f with the ng hemisphere test: a BRDF contributes only on the reflection side.
+ * wol / wil are the local-frame directions the BxDF sees (BSDF::Sample_f keeps the sampled
+ * local wi rather than re-projecting the world one). */
+static int bsdf_f(const o_mat *m, const frame_t *fr, v3 woW, v3 wiW, v3 wol, v3 wil, float f[O_NB]) {
+    if (!m->has_refl) return 0;
+    if (!(dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)) return 0;
+    if (!mf_f(m, wol, wil, f)) return 0;
+    for (int c = 0; c < O_NB; ++c)
+        if (f[c] != 0.f) return 1;
+    return 0;
+}
+static float power_h(float fp, float gp) { float f = 1 * fp, g = 1 * gp; return (f * f) / (f * f + g * g); }
+
+static float rho_at(const o_mat *m, float ct) { /* MultipoleBSSRDFData rho lookup (multipole.cpp:458-463) */
+    float fid = ct * (float)(m->n_rho - 1);
+    int id = (int)fid;
+    id = id < 0 ? 0 : (id > m->n_rho - 2 ? m->n_rho - 2 : id);
+    float t = fid - (float)id;
+    return (1.f - t) * m->rho[id] + t * m->rho[id + 1];
+}
+
+/* ------------------------------------------------------------------ BVH (own median split) */
+static int bvh_build_rec(o_scene *s, int lo, int hi, float *cent) {
+    int id = s->nbvh++;
+    o_bnode *n = &s->bvh[id];
+    float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = lo; i < hi; ++i) {
+        int t = s->order[i];
+        for (int k = 0; k < 3; ++k) {
+            float a = s->tp1[3 * t + k], b = a + s->te1[3 * t + k], c = a + s->te2[3 * t + k];
+            float mn = fminf(a, fminf(b, c)), mx = fmaxf(a, fmaxf(b, c));
+            /* the vertex positions themselves (p1 + e1 may round): widen by the mesh values */
+            bmin[k] = fminf(bmin[k], mn);
+            bmax[k] = fmaxf(bmax[k], mx);
+            cmin[k] = fminf(cmin[k], cent[3 * t + k]);
+            cmax[k] = fmaxf(cmax[k], cent[3 * t + k]);
+        }
+    }
+    for (int k = 0; k < 3; ++k) {
+        float pad = (bmax[k] - bmin[k]) * 1e-5f + 1e-7f;
+        s->bvh[id].bmin[k] = bmin[k] - pad;
+        s->bvh[id].bmax[k] = bmax[k] + pad;
+    }
+    if (hi - lo <= 4) {
+        n->left = n->right = -1;
+        n->first = lo;
+        n->count = hi - lo;
+        return id;
+    }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (cmax[k] - cmin[k] > cmax[ax] - cmin[ax]) ax = k;
+    int mid = (lo + hi) / 2;
+    /* nth_element by centroid on axis: simple insertion-free quickselect */
+    int l = lo, r = hi - 1;
+    while (l < r) {
+        float piv = cent[3 * s->order[(l + r) / 2] + ax];
+        int i = l, j = r;
+        while (i <= j) {
+            while (cent[3 * s->order[i] + ax] < piv) ++i;
+            while (cent[3 * s->order[j] + ax] > piv) --j;
+            if (i <= j) { int x = s->order[i]; s->order[i] = s->order[j]; s->order[j] = x; ++i; --j; }
+        }
+        if (mid <= j) r = j;
+        else if (mid >= i) l = i;
+        else break;
+    }
+    int left = bvh_build_rec(s, lo, mid, cent);
+    int right = bvh_build_rec(s, mid, hi, cent);
+    s->bvh[id].left = left;
+    s->bvh[id].right = right;
+    s->bvh[id].count = 0;
+    return id;
+}
+
+static void scene_prepare(o_scene *s) {
+    if (s->bvh) return;
+    int nt = 0;
+    for (int m = 0; m < s->nmeshes; ++m) nt += s->meshes[m].nt;
+    s->ntris = nt;
+    s->tri_mesh = (int *)malloc(nt * sizeof(int));
+    s->tri_local = (int *)malloc(nt * sizeof(int));
+    s->tp1 = (float *)malloc(3 * (size_t)nt * sizeof(float));
+    s->te1 = (float *)malloc(3 * (size_t)nt * sizeof(float));
+    s->te2 = (float *)malloc(3 * (size_t)nt * sizeof(float));
+    float *cent = (float *)malloc(3 * (size_t)nt * sizeof(float));
+    int g = 0;
+    for (int mi = 0; mi < s->nmeshes; ++mi) {
+        const o_mesh *m = &s->meshes[mi];
+        for (int t = 0; t < m->nt; ++t, ++g) {
+            v3 p1 = ld(m->P, m->idx[3 * t]), p2 = ld(m->P, m->idx[3 * t + 1]), p3 = ld(m->P, m->idx[3 * t + 2]);
+            v3 e1 = sub(p2, p1), e2 = sub(p3, p1);
+            s->tri_mesh[g] = mi;
+            s->tri_local[g] = t;
+            memcpy(&s->tp1[3 * g], &p1, 12);
+            memcpy(&s->te1[3 * g], &e1, 12);
+            memcpy(&s->te2[3 * g], &e2, 12);
+            cent[3 * g] = (p1.x + p2.x + p3.x) / 3.f;
+            cent[3 * g + 1] = (p1.y + p2.y + p3.y) / 3.f;
+            cent[3 * g + 2] = (p1.z + p2.z + p3.z) / 3.f;
+        }
+    }
+    s->order = (int *)malloc(nt * sizeof(int));
+    for (int i = 0; i < nt; ++i) s->order[i] = i;
+    s->bvh = (o_bnode *)malloc((2 * (size_t)nt + 1) * sizeof(o_bnode));
+    s->nbvh = 0;
+    bvh_build_rec(s, 0, nt, cent);
+    free(cent);
+}
+
+static int box_hit(const o_bnode *n, v3 o, v3 inv, float mint, float maxt) {
+    float t0 = mint, t1 = maxt;
+    const float oo[3] = {o.x, o.y, o.z}, ii[3] = {inv.x, inv.y, inv.z};
+    for (int k = 0; k < 3; ++k) {
+        float a = (n->bmin[k] - oo[k]) * ii[k], b = (n->bmax[k] - oo[k]) * ii[k];
+        if (a > b) { float x = a; a = b; b = x; }
+        if (a != a || b != b) continue; /* 0 * inf: axis-parallel ray inside the slab */
+        t0 = a > t0 ? a : t0;
+        t1 = b < t1 ? b : t1;
+        if (t0 > t1) return 0;
+    }
+    return 1;
+}
+
+typedef struct { float t, b1, b2; int tri; v3 lnn; } hit_t; /* tri >= 0 mesh, -1-l light, INT_MIN miss */
+#define NO_HIT (-2147483647 - 1)
+
+static hit_t intersect(const o_scene *s, v3 o, v3 d, float mint, float maxt) {
+    hit_t h;
+    h.tri = NO_HIT;
+    h.t = maxt;
+    v3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    int stack[128], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const o_bnode *n = &s->bvh[stack[--sp]];
+        if (!box_hit(n, o, inv, mint, h.t)) continue;
+        if (n->left < 0) {
+            for (int i = 0; i < n->count; ++i) {
+                int t = s->order[n->first + i];
+                float tt, b1, b2;
+                if (tri_hit(o, d, mint, h.t, ld(s->tp1, t), ld(s->te1, t), ld(s->te2, t), &tt, &b1, &b2)) {
+                    h.t = tt; h.b1 = b1; h.b2 = b2; h.tri = t;
+                }
+            }
+        } else {
+            stack[sp++] = n->right;
+            stack[sp++] = n->left;
+        }
+    }
+    for (int l = 0; l < s->nlights; ++l) {
+        float t;
+        v3 nn;
+        if (sphere_hit(&s->lights[l], o, d, mint, h.t, &t, &nn)) {
+            h.t = t;
+            h.tri = -1 - l;
+            h.lnn = nn;
+        }
+    }
+    return h;
+}
+
+static int occluded(const o_scene *s, v3 o, v3 d, float mint, float maxt) {
+    for (int l = 0; l < s->nlights; ++l) {
+        float t;
+        if (sphere_hit(&s->lights[l], o, d, mint, maxt, &t, NULL)) return 1;
+    }
+    v3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
+    int stack[128], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const o_bnode *n = &s->bvh[stack[--sp]];
+        if (!box_hit(n, o, inv, mint, maxt)) continue;
+        if (n->left < 0) {
+            for (int i = 0; i < n->count; ++i) {
+                int t = s->order[n->first + i];
+                float tt, b1, b2;
+                if (tri_hit(o, d, mint, maxt, ld(s->tp1, t), ld(s->te1, t), ld(s->te2, t), &tt, &b1, &b2)) return 1;
+            }
+        } else {
+            stack[sp++] = n->right;
+            stack[sp++] = n->left;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ tessellation */
+typedef struct { float b0, b1, b2; } bary;
+static const bary CENTROID = {1.f / 3.f, 1.f / 3.f, 1.f / 3.f};
+static bary blerp(float t, bary a, bary b) {
+    bary r = {(1.f - t) * a.b0 + t * b.b0, (1.f - t) * a.b1 + t * b.b1, (1.f - t) * a.b2 + t * b.b2};
+    return r;
+}
+static bary beval(bary s, bary a, bary b, bary c) {
+    bary r = {s.b0 * a.b0 + s.b1 * b.b0 + s.b2 * c.b0, s.b0 * a.b1 + s.b1 * b.b1 + s.b2 * c.b1,
+              s.b0 * a.b2 + s.b1 * b.b2 + s.b2 * c.b2};
+    return r;
+}
+static v3 bpoint(bary s, v3 a, v3 b, v3 c) { return add(add(mul(a, s.b0), mul(b, s.b1)), mul(c, s.b2)); }
+
+typedef struct {
+    const o_mesh *m;
+    int t, incenter;
+    float min_dist;
+    v3 v0, v1, v2;
+    o_surface_point *out;
+    long n, cap;
+} tess_ctx;
+
+static void domain(tess_ctx *c, bary a, bary b, bary d) {
+    v3 s0 = bpoint(a, c->v0, c->v1, c->v2), s1 = bpoint(b, c->v0, c->v1, c->v2), s2 = bpoint(d, c->v0, c->v1, c->v2);
+    bary bc;
+    if (!c->incenter) bc = beval(CENTROID, a, b, d);
+    else {
+        float l0 = len(sub(s1, s2)), l1 = len(sub(s2, s0)), l2 = len(sub(s0, s1));
+        bary bic = {l0 / (l0 + l1 + l2), l1 / (l0 + l1 + l2), l2 / (l0 + l1 + l2)};
+        bc = beval(bic, a, b, d);
+    }
+    if (c->out && c->n < c->cap) {
+        o_surface_point *sp = &c->out[c->n];
+        v3 p = bpoint(bc, c->v0, c->v1, c->v2);
+        frame_t fr = tri_frame(c->m, c->t, p, bc.b0, bc.b1, bc.b2);
+        sp->p[0] = p.x; sp->p[1] = p.y; sp->p[2] = p.z;
+        sp->n[0] = fr.nn.x; sp->n[1] = fr.nn.y; sp->n[2] = fr.nn.z;
+        sp->u = fr.u;
+        sp->v = fr.v;
+        sp->material = (uint32_t)c->m->material;
+        sp->area = .5f * len(crs(sub(s1, s0), sub(s2, s0)));
+        sp->ray_eps = c->min_dist / 10.f;
+    }
+    c->n++;
+}
+
+static void matching(tess_ctx *c, bary b0I, bary b1I, int segsI, bary b0O, bary b1O, int segsO) {
+    int ip = 0, op = 0;
+    while (ip < segsI || op < segsO) {
+        bary bIn = segsI ? blerp((float)ip / segsI, b0I, b1I) : b0I;
+        bary bOut = blerp((float)op / segsO, b0O, b1O);
+        float sIn = (ip < segsI) ? fabsf((float)(ip + 1) + 1.f - (float)op / segsO * (segsI + 2)) : INFINITY;
+        float sOut = (op < segsO) ? fabsf((float)ip + 1.f - (float)(op + 1) / segsO * (segsI + 2)) : INFINITY;
+        if (sIn < sOut) {
+            domain(c, blerp((float)(ip + 1) / segsI, b0I, b1I), bIn, bOut);
+            ip++;
+        } else {
+            domain(c, bIn, bOut, blerp((float)(op + 1) / segsO, b0O, b1O));
+            op++;
+        }
+    }
+}
+
+static int imax(int a, int b) { return a > b ? a : b; }
+
+static void tessellator(tess_ctx *c, float tfe0, float tfe1, float tfe2, float tfc) {
+    int e0 = imax((int)ceilf(tfe0), 1), e1 = imax((int)ceilf(tfe1), 1), e2 = imax((int)ceilf(tfe2), 1);
+    int ic = imax((int)ceilf(tfc), 1);
+    if (e0 > 1 || e1 > 1 || e2 > 1) ic = imax(ic, 2);
+    bary B0 = {1.f, 0.f, 0.f}, B1 = {0.f, 1.f, 0.f}, B2 = {0.f, 0.f, 1.f}, BC = CENTROID;
+    int rings = (ic + 1) / 2;
+    for (int r = 0; r < rings - 1; ++r) {
+        int inner = ic - (rings - r) * 2;
+        if (inner >= 0) {
+            int outer = inner + 2;
+            bary i0 = blerp((float)r / rings, BC, B0), i1 = blerp((float)r / rings, BC, B1),
+                 i2 = blerp((float)r / rings, BC, B2);
+            bary o0 = blerp((float)(r + 1) / rings, BC, B0), o1 = blerp((float)(r + 1) / rings, BC, B1),
+                 o2 = blerp((float)(r + 1) / rings, BC, B2);
+            matching(c, i0, i1, inner, o0, o1, outer);
+            matching(c, i1, i2, inner, o1, o2, outer);
+            matching(c, i2, i0, inner, o2, o0, outer);
+        } else {
+            bary o0 = blerp((float)(r + 1) / rings, BC, B0), o1 = blerp((float)(r + 1) / rings, BC, B1),
+                 o2 = blerp((float)(r + 1) / rings, BC, B2);
+            domain(c, o0, o1, o2);
+        }
+    }
+    int inner = ic - 2;
+    if (inner >= 0) {
+        float t = (float)(rings - 1) / rings;
+        bary i0 = blerp(t, BC, B0), i1 = blerp(t, BC, B1), i2 = blerp(t, BC, B2);
+        matching(c, i0, i1, inner, B0, B1, e2);
+        matching(c, i1, i2, inner, B1, B2, e0);
+        matching(c, i2, i0, inner, B2, B0, e1);
+    } else {
+        domain(c, B0, B1, B2);
+    }
+}
+
+long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_point *out, long cap) {
+    tess_ctx c;
+    memset(&c, 0, sizeof(c));
+    c.out = out;
+    c.cap = cap;
+    c.min_dist = min_dist;
+    c.incenter = incenter;
+    for (int mi = 0; mi < s->nmeshes; ++mi) {
+        const o_mesh *m = &s->meshes[mi];
+        c.m = m;
+        for (int t = 0; t < m->nt; ++t) {
+            c.t = t;
+            c.v0 = ld(m->P, m->idx[3 * t]);
+            c.v1 = ld(m->P, m->idx[3 * t + 1]);
+            c.v2 = ld(m->P, m->idx[3 * t + 2]);
+            float le0 = len(sub(c.v1, c.v2)), le1 = len(sub(c.v2, c.v0)), le2 = len(sub(c.v0, c.v1));
+            float tfe0 = le0 / min_dist * 0.8f, tfe1 = le1 / min_dist * 0.8f, tfe2 = le2 / min_dist * 0.8f;
+            float tfc = floorf((tfe0 + tfe1 + tfe2) / 3.f + .5f);
+            tfe0 = floorf(tfe0 + .5f);
+            tfe1 = floorf(tfe1 + .5f);
+            tfe2 = floorf(tfe2 + .5f);
+            tessellator(&c, tfe0, tfe1, tfe2, tfc);
+        }
+    }
+    return c.n;
+}
+
+/* ------------------------------------------------------------------ irradiance (IrradianceTask) */
+typedef struct {
+    o_scene *s;
+    const o_surface_point *pts;
+    int n, nthreads, tid;
+    uint32_t seed;
+    float *E;
+} irr_job;
+
+static void *irr_worker(void *arg) {
+    irr_job *j = (irr_job *)arg;
+    const o_scene *s = j->s;
+    for (int i = j->tid; i < j->n; i += j->nthreads) {
+        const o_surface_point *sp = &j->pts[i];
+        v3 p = mk(sp->p[0], sp->p[1], sp->p[2]), n = mk(sp->n[0], sp->n[1], sp->n[2]);
+        const o_mat *mat = sp->material < (uint32_t)s->nmats ? &s->mats[sp->material] : NULL;
+        float E[O_NB];
+        for (int c = 0; c < O_NB; ++c) E[c] = 0.f;
+        for (int l = 0; l < s->nlights; ++l) {
+            const o_light *L = &s->lights[l];
+            float El[O_NB];
+            for (int c = 0; c < O_NB; ++c) El[c] = 0.f;
+            int ns = L->ns_pow2;
+            uint32_t sc0 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS);
+            uint32_t sc1 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS + 8u);
+            for (int k = 0; k < ns; ++k) {
+                lsamp ls = light_sample(L, p, sp->ray_eps, vdc((uint32_t)k, sc0), sobol((uint32_t)k, sc1));
+                if (dot(ls.wi, n) <= 0.f) continue;
+                if (!ls.nonblack || ls.pdf == 0.f) continue;
+                if (!occluded(s, ls.so, ls.sd, ls.smint, ls.smaxt)) {
+                    float ct = absdot(ls.wi, n);
+                    ct = ct < 1.f ? ct : 1.f;
+                    float Ft = mat ? 1.f - rho_at(mat, ct) : 1.f;
+                    for (int c = 0; c < O_NB; ++c) El[c] += Ft * L->Le[c] * ct / ls.pdf;
+                }
+            }
+            for (int c = 0; c < O_NB; ++c) E[c] += El[c] / (float)ns;
+        }
+        if (mat)
+            for (int c = 0; c < O_NB; ++c) E[c] *= mat->alb_mix[c];
+        memcpy(&j->E[(size_t)i * O_NB], E, sizeof(E));
+    }
+    return NULL;
+}
+
+static void run_threads(void *(*fn)(void *), void *jobs, size_t job_size, int nthreads) {
+    pthread_t *th = (pthread_t *)malloc(nthreads * sizeof(pthread_t));
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, fn, (char *)jobs + t * job_size);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(th);
+}
+
+void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E) {
+    scene_prepare(s);
+    if (nthreads < 1) nthreads = 1;
+    irr_job *jobs = (irr_job *)malloc(nthreads * sizeof(irr_job));
+    for (int t = 0; t < nthreads; ++t) {
+        irr_job j = {s, pts, n, nthreads, t, seed, E};
+        jobs[t] = j;
+    }
+    run_threads(irr_worker, jobs, sizeof(irr_job), nthreads);
+    free(jobs);
+}
+
+void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nr, const float *E, const float *area,
+                        float max_error) {
+    if (s->octree) o_octree_free(s->octree);
+    s->octree = n > 0 ? o_octree_build(n, p, nr, E, area) : NULL;
+    s->max_error = max_error;
+}
+
+/* ------------------------------------------------------------------ Li per camera sample */
+static void to_xyz(const float L[O_NB], float xyz[3]) { /* Spectrum::ToXYZ + sample filter */
+    static const float cx[O_NB] = MPSS_BAND_CIE_X_INIT, cy[O_NB] = MPSS_BAND_CIE_Y_INIT,
+                       cz[O_NB] = MPSS_BAND_CIE_Z_INIT;
+    float X = 0.f, Y = 0.f, Z = 0.f;
+    int nan = 0;
+    for (int c = 0; c < O_NB; ++c) {
+        if (L[c] != L[c]) nan = 1;
+        X += cx[c] * L[c];
+        Y += cy[c] * L[c];
+        Z += cz[c] * L[c];
+    }
+    float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * O_NB);
+    float y = Y * (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * O_NB);
+    X *= scale; Y *= scale; Z *= scale;
+    if (nan || y < -1e-5f || isinf(y)) X = Y = Z = 0.f; /* samplerrenderer.cpp:119-133 */
+    xyz[0] = X; xyz[1] = Y; xyz[2] = Z;
+}
+
+static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, int si, float X, float Y,
+                      float xyz[3]) {
+    const uint32_t pix = (uint32_t)py * (uint32_t)s->xres + (uint32_t)px;
+    float L[O_NB];
+    for (int c = 0; c < O_NB; ++c) L[c] = 0.f;
+    v3 pcam = xpoint(s->r2c, mk(X, Y, 0.f));
+    v3 dcam = nrm(pcam);
+    v3 o = xpoint(s->c2w, mk(0.f, 0.f, 0.f));
+    v3 d = xvector(s->c2w, dcam);
+    hit_t h = intersect(s, o, d, 0.f, INFINITY);
+    if (h.tri == NO_HIT) { to_xyz(L, xyz); return; }
+    if (h.tri < 0) { /* an area light's own surface: emitted radiance only */
+        const o_light *Lt = &s->lights[-1 - h.tri];
+        if (dot(h.lnn, neg(d)) > 0.f)
+            for (int c = 0; c < O_NB; ++c) L[c] += Lt->Le[c];
+        to_xyz(L, xyz);
+        return;
+    }
+    const int mi = s->tri_mesh[h.tri], lt = s->tri_local[h.tri];
+    const o_mesh *mesh = &s->meshes[mi];
+    const o_mat *mat = &s->mats[mesh->material];
+    v3 p = add(o, mul(d, h.t));
+    float reps = 1e-3f * h.t;
+    frame_t fr = tri_frame(mesh, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
+    v3 wo = neg(d);
+    /* Mo() term (multipolesubsurface.cpp:268-290) */
+    if (s->octree) {
+        float q[3] = {fr.p.x, fr.p.y, fr.p.z}, mo[O_NB];
+        o_mo_batch(s->octree, 1, q, mat->rd, mat->L, mat->rcp, s->max_error, mo, NULL, NULL, 1);
+        float ct = absdot(wo, fr.nn);
+        ct = ct < 1.f ? ct : 1.f;
+        float Ft = mat->is_mc ? 1.f : 1.f - rho_at(mat, ct);
+        for (int c = 0; c < O_NB; ++c) {
+            float t = ((INV_PI_F * Ft) * mo[c]) * mat->alb_1mmix[c];
+            L[c] += t < 0.f ? 0.f : t;
+        }
+    }
+    /* UniformSampleAllLights -> EstimateDirect (integrator.cpp:47-174) */
+    float ld[O_NB];
+    for (int c = 0; c < O_NB; ++c) ld[c] = 0.f;
+    for (int l = 0; l < s->nlights; ++l) {
+        const o_light *Lt = &s->lights[l];
+        const int ns = Lt->ns_pow2;
+        float Ld[O_NB];
+        for (int c = 0; c < O_NB; ++c) Ld[c] = 0.f;
+        uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + D_PERM) & (uint32_t)(spp - 1)) : 0u;
+        uint32_t base = (uint32_t)(si ^ xr) * (uint32_t)ns;
+        uint32_t a0 = hash3(seed, pix, 16u * l + D_LIGHT_POS), a1 = hash3(seed, pix, 16u * l + D_LIGHT_POS + 8u);
+        uint32_t b0 = hash3(seed, pix, 16u * l + D_BSDF_DIR), b1 = hash3(seed, pix, 16u * l + D_BSDF_DIR + 8u);
+        for (int j = 0; j < ns; ++j) {
+            uint32_t k = base + (uint32_t)j;
+            float ed[O_NB], f[O_NB];
+            for (int c = 0; c < O_NB; ++c) ed[c] = 0.f;
+            lsamp ls = light_sample(Lt, fr.p, reps, vdc(k, a0), sobol(k, a1));
+            float lightPdf = ls.pdf;
+            if (lightPdf > 0.f && ls.nonblack) {
+                if (bsdf_f(mat, &fr, wo, ls.wi, to_local(&fr, wo), to_local(&fr, ls.wi), f) &&
+                    !occluded(s, ls.so, ls.sd, ls.smint, ls.smaxt)) {
+                    float bsdfPdf = mf_pdf(mat, to_local(&fr, wo), to_local(&fr, ls.wi));
+                    float w = power_h(lightPdf, bsdfPdf);
+                    float k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
+                    for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Lt->Le[c] * k1;
+                }
+            }
+            if (mat->has_refl) {
+                v3 wil;
+                float bsdfPdf;
+                mf_sample(mat, to_local(&fr, wo), vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
+                if (bsdfPdf != 0.f) {
+                    v3 wi = to_world(&fr, wil);
+                    if (bsdf_f(mat, &fr, wo, wi, to_local(&fr, wo), wil, f) && bsdfPdf > 0.f) {
+                        lightPdf = light_pdf(Lt, fr.p, wi);
+                        if (lightPdf != 0.f) {
+                            float w = power_h(bsdfPdf, lightPdf);
+                            hit_t hl = intersect(s, fr.p, wi, reps, INFINITY);
+                            if (hl.tri == -1 - l && dot(hl.lnn, neg(wi)) > 0.f) {
+                                float adn = absdot(wi, fr.nn);
+                                for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Lt->Le[c] * adn * w / bsdfPdf;
+                            }
+                        }
+                    }
+                }
+            }
+            for (int c = 0; c < O_NB; ++c) Ld[c] += ed[c];
+        }
+        for (int c = 0; c < O_NB; ++c) ld[c] += Ld[c] / (float)ns;
+    }
+    for (int c = 0; c < O_NB; ++c) L[c] += ld[c];
+    to_xyz(L, xyz);
+}
+
+/* ImageFilm::AddSample pixel range of one coordinate (0.5-wide box filter) */
+static void extent(float X, int res, int *lo, int *hi) {
+    float d = X - 0.5f;
+    *lo = (int)ceilf(d - 0.5f);
+    *hi = (int)floorf(d + 0.5f);
+    if (*lo < 0) *lo = 0;
+    if (*hi > res - 1) *hi = res - 1;
+}
+
+typedef struct {
+    const o_scene *s;
+    int spp, x0, x1, y0, y1, nthreads, tid;
+    uint32_t seed;
+    float *out;
+} tile_job;
+
+/* One pixel: its own samples, then neighbours' samples whose rounded image position lands
+ * on the shared edge, neighbours in row-major order (matches the product's film order). */
+static void render_pixel(const tile_job *j, int px, int py, float *o4) {
+    const o_scene *s = j->s;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < 9; ++q) {
+        int idx = q == 0 ? 4 : (q - 1 + (q > 4));
+        int dx = idx % 3 - 1, dy = idx / 3 - 1;
+        int qx = px + dx, qy = py + dy;
+        if (qx < 0 || qy < 0 || qx >= s->xres || qy >= s->yres) continue;
+        uint32_t pix = (uint32_t)qy * (uint32_t)s->xres + (uint32_t)qx;
+        uint32_t su = hash3(j->seed, pix, D_IMAGE), sv = hash3(j->seed, pix, D_IMAGE + 1);
+        for (int si = 0; si < j->spp; ++si) {
+            float X = (float)qx + vdc((uint32_t)si, su), Y = (float)qy + sobol((uint32_t)si, sv);
+            int lx, hx, ly, hy;
+            extent(X, s->xres, &lx, &hx);
+            extent(Y, s->yres, &ly, &hy);
+            if (px < lx || px > hx || py < ly || py > hy) continue;
+            float xyz[3];
+            sample_li(s, j->spp, j->seed, qx, qy, si, X, Y, xyz);
+            acc[0] += 1.f * xyz[0];
+            acc[1] += 1.f * xyz[1];
+            acc[2] += 1.f * xyz[2];
+            acc[3] += 1.f;
+        }
+    }
+    memcpy(o4, acc, sizeof(acc));
+}
+
+static void *tile_worker(void *arg) {
+    tile_job *j = (tile_job *)arg;
+    int tw = j->x1 - j->x0, th = j->y1 - j->y0;
+    for (int i = j->tid; i < tw * th; i += j->nthreads) {
+        int px = j->x0 + i % tw, py = j->y0 + i / tw;
+        render_pixel(j, px, py, &j->out[(size_t)i * 4]);
+    }
+    return NULL;
+}
+
+void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw) {
+    scene_prepare(s);
+    if (nthreads < 1) nthreads = 1;
+    tile_job *jobs = (tile_job *)malloc(nthreads * sizeof(tile_job));
+    for (int t = 0; t < nthreads; ++t) {
+        tile_job j = {s, spp, x0, x1, y0, y1, nthreads, t, seed, xyzw};
+        jobs[t] = j;
+    }
+    run_threads(tile_worker, jobs, sizeof(tile_job), nthreads);
+    free(jobs);
+}
+
+void o_scene_free(o_scene *s) {
+    if (!s) return;
+    for (int m = 0; m < s->nmeshes; ++m) {
+        free(s->meshes[m].P); free(s->meshes[m].N); free(s->meshes[m].S); free(s->meshes[m].uv);
+        free(s->meshes[m].idx);
+    }
+    for (int m = 0; m < s->nmats; ++m) { free(s->mats[m].rho); free(s->mats[m].rd); }
+    free(s->meshes); free(s->lights); free(s->mats);
+    free(s->tri_mesh); free(s->tri_local); free(s->tp1); free(s->te1); free(s->te2);
+    free(s->bvh); free(s->order);
+    if (s->octree) o_octree_free(s->octree);
+    free(s);
+}

@@ -9,6 +9,17 @@ namespace mpss {
 
 MPSS_HD float lerpf_t(float t, float a, float b) { return (1.f - t) * a + t * b; }  // pbrt.h:250
 
+// Pixel range [lo, hi] one image-sample coordinate reaches through the 0.5-wide box filter
+// (ImageFilm::AddSample, film/image.cpp:77-96: dImage = X - 0.5; [Ceil(d - .5), Floor(d + .5)],
+// clamped to the film).
+MPSS_HD void film_extent(float X, int res, int &lo, int &hi) {
+    const float d = X - 0.5f;
+    lo = (int)ceilf(d - 0.5f);
+    hi = (int)floorf(d + 0.5f);
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > res - 1 ? res - 1 : hi;
+}
+
 // Raw (device-friendly) view of one triangle mesh.
 struct MeshView {
     const float *P, *N, *S, *uv;  // N, S, uv may be null

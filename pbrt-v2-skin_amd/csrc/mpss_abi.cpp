@@ -238,6 +238,35 @@ int mpss_render_tile(mpss_ctx *c, int spp, uint32_t seed, int x0, int x1, int y0
 // ---------------------------------------------------------------- host-side utilities
 extern "C" {
 
+int mpss_host_tessellate(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
+                         const int32_t *idx, const float *o2w, const float *w2o, int flip, uint32_t mat,
+                         float min_dist, int incenter, void *rec, uint32_t *n) {
+    return guarded([&] {
+        require(P && idx && o2w && w2o && n && nv > 0 && min_dist > 0.f, "mpss_host_tessellate: bad argument");
+        SceneData sd;
+        Mesh m;
+        m.P.assign(P, P + 3 * (size_t)nv);
+        if (N) m.N.assign(N, N + 3 * (size_t)nv);
+        if (S) m.S.assign(S, S + 3 * (size_t)nv);
+        if (uv) m.uv.assign(uv, uv + 2 * (size_t)nv);
+        m.idx.assign(idx, idx + 3 * (size_t)nt);
+        for (int32_t v : m.idx) require(v >= 0 && (uint32_t)v < nv, "mpss_host_tessellate: index out of range");
+        memcpy(m.o2w, o2w, sizeof(m.o2w));
+        memcpy(m.w2o, w2o, sizeof(m.w2o));
+        m.reverse_orientation = flip != 0;
+        m.swaps_handedness = false;
+        m.material = mat;
+        sd.meshes.push_back(std::move(m));
+        std::vector<SurfacePoint> pts;
+        tessellate_surface_points(sd, min_dist, incenter != 0, pts);
+        if (rec) {
+            require(*n >= pts.size(), "mpss_host_tessellate: records buffer too small");
+            memcpy(rec, pts.data(), pts.size() * sizeof(SurfacePoint));
+        }
+        *n = (uint32_t)pts.size();
+    });
+}
+
 int mpss_host_from_rgb(const float *rgb, int illuminant, float *out) {
     return guarded([&] {
         require(rgb && out, "mpss_host_from_rgb: null argument");

@@ -43,10 +43,11 @@ struct RenderScene {
     float raster_to_camera[16], camera_to_world[16];
 };
 
-// A tile [x0,x1) x [y0,y1) extended by one column/row (ew x eh pixels) for samples that
-// land exactly on a pixel edge (film_kernel).
+// A tile [x0,x1) x [y0,y1) extended by one pixel on every side that exists (origin ex0, ey0;
+// ew x eh pixels): a sample whose float image coordinate rounds onto a pixel edge also lands
+// in the neighbouring pixel (film_kernel).
 struct TileBatch {
-    int x0, x1, y0, y1, ew, eh, spp;
+    int x0, x1, y0, y1, ex0, ey0, ew, eh, spp;
     uint32_t seed;
     int64_t nsamples;  // ew * eh * spp
 };
@@ -74,6 +75,6 @@ template <bool COUNT>
 __global__ void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples, int nblocks,
                              int have_octree, unsigned long long *counts);
 __global__ void film_kernel(TileBatch tb, const uint32_t *flags, const float *xyz, float *out, int out_stride_px,
-                            int xres);
+                            int xres, int yres);
 
 }  // namespace mpss

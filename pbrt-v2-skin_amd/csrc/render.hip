@@ -225,25 +225,24 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
     if (sid >= tb.nsamples) return;
     const int s = (int)(sid % tb.spp);
     const int li = (int)(sid / tb.spp);
-    const int px = tb.x0 + li % tb.ew, py = tb.y0 + li / tb.ew;
+    const int px = tb.ex0 + li % tb.ew, py = tb.ey0 + li / tb.ew;
     const uint32_t pix = (uint32_t)py * (uint32_t)sc.xres + (uint32_t)px;
-    // image sample (LDPixelSample's imageSamples, montecarlo.cpp:200-250)
-    const float u = van_der_corput((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE));
-    const float v = sobol2((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE + 1));
-    // samples of the extra column/row only matter when they spill into the tile (film_kernel)
-    const bool inside = px < tb.x1 && py < tb.y1;
-    const bool spill = (px == tb.x1 && u == 0.f) || (py == tb.y1 && v == 0.f);
-    const bool live = px < tb.x1 ? (py < tb.y1 || v == 0.f) : (u == 0.f && (py < tb.y1 || v == 0.f));
+    // image sample (LDPixelSample's imageSamples, montecarlo.cpp:200-250): imageX = x + u in float
+    const float X = (float)px + van_der_corput((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE));
+    const float Y = (float)py + sobol2((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE + 1));
+    // border samples matter only when the box filter carries them into the tile (film_kernel)
+    int lx, hx, ly, hy;
+    film_extent(X, sc.xres, lx, hx);
+    film_extent(Y, sc.yres, ly, hy);
+    const bool live = lx < tb.x1 && hx >= tb.x0 && ly < tb.y1 && hy >= tb.y0;
     uint32_t flags = 0;
     float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
     float ld[NB];
     for (int c = 0; c < NB; ++c) ld[c] = 0.f;
-    (void)inside;
-    (void)spill;
     if (live) {
         flags |= REC_LIVE;
         // PerspectiveCamera::GenerateRay (cameras/perspective.cpp)
-        const V3 pras = V3{(float)px + u, (float)py + v, 0.f};
+        const V3 pras = V3{X, Y, 0.f};
         const V3 pcam = xform_point(sc.raster_to_camera, pras);
         const V3 dcam = normalize(pcam);
         const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
@@ -440,25 +439,34 @@ template __global__ void shade_kernel<true>(RenderScene, PacketTree, SampleRecs,
 // ------------------------------------------------------------------ film
 __global__ __launch_bounds__(256) void film_kernel(TileBatch tb, const uint32_t *__restrict__ flags,
                                                    const float *__restrict__ xyz, float *__restrict__ out,
-                                                   int out_stride_px, int xres) {
+                                                   int out_stride_px, int xres, int yres) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int tw = tb.x1 - tb.x0, th = tb.y1 - tb.y0;
     if (i >= tw * th) return;
     const int px = tb.x0 + i % tw, py = tb.y0 + i / tw;
     float X = 0.f, Y = 0.f, Z = 0.f, W = 0.f;
-    // own samples, then the right, lower and diagonal neighbours' samples that sit exactly on
-    // this pixel's far edge (ImageFilm::AddSample extent with xWidth = 0.5, image.cpp:77-137)
-    const int nb[4][2] = {{0, 0}, {1, 0}, {0, 1}, {1, 1}};
-    for (int q = 0; q < 4; ++q) {
-        const int qx = px + nb[q][0], qy = py + nb[q][1];
-        if (qx >= tb.x0 + tb.ew || qy >= tb.y0 + tb.eh) continue;
-        const int64_t li = (int64_t)(qy - tb.y0) * tb.ew + (qx - tb.x0);
+    // own samples (always inside this pixel's filter support), then the 8 neighbours' samples
+    // in row-major order whose float image position rounds onto the shared edge
+    // (ImageFilm::AddSample with the 0.5-wide box filter, image.cpp:77-137)
+    for (int q = 0; q < 9; ++q) {
+        const int dx = q == 0 ? 0 : ((q - 1 + (q > 4)) % 3) - 1;
+        const int dy = q == 0 ? 0 : ((q - 1 + (q > 4)) / 3) - 1;
+        const int qx = px + dx, qy = py + dy;
+        if (qx < tb.ex0 || qy < tb.ey0 || qx >= tb.ex0 + tb.ew || qy >= tb.ey0 + tb.eh) continue;
+        const int64_t li = (int64_t)(qy - tb.ey0) * tb.ew + (qx - tb.ex0);
         const uint32_t pix = (uint32_t)qy * (uint32_t)xres + (uint32_t)qx;
         const uint32_t su = hash3(tb.seed, pix, DIM_IMAGE), sv = hash3(tb.seed, pix, DIM_IMAGE + 1);
         for (int s = 0; s < tb.spp; ++s) {
             if (q > 0) {
-                const float u = van_der_corput((uint32_t)s, su), v = sobol2((uint32_t)s, sv);
-                if ((nb[q][0] && u != 0.f) || (nb[q][1] && v != 0.f)) continue;
+                int lo, hi;
+                if (dx != 0) {
+                    film_extent((float)qx + van_der_corput((uint32_t)s, su), xres, lo, hi);
+                    if (px < lo || px > hi) continue;
+                }
+                if (dy != 0) {
+                    film_extent((float)qy + sobol2((uint32_t)s, sv), yres, lo, hi);
+                    if (py < lo || py > hi) continue;
+                }
             }
             const int64_t sid = li * tb.spp + s;
             const float *x = xyz + (size_t)sid * 3;

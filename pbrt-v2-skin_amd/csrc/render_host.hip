@@ -244,9 +244,10 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
     }
     const RenderScene sc = render_scene();
     const int tw = x1 - x0;
-    const int ew = tw + (x1 < W ? 1 : 0);
+    const int ex0 = std::max(x0 - 1, 0);
+    const int ew = std::min(x1 + 1, W) - ex0;
     const int64_t max_samples = 1 << 21;
-    int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp));
+    int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp) - 2);
     for (int yb = y0; yb < y1; yb += rows) {
         const int ye = std::min(y1, yb + rows);
         TileBatch tb;
@@ -254,8 +255,10 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
         tb.x1 = x1;
         tb.y0 = yb;
         tb.y1 = ye;
+        tb.ex0 = ex0;
+        tb.ey0 = std::max(yb - 1, 0);
         tb.ew = ew;
-        tb.eh = (ye - yb) + (ye < H ? 1 : 0);
+        tb.eh = std::min(ye + 1, H) - tb.ey0;
         tb.spp = spp;
         tb.seed = seed;
         tb.nsamples = (int64_t)tb.ew * tb.eh * spp;
@@ -290,7 +293,7 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
         const int npx = tw * (ye - yb);
         time_begin(stream, ev);
         hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, tb, ws_flags_.ptr,
-                           ws_xyz_.ptr, out + (size_t)(yb - y0) * tw * 4, tw, W);
+                           ws_xyz_.ptr, out + (size_t)(yb - y0) * tw * 4, tw, W, H);
         time_end(stream, ev, 3);
         MPSS_HIP(hipGetLastError());
         stats_.samples += tb.nsamples;

@@ -92,6 +92,8 @@ _sig("mpss_reset_render_stats", C.c_int, [vp])
 _sig("mpss_set_instrumentation", C.c_int, [vp, C.c_int, C.c_int])
 _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
 _sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
+_sig("mpss_host_tessellate", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32,
+                                       C.c_float, C.c_int, vp, u32p])
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
@@ -150,6 +152,20 @@ assert SURFACE_POINT.itemsize == 44
 def host_from_rgb(rgb, illuminant=False):
     out = np.zeros(NB, np.float32)
     check(_lib.mpss_host_from_rgb(np.ascontiguousarray(rgb, np.float32), int(illuminant), out))
+    return out
+
+
+def host_tessellate(P, idx, o2w, w2o, min_dist, N=None, S=None, uv=None, flip=False, material=0, incenter=False):
+    P = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
+    idx = np.ascontiguousarray(idx, np.int32).reshape(-1, 3)
+    opt = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (N, S, uv)]
+    args = [len(P), P] + [None if a is None else a.ctypes.data for a in opt] + \
+        [len(idx), idx.ctypes.data_as(C.POINTER(C.c_int32)), np.ascontiguousarray(o2w, np.float32),
+         np.ascontiguousarray(w2o, np.float32), int(flip), material, min_dist, int(incenter)]
+    n = C.c_uint32(0)
+    check(_lib.mpss_host_tessellate(*args, None, C.byref(n)))
+    out = np.zeros(n.value, SURFACE_POINT)
+    check(_lib.mpss_host_tessellate(*args, out.ctypes.data, C.byref(n)))
     return out
 
 

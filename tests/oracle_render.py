@@ -1,0 +1,165 @@
+"""ctypes front-end to the oracle's per-pixel path (oracle/render.c).
+
+TEST INFRASTRUCTURE ONLY: used by tests/ as the parity checker and by bench.py's
+cpu_baseline leg; never by the product package.
+"""
+import ctypes as C
+import os
+import time
+
+import numpy as np
+
+import oracle_lib
+
+NB = 30
+f32p = oracle_lib.f32p
+vp = C.c_void_p
+
+SURFACE_POINT = np.dtype([("p", "<f4", 3), ("n", "<f4", 3), ("u", "<f4"), ("v", "<f4"), ("material", "<u4"),
+                          ("area", "<f4"), ("ray_eps", "<f4")])
+
+
+def _lib():
+    L = oracle_lib.lib()
+    if getattr(L, "_render_sigs", False):
+        return L
+    L.o_scene_create.restype = vp
+    L.o_scene_create.argtypes = [C.c_int, C.c_int, f32p, f32p]
+    L.o_scene_add_material.restype = C.c_int
+    L.o_scene_add_material.argtypes = [vp, f32p, f32p, C.c_float, C.c_float, C.c_float, C.c_int, f32p, C.c_int,
+                                       C.c_int, f32p, C.c_int, f32p]
+    L.o_scene_add_mesh.restype = C.c_int
+    L.o_scene_add_mesh.argtypes = [vp, C.c_int, f32p, vp, vp, vp, C.c_int, oracle_lib.i32p, f32p, f32p, C.c_int,
+                                   C.c_int]
+    L.o_scene_add_sphere_light.restype = C.c_int
+    L.o_scene_add_sphere_light.argtypes = [vp, f32p, C.c_float, f32p, C.c_int]
+    L.o_tessellate.restype = C.c_long
+    L.o_tessellate.argtypes = [vp, C.c_float, C.c_int, vp, C.c_long]
+    L.o_irradiance.argtypes = [vp, C.c_int, vp, C.c_uint32, C.c_int, f32p]
+    L.o_scene_set_octree.argtypes = [vp, C.c_int, f32p, f32p, f32p, f32p, C.c_float]
+    L.o_render_tile.argtypes = [vp, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p]
+    L.o_scene_free.argtypes = [vp]
+    L._render_sigs = True
+    return L
+
+
+def _opt(a):
+    return None if a is None else np.ascontiguousarray(a, np.float32)
+
+
+def tables_from_ctx(ctx, n):
+    return [ctx.material_tables(i)[:3] for i in range(n)]
+
+
+def tables_from_host(sc, mpss):
+    """Material tables from the product's host builders (CPU only; no device needed)."""
+    out = []
+    for m in sc.materials:
+        kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
+        skin = mpss.default_skin(**kw)
+        tab, rcp, _ = mpss.host_build_profile(*mpss.host_skin_layers(skin), desired_length=skin.desired_length,
+                                              lerp=bool(skin.lerp_on_thin_slab))
+        rho, _ = mpss.host_rho_table(skin.roughness, skin.layer_ior[0], double_ref_sslf=bool(skin.double_ref_sslf))
+        out.append((tab, rcp, rho))
+    return out
+
+
+class OracleScene:
+    """The oracle's copy of a pbrtscene.Scene. Material tables (Rd profile, rho_hd) come
+    from the product (its context or its host builders), so this checks the per-pixel path
+    in isolation; the tables themselves are checked against the oracle in
+    test_host_parity.py. cfg: an mpss.Config (or anything with the same fields)."""
+
+    def __init__(self, sc, tables, cfg, mpss):
+        L = _lib()
+        r2c, c2w = sc.raster_to_camera()
+        self.sc = sc
+        self.h = L.o_scene_create(sc.xres, sc.yres, np.ascontiguousarray(r2c, np.float32),
+                                  np.ascontiguousarray(c2w, np.float32))
+        self._keep = []
+        for mid, m in enumerate(sc.materials):
+            kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
+            skin = mpss.default_skin(**kw)
+            Kr = mpss.host_from_rgb(m["Kr"]) if "Kr" in m else np.ones(NB, np.float32)
+            alb = mpss.host_from_rgb(m["albedo"]) if "albedo" in m else np.ones(NB, np.float32)
+            tab, rcp, rho = tables[mid]
+            L.o_scene_add_material(self.h, Kr, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
+                                   int(skin.double_ref_sslf), rho, len(rho), 0,
+                                   np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
+        for me in sc.meshes:
+            N, S, uv = _opt(me["N"]), _opt(me["S"]), _opt(me["uv"])
+            self._keep += [N, S, uv]
+            det = np.linalg.det(me["o2w"][:3, :3].astype(np.float64))
+            flip = int(bool(me["reverse"]) ^ bool(det < 0))
+            L.o_scene_add_mesh(self.h, len(me["P"]), np.ascontiguousarray(me["P"], np.float32),
+                               None if N is None else N.ctypes.data, None if S is None else S.ctypes.data,
+                               None if uv is None else uv.ctypes.data, len(me["indices"]),
+                               np.ascontiguousarray(me["indices"], np.int32), me["o2w"], me["w2o"], flip,
+                               me["material"])
+        for li in sc.lights:
+            ns = li["nsamples"] if not cfg.quick_render else max(1, li["nsamples"] // 4)
+            L.o_scene_add_sphere_light(self.h, np.ascontiguousarray(li["center"], np.float32), li["radius"],
+                                       mpss.host_from_rgb(li["L"]), ns)
+        self.max_error = cfg.max_error * (4 if cfg.quick_render else 1)
+        self.min_dist = cfg.min_sample_distance * (4 if cfg.quick_render else 1)
+
+    def close(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib().o_scene_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def tessellate(self, incenter=False):
+        L = _lib()
+        n = L.o_tessellate(self.h, self.min_dist, int(incenter), None, 0)
+        out = np.zeros(n, SURFACE_POINT)
+        L.o_tessellate(self.h, self.min_dist, int(incenter), out.ctypes.data, n)
+        return out
+
+    def irradiance(self, pts, seed, nthreads=None):
+        pts = np.ascontiguousarray(pts, SURFACE_POINT)
+        E = np.zeros((len(pts), NB), np.float32)
+        _lib().o_irradiance(self.h, len(pts), pts.ctypes.data, seed, nthreads or os.cpu_count(), E)
+        return E
+
+    def set_octree(self, pts, E):
+        p = np.ascontiguousarray(pts["p"], np.float32)
+        n = np.ascontiguousarray(pts["n"], np.float32)
+        a = np.ascontiguousarray(pts["area"], np.float32)
+        _lib().o_scene_set_octree(self.h, len(pts), p, n, np.ascontiguousarray(E, np.float32), a, self.max_error)
+
+    def render_tile(self, spp, seed, x0, x1, y0, y1, nthreads=None):
+        out = np.zeros(((y1 - y0) * (x1 - x0) * 4,), np.float32)
+        _lib().o_render_tile(self.h, spp, seed, x0, x1, y0, y1, nthreads or os.cpu_count(), out)
+        return out.reshape(y1 - y0, x1 - x0, 4)
+
+
+def time_cpu_baseline(sc, ctx, spp, seed, seconds, nthreads=None):
+    """Time the oracle's pixel loop on a bounded, frame-representative sample: 16x16 tiles
+    visited in a fixed pseudo-random order over the whole frame, using the product's
+    Preprocess outputs (surface points + irradiance) for the octree."""
+    import mpss
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    osc = OracleScene(sc, tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    osc.set_octree(ctx.surface_points(), ctx.irradiance())
+    T = 16
+    tiles = [(x, y) for y in range(0, sc.yres, T) for x in range(0, sc.xres, T)]
+    rng = np.random.default_rng(1234)
+    order = rng.permutation(len(tiles))
+    px = ntiles = 0
+    t0 = time.perf_counter()
+    for k in order:
+        x, y = tiles[k]
+        x1, y1 = min(x + T, sc.xres), min(y + T, sc.yres)
+        osc.render_tile(spp, seed, x, x1, y, y1, nthreads)
+        px += (x1 - x) * (y1 - y)
+        ntiles += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    dt = time.perf_counter() - t0
+    osc.close()
+    return {"value": round(px * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": nthreads, "kind": "port",
+            "sample": "%d of %d 16x16 tiles (%d px x %d spp) of the same frame in fixed random order, %.1f s, "
+                      "oracle/render.c (scalar C restatement, pthreads)" % (ntiles, len(tiles), px, spp, dt)}
