@@ -23,7 +23,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-skin_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
-MO_BYTES_PER_RECORD = 136  # position 12 + area 4 + 30-band E/Et 120
+# SURVEY.md §8d algorithmic bytes per octree record read by the Mo() gather: position 12 +
+# area 4 + 4 bytes per band of E/Et. The sharded kernel reads each record once per band group
+# (16 + 4 * bands_in_group bytes), so a step's bytes are summed over groups.
+REC_HDR_BYTES = 16
 
 
 def parse():
@@ -120,14 +123,16 @@ def main():
     samples_per_step = frames * sc.xres * sc.yres * sc.spp
     value = samples_per_step * a.steps / dt / 1e6
     # dominant kernel + Mo gather roofline (per-launch averages over the timed region)
-    kern = {"camera_direct": (st["ms_camera"], st["n_camera"]), "shade_mo": (st["ms_shade"], st["n_shade"]),
+    kern = {"camera_direct": (st["ms_camera"], st["n_camera"]), "mo_band": (st["ms_shade"], st["n_shade"]),
             "film": (st["ms_film"], st["n_film"])}
     dom = max(kern, key=lambda k: kern[k][0])
-    mo_bytes_step = MO_BYTES_PER_RECORD * (cnt["mo_nodes"] + cnt["mo_points"])   # this rank, one step
+    nbands = [sum(1 for c in grp if c >= 0) for grp in cnt["group_bands"]]
+    mo_bytes_step = sum((cnt["group_nodes"][g] + cnt["group_points"][g]) * (REC_HDR_BYTES + 4 * nbands[g])
+                        for g in range(8))  # this rank, one step
     shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
-    roofline = {"kernel": "shade_kernel (Mo gather)", "bound": "hbm", "achieved": round(mo_gbs, 1),
+    roofline = {"kernel": "mo_band_kernel (Mo gather, spectrally sharded)", "bound": "hbm", "achieved": round(mo_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(mo_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
                 "dominant_kernel": dom,
@@ -147,8 +152,9 @@ def main():
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3),
                            "mo_gbs": round(mo_gbs, 1), "mo_sss_samples": cnt["sss_samples"],
-                           "mo_records_per_sss_sample": round((cnt["mo_nodes"] + cnt["mo_points"]) /
-                                                              max(1, cnt["sss_samples"]), 2)},
+                           "mo_record_visits_per_sss_sample": round((cnt["mo_nodes"] + cnt["mo_points"]) /
+                                                                    max(1, cnt["sss_samples"]), 2),
+                           "mo_group_visits": [a + b for a, b in zip(cnt["group_nodes"], cnt["group_points"])]},
                 "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if a.out and rank == 0:

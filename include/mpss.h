@@ -56,8 +56,10 @@ typedef struct {
     int show_irradiance_points;/* "showirradiancepoints" = false */
     int incenter;              /* "incenter" = false */
     int quick_render;          /* PbrtOptions.quickRender: maxError *= 4, minDist *= 4 */
-    int exact_mo;              /* 1: Mo sums in the reference recursion order (bit-exact, slower);
-                                  0: packet kernel, same terms, one running sum per band (default) */
+    int exact_mo;              /* Mo gather kernel. 1: sums in the reference recursion order
+                                  (bit-exact, slower); 0 (default): spectrally sharded kernel (band
+                                  groups pinned to XCDs); 2: packet kernel. 0 and 2 evaluate the same
+                                  terms with one running sum per band and agree bit for bit */
     int kernel_timing;         /* 1: time every render kernel with HIP events (mpss_get_render_stats) */
     int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
 } mpss_config;
@@ -140,8 +142,10 @@ typedef struct {
     int64_t n_irradiance, n_camera, n_shade, n_film;     /* launches */
     int64_t samples;      /* camera samples traced (incl. the tile's one-pixel border) */
     int64_t sss_samples;  /* samples that evaluated Mo() */
-    int64_t mo_nodes;     /* octree nodes whose header/Et the shade kernel read (per sample) */
-    int64_t mo_points;    /* leaf points it evaluated */
+    int64_t mo_nodes;     /* octree node visits of the Mo() gather, summed over band groups */
+    int64_t mo_points;    /* leaf point evaluations, summed over band groups */
+    int64_t group_nodes[8], group_points[8];  /* the same per band group (8 groups <= 4 bands) */
+    int32_t group_bands[8][4];                /* band indices of each group (-1: empty slot) */
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal after creation (instrumented passes). */

@@ -75,8 +75,10 @@ private:
     DevBuf<struct RenderLight> d_lights_;
     DevBuf<struct RenderMaterial> d_materials_;
     DevBuf<uint32_t> ws_flags_;
-    DevBuf<float4> ws_pq_;
-    DevBuf<float> ws_ld_, ws_xyz_;
+    DevBuf<int32_t> ws_slot_;
+    DevBuf<int> ws_count_;
+    DevBuf<float4> ws_q_, ws_mo_;
+    DevBuf<float> ws_ld_;
     int64_t ws_n_ = 0;
     // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)
     struct Timed {
@@ -87,7 +89,7 @@ private:
     void time_begin(hipStream_t s, hipEvent_t &a);
     void time_end(hipStream_t s, hipEvent_t a, int kind);
     mpss_render_stats stats_{};
-    DevBuf<unsigned long long> d_counts_;  // [3]: sss samples, nodes, points
+    DevBuf<unsigned long long> d_counts_;  // [2 * kGroups]: nodes, points per band group
     mpss_config cfg_;
     float max_error_, min_dist_;
     std::vector<std::unique_ptr<Material>> materials_;

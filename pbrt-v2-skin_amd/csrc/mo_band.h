@@ -1,0 +1,174 @@
+// mo_band.h -- the spectrally sharded Mo() gather (device), used by the render path and by
+// mpss_mo_batch's default mode.
+//
+// Why: the gather's cost is the Rd(d^2) table lookups. The 30 per-band tables (L floats each,
+// 14 MB for skin) are hit at 30 unrelated offsets per (query, record) and do not fit one XCD's
+// 4 MB L2, so with every wave touching every band the lookups miss to the fabric (measured:
+// 39-61 % L2 hit rate, ~4x the algorithmic bytes through the fabric).
+//
+// Mapping: the 30 bands are dealt into 8 groups of <= 4 (BandGroups) and group g runs only on
+// workgroups with blockIdx % 8 == g, i.e. on one XCD under the round-robin dispatch. Each XCD's
+// L2 then holds only its own <= 4 tables (< 2 MB). One wave64 = 64 queries x one group: lane
+// = query, 4 bands per lane. Node / point headers and the group's 16-byte Et/E slice are
+// wave-uniform scalar loads from a group-major copy of the octree (band_et / band_e, 16 B per
+// record per group, so consecutive pre-order records share lines); only the table lookups
+// are per-lane gathers.
+//
+// Each query walks exactly the node set of SubsurfaceOctreeNode::Mo (diffusionutil.h:175-210)
+// minus subtrees that lie past the end of all of the group's profiles (they add +0 for these
+// bands), in pre-order, with the packet kernel's summation order: results are bit-identical
+// to mo_packet_traverse (one running sum per band, a leaf's points summed first).
+#pragma once
+#include "common.h"
+#include "octree.h"
+
+namespace mpss {
+
+constexpr int kGroups = 8;
+
+// Band -> (group, slot) assignment and per-group pruning scale.
+struct BandGroups {
+    int band[kGroups][4];    // band index, or -1 for an empty slot
+    float rcp_min[kGroups];  // min rcpDsqSpacing over the group's bands
+    int pos[NB];             // band c lives at float pos[c] of a group-major row (4 * g + slot)
+};
+
+// Deal bands to groups: bands sorted by decreasing profile reach (L-1)/rcp, snake order
+// (0..7, 7..0, ...), so every group gets one of the 8 longest-reaching bands (the work a
+// group does is set by its longest-reaching band) and the rest spread evenly.
+inline BandGroups make_band_groups(const float *rcp) {
+    int order[NB];
+    for (int c = 0; c < NB; ++c) order[c] = c;
+    for (int i = 1; i < NB; ++i)  // insertion sort by increasing rcp (= decreasing reach)
+        for (int j = i; j > 0 && rcp[order[j]] < rcp[order[j - 1]]; --j) {
+            const int t = order[j];
+            order[j] = order[j - 1];
+            order[j - 1] = t;
+        }
+    BandGroups g;
+    int fill[kGroups] = {0};
+    for (int i = 0; i < kGroups; ++i) {
+        g.rcp_min[i] = INFINITY;
+        for (int s = 0; s < 4; ++s) g.band[i][s] = -1;
+    }
+    for (int r = 0; r < NB; ++r) {
+        const int round = r / kGroups, k = r % kGroups;
+        const int grp = (round & 1) ? kGroups - 1 - k : k;
+        const int c = order[r];
+        g.band[grp][fill[grp]] = c;
+        g.pos[c] = 4 * grp + fill[grp];
+        ++fill[grp];
+        g.rcp_min[grp] = rcp[c] < g.rcp_min[grp] ? rcp[c] : g.rcp_min[grp];
+    }
+    return g;
+}
+
+struct BandTree {
+    const NodeHdr *__restrict__ nodes;
+    const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
+    const float4 *__restrict__ pt_hdr;   // [n_points] {p, area (sign bit: E black)}
+    const float4 *__restrict__ band_e;   // [kGroups][n_points]
+    const float *__restrict__ table;     // [NB][L]
+    const float *__restrict__ rcp;       // [NB]
+    BandGroups groups;
+    int L, n_nodes, n_points;
+    float max_error, prune_f;
+};
+
+#ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
+template <bool COUNT>
+__device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
+                                                 float acc[4], int &k_nodes, int &k_pts) {
+    float rcp[4];
+    const float *tb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = a.groups.band[grp][j];
+        rcp[j] = c >= 0 ? a.rcp[c] : INFINITY;
+        tb[j] = a.table + (size_t)(c >= 0 ? c : 0) * a.L;
+        acc[j] = 0.f;
+    }
+    const float rcp_min = a.groups.rcp_min[grp];
+    const float4 *__restrict__ et_g = a.band_et + (size_t)grp * a.n_nodes;
+    const float4 *__restrict__ e_g = a.band_e + (size_t)grp * a.n_points;
+    const float lm1 = (float)(a.L - 1);
+    int resume = valid ? 0 : 0x7fffffff;
+    int node = 0;
+    while (node < a.n_nodes) {
+        node = __builtin_amdgcn_readfirstlane(node);
+        const NodeHdr h = a.nodes[node];
+        const int skip = h.skip;
+        bool open = false;
+        if (node >= resume) {
+            if (COUNT) ++k_nodes;
+            const float bx = fmaxf(fmaxf(h.bminx - px, px - h.bmaxx), 0.f);
+            const float by = fmaxf(fmaxf(h.bminy - py, py - h.bmaxy), 0.f);
+            const float bz = fmaxf(fmaxf(h.bminz - pz, pz - h.bmaxz), 0.f);
+            const bool prune = (bx * bx + by * by + bz * bz) * rcp_min >= a.prune_f;
+            if (prune || (h.flags & NODE_BLACK)) {
+                resume = skip;
+            } else {
+                const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
+                const float d2 = dx * dx + dy * dy + dz * dz;
+                const float dw = h.sum_area / d2;
+                const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
+                                    pz >= h.bminz && pz <= h.bmaxz;
+                if (dw < a.max_error && !inside) {
+                    resume = skip;
+                    const float4 et = et_g[node];
+                    const float e[4] = {et.x, et.y, et.z, et.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float f = d2 * rcp[j];
+                        if (f < lm1) {
+                            const uint32_t s = (uint32_t)f;
+                            const float t = f - (float)s;
+                            const float ta = tb[j][s], tbb = tb[j][s + 1];
+                            acc[j] += ((1.f - t) * ta + t * tbb) * e[j];
+                        }
+                    }
+                } else {
+                    open = true;
+                }
+            }
+        }
+        const bool any_open = __builtin_amdgcn_ballot_w64(open) != 0;
+        if (h.leaf_first >= 0) {
+            if (any_open) {
+                float lacc[4] = {0.f, 0.f, 0.f, 0.f};
+                for (int i = 0; i < h.leaf_count; ++i) {
+                    const int kp = h.leaf_first + i;
+                    const float4 ph = a.pt_hdr[kp];
+                    if (__builtin_signbit(ph.w)) continue;  // E is black
+                    if (!open) continue;
+                    if (COUNT) ++k_pts;
+                    const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
+                    const float d2 = ex * ex + ey * ey + ez * ez;
+                    const float4 ev = e_g[kp];
+                    const float e[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float f = d2 * rcp[j];
+                        if (f < lm1) {
+                            const uint32_t s = (uint32_t)f;
+                            const float t = f - (float)s;
+                            const float ta = tb[j][s], tbb = tb[j][s + 1];
+                            lacc[j] += ((1.f - t) * ta + t * tbb) * e[j] * ph.w;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += lacc[j];
+            }
+            if (open) resume = skip;
+            node = skip;
+        } else if (any_open) {
+            node = node + 1;
+        } else {
+            node = skip;
+        }
+    }
+}
+#endif
+
+}  // namespace mpss

@@ -26,6 +26,7 @@
 #include "mo_kernel.h"
 #include "mo_packet.h"
 
+#include <cstring>
 #include <vector>
 
 namespace mpss {
@@ -192,6 +193,99 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Spectrally sharded gather (mo_band.h): block b runs band group b % 8 for queries
+// [256 * (b / 8), +256); query count read on the device (render path: compacted list).
+// ---------------------------------------------------------------------------------------
+struct BandArgs {
+    BandTree t;
+    const float *__restrict__ queries3;  // q * 3 (batch API) or null
+    const float4 *__restrict__ queries4; // {p, *} (render path) or null
+    const int *__restrict__ count;       // device query count (nullable: use nq)
+    int nq;
+    float *__restrict__ out;             // mode 0: out[q * stride + band]
+    float4 *__restrict__ out4;           // mode 1: out4[q * 8 + group]
+    int out_stride;
+    int32_t *__restrict__ counters;      // batch API COUNT: q * 4 (+= per group)
+    unsigned long long *__restrict__ counts;  // render COUNT: [2 * kGroups]
+};
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void mo_band_kernel(BandArgs a) {
+    const int grp = (int)(blockIdx.x & (kGroups - 1));
+    const int base = (int)(blockIdx.x / kGroups) * 256;
+    const int nq = a.count ? *a.count : a.nq;
+    if (base >= nq) return;
+    const int q = base + (int)threadIdx.x;
+    const bool valid = q < nq;
+    float px = 0.f, py = 0.f, pz = 0.f;
+    if (valid) {
+        if (a.queries4) {
+            const float4 v = a.queries4[q];
+            px = v.x;
+            py = v.y;
+            pz = v.z;
+        } else {
+            px = a.queries3[3 * (size_t)q];
+            py = a.queries3[3 * (size_t)q + 1];
+            pz = a.queries3[3 * (size_t)q + 2];
+        }
+    }
+    float acc[4];
+    int kn = 0, kp = 0;
+    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, valid, acc, kn, kp);
+    if (!valid) return;
+    if (a.out4) {
+        a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = a.t.groups.band[grp][j];
+            if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
+        }
+    }
+    if (COUNT) {
+        if (a.counters) {
+            atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
+            atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
+        }
+        if (a.counts) {
+            atomicAdd(&a.counts[2 * grp], (unsigned long long)kn);
+            atomicAdd(&a.counts[2 * grp + 1], (unsigned long long)kp);
+        }
+    }
+}
+
+__global__ void band_permute_kernel(const float *__restrict__ rows, int n, BandGroups g, float4 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n * kGroups) return;
+    const int grp = (int)(i / n), r = (int)(i % n);
+    const float *row = rows + (size_t)r * ROW;
+    float v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[s] = g.band[grp][s] >= 0 ? row[g.band[grp][s]] : 0.f;
+    out[i] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+BandTree band_tree(const DeviceOctree &t, const DeviceProfile &p, float max_error) {
+    BandTree bt;
+    bt.nodes = t.nodes.ptr;
+    bt.band_et = t.band_et.ptr;
+    bt.pt_hdr = t.pt_hdr.ptr;
+    bt.band_e = t.band_e.ptr;
+    bt.table = p.table.ptr;
+    bt.rcp = p.rcp.ptr;
+    bt.groups = p.groups;
+    bt.L = p.L;
+    bt.n_nodes = t.n_nodes;
+    bt.n_points = t.n_points;
+    bt.max_error = max_error;
+    bt.prune_f = (p.rcp_min > 0.f) ? (float)(p.L - 1) * 1.0001f : INFINITY;
+    if (!(p.rcp_min > 0.f))
+        for (int g = 0; g < kGroups; ++g) bt.groups.rcp_min[g] = 0.f;  // rcp <= 0: no pruning
+    return bt;
+}
+
 template <int MAXD>
 void launch_t(const MoArgs &a, bool count, hipStream_t s) {
     const int waves = (a.nq + 1) / 2;
@@ -221,10 +315,47 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
     L = len;
     rcp_min = rcp_[0];
     for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
+    for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
+    groups = make_band_groups(rcp_);
 }
 
-void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
-                      float *out, int out_stride, int32_t *counters, hipStream_t stream, bool exact) {
+void DeviceOctree::ensure_band_layout(const BandGroups &g, hipStream_t stream) {
+    if (band_valid && memcmp(g.band, band_groups.band, sizeof(g.band)) == 0) return;
+    band_et.alloc((size_t)n_nodes * kGroups);
+    band_e.alloc((size_t)(n_points > 0 ? n_points : 1) * kGroups);
+    const int64_t tn = (int64_t)n_nodes * kGroups, tp = (int64_t)n_points * kGroups;
+    if (tn) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, stream,
+                               node_et.ptr, n_nodes, g, band_et.ptr);
+    if (tp) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, stream,
+                               pt_e.ptr, n_points, g, band_e.ptr);
+    MPSS_HIP(hipGetLastError());
+    band_groups = g;
+    band_valid = true;
+}
+
+void launch_mo_band(DeviceOctree &t, const DeviceProfile &p, float max_error, int nq_max, const float4 *queries4,
+                    const int *count_dev, float4 *out4, unsigned long long *counts, hipStream_t stream) {
+    if (nq_max <= 0) return;
+    t.ensure_band_layout(p.groups, stream);
+    BandArgs a{};
+    a.t = band_tree(t, p, max_error);
+    a.queries4 = queries4;
+    a.count = count_dev;
+    a.nq = nq_max;
+    a.out4 = out4;
+    a.counts = counts;
+    const unsigned blocks = (unsigned)((nq_max + 255) / 256) * kGroups;
+    if (counts)
+        hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(256), 0, stream, a);
+    MPSS_HIP(hipGetLastError());
+}
+
+void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_error, int nq, const float *queries,
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream, int mode) {
+    DeviceOctree &t = const_cast<DeviceOctree &>(t_);  // band layout is a cache of the octree
+    const bool exact = mode == 1;
     if (nq <= 0) return;
     if (t.n_nodes <= 0) throw Error(-1, "launch_mo_gather: octree is empty");
     if (p.L < 2) throw Error(-1, "launch_mo_gather: profile table has fewer than 2 entries");
@@ -246,6 +377,24 @@ void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_e
     a.rcp_min = p.rcp_min > 0.f ? p.rcp_min : 0.f;  // rcp_min <= 0 disables pruning
     a.prune_f = (a.rcp_min > 0.f) ? (float)(p.L - 1) * 1.0001f : INFINITY;
     const bool count = counters != nullptr;
+    if (mode == 0) {
+        t.ensure_band_layout(p.groups, stream);
+        if (count) MPSS_HIP(hipMemsetAsync(counters, 0, sizeof(int32_t) * 4 * (size_t)nq, stream));
+        BandArgs b{};
+        b.t = band_tree(t, p, max_error);
+        b.queries3 = queries;
+        b.nq = nq;
+        b.out = out;
+        b.out_stride = out_stride;
+        b.counters = counters;
+        const unsigned blocks = (unsigned)((nq + 255) / 256) * kGroups;
+        if (count)
+            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(256), 0, stream, b);
+        else
+            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(256), 0, stream, b);
+        MPSS_HIP(hipGetLastError());
+        return;
+    }
     if (!exact) {
         const int packets = (nq + 7) / 8, blocks = (packets + 3) / 4;
         if (count)

@@ -147,7 +147,7 @@ int mpss_mo_batch(mpss_ctx *c, uint32_t id, uint32_t q, const float *p_dev, floa
         Context &ctx = *reinterpret_cast<Context *>(c);
         const Material &m = ctx.material(id);
         launch_mo_gather(ctx.octree(), m.dev_profile, ctx.max_error(), (int)q, p_dev, mo_dev, NB, counters_dev,
-                         (hipStream_t)stream, ctx.config().exact_mo != 0);
+                         (hipStream_t)stream, ctx.config().exact_mo);
     });
 }
 

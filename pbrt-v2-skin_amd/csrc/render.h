@@ -6,7 +6,7 @@
 #include "common.h"
 #include "geom.h"
 #include "mo_kernel.h"
-#include "mo_packet.h"
+#include "mo_band.h"
 #include "scene.h"
 
 namespace mpss {
@@ -40,6 +40,7 @@ struct RenderScene {
     const RenderLight *lights;
     const RenderMaterial *materials;
     int nlights, nmaterials, xres, yres;
+    int have_octree;  // Preprocess built an octree: BSSRDF hits evaluate Mo()
     float raster_to_camera[16], camera_to_world[16];
 };
 
@@ -63,18 +64,21 @@ enum : uint32_t {
 
 struct SampleRecs {
     uint32_t *flags;
-    float4 *pq;   // p.xyz, cos(theta_o) at the shading point
-    float *ld;    // [n][ROW] UniformSampleAllLights result
-    float *xyz;   // [n][3]
+    int32_t *slot;   // index into the compacted Mo() query list (REC_SSS samples), else -1
+    float *ld;       // [n][ROW] UniformSampleAllLights result
+    float4 *sss_q;   // [n] compacted Mo() queries: p.xyz, cos(theta_o)
+    int *sss_count;  // device counter of sss_q entries
+    float4 *mo4;     // [n][kGroups] Mo() per band group (mo_band.h layout)
 };
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, int n, uint32_t seed, float *E_out);
+struct BandPos {
+    int pos[NB];  // band c's float offset inside a sample's mo4 row (BandGroups::pos)
+};
+
 __global__ void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
-template <bool COUNT>
-__global__ void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples, int nblocks,
-                             int have_octree, unsigned long long *counts);
-__global__ void film_kernel(TileBatch tb, const uint32_t *flags, const float *xyz, float *out, int out_stride_px,
-                            int xres, int yres);
+// Li assembly (L = Le + SSS + Ld, sample filter, ToXYZ) fused into the box-filtered film.
+__global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, BandPos bp, float *out, int out_stride_px);
 
 }  // namespace mpss

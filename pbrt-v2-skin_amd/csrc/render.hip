@@ -4,10 +4,11 @@
 //                        MultipoleSubsurfaceIntegrator::Li up to UniformSampleAllLights
 //                        (renderers/samplerrenderer.cpp:60-167, cameras/perspective.cpp,
 //                         accelerators/bvh.cpp:388-488, core/integrator.cpp:45-174)
-//   shade_kernel         the Mo() term of Li (multipolesubsurface.cpp:352-374 [file]) via the
-//                        packet gather (mo_packet.h), Li's summation order, the NaN/negative/inf
-//                        sample filter (samplerrenderer.cpp:119-133) and Spectrum::ToXYZ
-//   film_kernel          ImageFilm::AddSample with the 0.5-wide box filter (film/image.cpp:77-137)
+//                        and compacts the samples that need Mo() into a dense query list
+//   (mo_band_kernel)     the Mo() gather, spectrally sharded across XCDs (mo_band.h, mo_kernel.hip)
+//   film_kernel          Li assembly (multipolesubsurface.cpp:253-303: L = Le + SSS + Ld), the
+//                        NaN/negative/inf sample filter (samplerrenderer.cpp:119-133), ToXYZ, and
+//                        ImageFilm::AddSample with the 0.5-wide box filter (film/image.cpp:77-137)
 // Sample values come from counter-based scrambled (0,2)-sequences (pbrt_math.h), identical
 // in the CPU oracle ("replay mode").
 #include "render.h"
@@ -16,7 +17,6 @@
 
 #include "../../data/spectral_bands.h"
 #include "geom.h"
-#include "mo_packet.h"
 
 namespace mpss {
 
@@ -221,8 +221,9 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
 __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
-    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (sid >= tb.nsamples) return;
+    const int64_t sid0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in_range = sid0 < tb.nsamples;
+    const int64_t sid = in_range ? sid0 : tb.nsamples - 1;
     const int s = (int)(sid % tb.spp);
     const int li = (int)(sid / tb.spp);
     const int px = tb.ex0 + li % tb.ew, py = tb.ey0 + li / tb.ew;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
     int lx, hx, ly, hy;
     film_extent(X, sc.xres, lx, hx);
     film_extent(Y, sc.yres, ly, hy);
-    const bool live = lx < tb.x1 && hx >= tb.x0 && ly < tb.y1 && hy >= tb.y0;
+    const bool live = in_range && lx < tb.x1 && hx >= tb.x0 && ly < tb.y1 && hy >= tb.y0;
     uint32_t flags = 0;
     float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
     float ld[NB];
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
             const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
             const V3 wo = -d;
             const RenderMaterial &mat = sc.materials[mesh.material];
-            if (mat.has_bssrdf) {
+            if (mat.has_bssrdf && sc.have_octree) {
                 float ct = absdot(wo, fr.nn);
                 ct = ct < 1.f ? ct : 1.f;
                 flags |= REC_SSS | (mesh.material << REC_MAT_SHIFT);
@@ -339,83 +340,64 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
             }
         }
     }
+    // compact the Mo() queries: one atomic per wave, sample order kept inside the wave
+    const bool sss = (flags & REC_SSS) != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(sss);
+    const int lane = (int)(threadIdx.x & 63);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(rec.sss_count, (int)__builtin_popcountll(m));
+    base = __shfl(base, 0);
+    const int slot = base + (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    if (!in_range) return;
     rec.flags[sid] = flags;
-    rec.pq[sid] = pq;
-    float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)sid * ROW);
+    rec.slot[sid] = sss ? slot : -1;
+    if (sss) rec.sss_q[slot] = pq;
+    if (flags & REC_SURF) {
+        float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)sid * ROW);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int c = 4 * k;
-        row[k] = make_float4(ld[c], ld[c + 1], c + 2 < NB ? ld[c + 2] : 0.f, c + 3 < NB ? ld[c + 3] : 0.f);
+        for (int k = 0; k < 8; ++k) {
+            const int c = 4 * k;
+            row[k] = make_float4(ld[c], ld[c + 1], c + 2 < NB ? ld[c + 2] : 0.f, c + 3 < NB ? ld[c + 3] : 0.f);
+        }
     }
 }
 
-// ------------------------------------------------------------------ Mo term + Li assembly
-template <bool COUNT>
-__global__ __launch_bounds__(256) void shade_kernel(RenderScene sc, PacketTree tree, SampleRecs rec, int64_t nsamples,
-                                                    int nblocks, int have_octree, unsigned long long *counts) {
-    const int lb = xcd_remap((int)blockIdx.x, nblocks);
-    const int lane = threadIdx.x & 63;
-    const int g = lane >> 3, k = lane & 7;
-    const int64_t sid = ((int64_t)lb * 4 + (threadIdx.x >> 6)) * 8 + g;
-    const bool valid = sid < nsamples;
-    uint32_t flags = valid ? rec.flags[sid] : 0u;
-    const float4 pq = valid ? rec.pq[sid] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool sss = (flags & REC_SSS) && have_octree;
-    float mo[4];
-    int kn = 0, kp = 0;
-    mo_packet_traverse<COUNT>(tree, pq.x, pq.y, pq.z, sss, k, mo, kn, kp);
-    if (!valid) return;
-    if (COUNT && k == 0 && sss) {
-        atomicAdd(&counts[0], 1ull);
-        atomicAdd(&counts[1], (unsigned long long)kn);
-        atomicAdd(&counts[2], (unsigned long long)kp);
+// ------------------------------------------------------------------ film
+// Li of one camera sample (MultipoleSubsurfaceIntegrator::Li, multipolesubsurface.cpp:253-303):
+// L = 0 + Le; L += ((INV_PI * Ft) * Mo * Pow(albedo, 1 - mix)).Clamp(0); L += Ld -- then the
+// SamplerRenderer sample filter (NaN / y < -1e-5 / inf -> 0) and Spectrum::ToXYZ, band order.
+__device__ __forceinline__ void sample_xyz(const RenderScene &sc, const SampleRecs &rec, const BandPos &bp,
+                                           int64_t sid, float &X, float &Y, float &Z) {
+    const uint32_t flags = rec.flags[sid];
+    X = Y = Z = 0.f;
+    if (!(flags & (REC_SURF | REC_LE))) return;
+    const float *le = (flags & REC_LE) ? sc.lights[(flags >> REC_LIGHT_SHIFT) & 0xff].Lemit : nullptr;
+    const float *mo = nullptr;
+    const RenderMaterial *mat = nullptr;
+    float kss = 0.f;
+    if (flags & REC_SSS) {
+        const int slot = rec.slot[sid];
+        const float4 q = rec.sss_q[slot];
+        mat = &sc.materials[(flags >> REC_MAT_SHIFT) & 0xff];
+        const float Ft = mat->is_mc ? 1.f : 1.f - rho_lookup(mat->rho, mat->n_rho, q.w);
+        kss = kInvPiF * Ft;
+        mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
     }
-    // L = 0 + Le; L += SSS; L += Ld   (MultipoleSubsurfaceIntegrator::Li, file lines 341-386)
-    float L[4] = {0.f, 0.f, 0.f, 0.f};
-    if (flags & REC_LE) {
-        const RenderLight &Lt = sc.lights[(flags >> REC_LIGHT_SHIFT) & 0xff];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = 4 * k + j;
-            L[j] += c < NB ? Lt.Lemit[c] : 0.f;
-        }
-    }
-    if (sss) {
-        const RenderMaterial &mat = sc.materials[(flags >> REC_MAT_SHIFT) & 0xff];
-        const float Ft = mat.is_mc ? 1.f : 1.f - rho_lookup(mat.rho, mat.n_rho, pq.w);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = 4 * k + j;
-            if (c < NB) {
-                float t = ((kInvPiF * Ft) * mo[j]) * mat.alb_1mmix[c];
-                t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
-                L[j] += t;
-            }
-        }
-    }
-    if (flags & REC_SURF) {
-        const float4 ldv = reinterpret_cast<const float4 *>(rec.ld + (size_t)sid * ROW)[k];
-        L[0] += ldv.x;
-        L[1] += ldv.y;
-        L[2] += ldv.z;
-        L[3] += ldv.w;
-    }
-    // y() and ToXYZ over the 30 bands: reduce the 8 lanes of this sample in band order
-    float X = 0.f, Y = 0.f, Z = 0.f;
+    const float *ld = (flags & REC_SURF) ? rec.ld + (size_t)sid * ROW : nullptr;
     bool nan = false;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float Lj = __shfl(L[j], (lane & ~7) | kk);
-            const int c = 4 * kk + j;
-            if (c < NB) {
-                nan = nan || (Lj != Lj);
-                X += kCieX[c] * Lj;
-                Y += kCieY[c] * Lj;
-                Z += kCieZ[c] * Lj;
-            }
+    for (int c = 0; c < NB; ++c) {
+        float L = 0.f;
+        if (le) L += le[c];
+        if (mo) {
+            float t = (kss * mo[bp.pos[c]]) * mat->alb_1mmix[c];
+            t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
+            L += t;
         }
+        if (ld) L += ld[c];
+        nan = nan || (L != L);
+        X += kCieX[c] * L;
+        Y += kCieY[c] * L;
+        Z += kCieZ[c] * L;
     }
     const float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
     const float y = Y * (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
@@ -423,26 +405,14 @@ __global__ __launch_bounds__(256) void shade_kernel(RenderScene sc, PacketTree t
     Y *= scale;
     Z *= scale;
     if (nan || y < -1e-5f || __builtin_isinf(y)) X = Y = Z = 0.f;  // samplerrenderer.cpp:119-133
-    if (k == 0) {
-        float *o = rec.xyz + (size_t)sid * 3;
-        o[0] = X;
-        o[1] = Y;
-        o[2] = Z;
-    }
 }
 
-template __global__ void shade_kernel<false>(RenderScene, PacketTree, SampleRecs, int64_t, int, int,
-                                             unsigned long long *);
-template __global__ void shade_kernel<true>(RenderScene, PacketTree, SampleRecs, int64_t, int, int,
-                                            unsigned long long *);
-
-// ------------------------------------------------------------------ film
-__global__ __launch_bounds__(256) void film_kernel(TileBatch tb, const uint32_t *__restrict__ flags,
-                                                   const float *__restrict__ xyz, float *__restrict__ out,
-                                                   int out_stride_px, int xres, int yres) {
+__global__ __launch_bounds__(256) void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, BandPos bp,
+                                                   float *__restrict__ out, int out_stride_px) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int tw = tb.x1 - tb.x0, th = tb.y1 - tb.y0;
     if (i >= tw * th) return;
+    const int xres = sc.xres, yres = sc.yres;
     const int px = tb.x0 + i % tw, py = tb.y0 + i / tw;
     float X = 0.f, Y = 0.f, Z = 0.f, W = 0.f;
     // own samples (always inside this pixel's filter support), then the 8 neighbours' samples
@@ -468,11 +438,11 @@ __global__ __launch_bounds__(256) void film_kernel(TileBatch tb, const uint32_t 
                     if (py < lo || py > hi) continue;
                 }
             }
-            const int64_t sid = li * tb.spp + s;
-            const float *x = xyz + (size_t)sid * 3;
-            X += 1.f * x[0];
-            Y += 1.f * x[1];
-            Z += 1.f * x[2];
+            float sx, sy, sz;
+            sample_xyz(sc, rec, bp, li * tb.spp + s, sx, sy, sz);
+            X += 1.f * sx;
+            Y += 1.f * sy;
+            Z += 1.f * sz;
             W += 1.f;
         }
     }
@@ -481,7 +451,6 @@ __global__ __launch_bounds__(256) void film_kernel(TileBatch tb, const uint32_t 
     o[1] = Y;
     o[2] = Z;
     o[3] = W;
-    (void)flags;
 }
 
 }  // namespace mpss

@@ -224,30 +224,29 @@ void Context::preprocess(uint32_t seed) {
     set_irradiance_points(n, p.data(), nr.data(), irradiance_.data(), area.data());
 }
 
-// SamplerRenderer::Render restricted to the pixel rectangle [x0,x1) x [y0,y1)
+// SamplerRenderer::Render restricted to the pixel rectangle [x0,x1) x [y0,y1): per row batch,
+// camera/direct kernel -> sharded Mo() gather over the compacted SSS samples -> film.
 void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, hipStream_t stream) {
     if (scene_dirty_) upload_scene();
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
     if (spp < 1 || x0 < 0 || y0 < 0 || x1 > W || y1 > H || x0 >= x1 || y0 >= y1)
         throw Error(MPSS_ERR_INVALID, "render_tile: bad rectangle or spp");
+    if (!out) throw Error(MPSS_ERR_INVALID, "render_tile: null output");
     const int sss_mat = first_bssrdf_material();
-    PacketTree tree{};
-    int have_tree = 0;
-    if (have_octree_ && sss_mat >= 0) {
-        const Material &m = *materials_[sss_mat];
-        tree = PacketTree{dev_octree_.nodes.ptr, dev_octree_.node_et.ptr, dev_octree_.pt_hdr.ptr,
-                          dev_octree_.pt_e.ptr, m.dev_profile.table.ptr, m.dev_profile.rcp.ptr, m.dev_profile.L,
-                          dev_octree_.n_nodes, max_error_, (float)(m.dev_profile.L - 1) * 1.0001f,
-                          m.dev_profile.rcp_min};
-        have_tree = 1;
-    }
-    const RenderScene sc = render_scene();
+    const bool have_tree = have_octree_ && sss_mat >= 0;
+    Material *m = have_tree ? materials_[sss_mat].get() : nullptr;
+    RenderScene sc = render_scene();
+    sc.have_octree = have_tree ? 1 : 0;
+    BandPos bp{};
+    if (m)
+        for (int c = 0; c < NB; ++c) bp.pos[c] = m->dev_profile.groups.pos[c];
     const int tw = x1 - x0;
     const int ex0 = std::max(x0 - 1, 0);
     const int ew = std::min(x1 + 1, W) - ex0;
     const int64_t max_samples = 1 << 21;
-    int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp) - 2);
+    const int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp) - 2);
+    if (!ws_count_.ptr) ws_count_.alloc(1);
     for (int yb = y0; yb < y1; yb += rows) {
         const int ye = std::min(y1, yb + rows);
         TileBatch tb;
@@ -264,39 +263,42 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
         tb.nsamples = (int64_t)tb.ew * tb.eh * spp;
         if (ws_n_ < tb.nsamples) {
             ws_flags_.alloc(tb.nsamples);
-            ws_pq_.alloc(tb.nsamples);
+            ws_slot_.alloc(tb.nsamples);
             ws_ld_.alloc(tb.nsamples * ROW);
-            ws_xyz_.alloc(tb.nsamples * 3);
+            ws_q_.alloc(tb.nsamples);
+            ws_mo_.alloc(tb.nsamples * kGroups);
             ws_n_ = tb.nsamples;
         }
-        SampleRecs rec{ws_flags_.ptr, ws_pq_.ptr, ws_ld_.ptr, ws_xyz_.ptr};
+        SampleRecs rec{ws_flags_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
+        MPSS_HIP(hipMemsetAsync(ws_count_.ptr, 0, sizeof(int), stream));
         hipEvent_t ev{};
         time_begin(stream, ev);
         hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
                            sc, tb, rec);
         time_end(stream, ev, 1);
-        const int64_t packets = (tb.nsamples + 7) / 8;
-        const int blocks = (int)((packets + 3) / 4);
-        time_begin(stream, ev);
-        if (cfg_.count_traversal) {
-            if (!d_counts_.ptr) {
-                d_counts_.alloc(3);
-                MPSS_HIP(hipMemset(d_counts_.ptr, 0, 3 * sizeof(unsigned long long)));
+        if (m) {
+            if (cfg_.count_traversal && !d_counts_.ptr) {
+                d_counts_.alloc(2 * kGroups);
+                MPSS_HIP(hipMemset(d_counts_.ptr, 0, 2 * kGroups * sizeof(unsigned long long)));
             }
-            hipLaunchKernelGGL(shade_kernel<true>, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples,
-                               blocks, have_tree, d_counts_.ptr);
-        } else {
-            hipLaunchKernelGGL(shade_kernel<false>, dim3(blocks), dim3(256), 0, stream, sc, tree, rec, tb.nsamples,
-                               blocks, have_tree, nullptr);
+            time_begin(stream, ev);
+            launch_mo_band(dev_octree_, m->dev_profile, max_error_, (int)tb.nsamples, ws_q_.ptr, ws_count_.ptr,
+                           ws_mo_.ptr, cfg_.count_traversal ? d_counts_.ptr : nullptr, stream);
+            time_end(stream, ev, 2);
         }
-        time_end(stream, ev, 2);
         const int npx = tw * (ye - yb);
         time_begin(stream, ev);
-        hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, tb, ws_flags_.ptr,
-                           ws_xyz_.ptr, out + (size_t)(yb - y0) * tw * 4, tw, W, H);
+        hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec, bp,
+                           out + (size_t)(yb - y0) * tw * 4, tw);
         time_end(stream, ev, 3);
         MPSS_HIP(hipGetLastError());
         stats_.samples += tb.nsamples;
+        if (cfg_.count_traversal) {  // instrumented pass only: synchronous read of the SSS count
+            int cnt = 0;
+            MPSS_HIP(hipMemcpyAsync(&cnt, ws_count_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+            MPSS_HIP(hipStreamSynchronize(stream));
+            stats_.sss_samples += cnt;
+        }
     }
 }
 
@@ -329,12 +331,19 @@ mpss_render_stats Context::render_stats() {
     }
     timed_.clear();
     mpss_render_stats out = stats_;
+    const int sm = first_bssrdf_material();
+    for (int g = 0; g < kGroups; ++g)
+        for (int s = 0; s < 4; ++s)
+            out.group_bands[g][s] = sm >= 0 ? materials_[sm]->dev_profile.groups.band[g][s] : -1;
     if (d_counts_.ptr) {
-        unsigned long long c[3];
+        unsigned long long c[2 * kGroups];
         MPSS_HIP(hipMemcpy(c, d_counts_.ptr, sizeof(c), hipMemcpyDeviceToHost));
-        out.sss_samples = (int64_t)c[0];
-        out.mo_nodes = (int64_t)c[1];
-        out.mo_points = (int64_t)c[2];
+        for (int g = 0; g < kGroups; ++g) {
+            out.mo_nodes += (int64_t)c[2 * g];
+            out.mo_points += (int64_t)c[2 * g + 1];
+            out.group_nodes[g] = (int64_t)c[2 * g];
+            out.group_points[g] = (int64_t)c[2 * g + 1];
+        }
     }
     return out;
 }
@@ -342,7 +351,7 @@ mpss_render_stats Context::render_stats() {
 void Context::reset_render_stats() {
     (void)render_stats();  // drain pending events
     stats_ = mpss_render_stats{};
-    if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, 3 * sizeof(unsigned long long)));
+    if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, 2 * kGroups * sizeof(unsigned long long)));
 }
 
 int Context::first_bssrdf_material() const { return materials_.empty() ? -1 : 0; }

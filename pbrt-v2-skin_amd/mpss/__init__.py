@@ -48,7 +48,8 @@ class RenderStats(C.Structure):
     _fields_ = [("ms_irradiance", C.c_double), ("ms_camera", C.c_double), ("ms_shade", C.c_double),
                 ("ms_film", C.c_double), ("n_irradiance", C.c_int64), ("n_camera", C.c_int64),
                 ("n_shade", C.c_int64), ("n_film", C.c_int64), ("samples", C.c_int64), ("sss_samples", C.c_int64),
-                ("mo_nodes", C.c_int64), ("mo_points", C.c_int64)]
+                ("mo_nodes", C.c_int64), ("mo_points", C.c_int64), ("group_nodes", C.c_int64 * 8),
+                ("group_points", C.c_int64 * 8), ("group_bands", (C.c_int32 * 4) * 8)]
 
 
 class LayeredSkin(C.Structure):
@@ -308,7 +309,11 @@ class Context:
     def render_stats(self):
         st = RenderStats()
         check(_lib.mpss_get_render_stats(self.h, C.byref(st)))
-        return {k: getattr(st, k) for k, _ in RenderStats._fields_}
+        out = {}
+        for k, _ in RenderStats._fields_:
+            v = getattr(st, k)
+            out[k] = [list(x) for x in v] if k == "group_bands" else (list(v) if k.startswith("group_") else v)
+        return out
 
     def set_instrumentation(self, kernel_timing=False, count_traversal=False):
         check(_lib.mpss_set_instrumentation(self.h, int(kernel_timing), int(count_traversal)))

@@ -4,7 +4,8 @@ The kernel follows the reference recursion's summation order (diffusionutil.h:17
 rounds every product/sum like the scalar code, so equality is exact, not a tolerance.
 Counters (octree nodes entered, leaf points evaluated) must match the oracle's
 instrumented recursion too (they feed the algorithmic-bytes figure).
-The default packet kernel (exact_mo=0) evaluates the same terms with one running sum per
+The default spectrally sharded kernel (exact_mo=0) and the packet kernel (exact_mo=2) must
+agree bit for bit with each other; the packet kernel evaluates the same terms with one running sum per
 band; it is held to 2e-5 relative of the reference order (all terms are >= 0, so the
 reassociation error is bounded by n*eps of the result) and must visit exactly the same
 pruned node/point sets as the exact kernel.
@@ -43,9 +44,9 @@ def wide_profile():
     return tab, rcp
 
 
-def run_gpu(mpss, torch, cloud, table, rcp, q, max_error, exact=True):
+def run_gpu(mpss, torch, cloud, table, rcp, q, max_error, exact=True, mode=None):
     p, n, E, area = cloud
-    ctx = mpss.Context(max_error=max_error, exact_mo=int(exact))
+    ctx = mpss.Context(max_error=max_error, exact_mo=int(exact) if mode is None else mode)
     mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
     ctx.set_irradiance_points(p, n, E, area)
     qd = torch.from_numpy(q).cuda()
@@ -133,13 +134,18 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
     for (table, rcp), npts in ((skin_profile, 200000), (wide_profile, 50000)):
         cloud = synth.ellipsoid_cloud(npts, radii=RADII, seed=23, black_frac=0.05)
         q = synth.surface_queries(6001, radii=RADII, seed=29)
-        fast, cnt_f, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=False)
+        fast, cnt_f, plain_f, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=2)
+        band, cnt_b, plain_b, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=0)
         exact, cnt_e, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=True)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, max_error)
         assert np.array_equal(exact, ref)
         assert _rel_close(fast, ref, 2e-5), np.abs(fast - ref).max()
         assert np.array_equal(cnt_f[:, 2:], cnt_e[:, 2:])  # same pruned traversal per query
         assert np.array_equal(fast == 0, ref == 0)
+        # spectral sharding: same terms, same order per band -> bit-identical to the packet kernel
+        assert np.array_equal(band, fast) and np.array_equal(plain_b, fast) and np.array_equal(plain_f, fast)
+        # per-group pruning never visits more than the all-band traversal, per group
+        assert np.all(cnt_b[:, 2] <= 8 * cnt_f[:, 2]) and np.all(cnt_b[:, 2] > 0)
 
 
 def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
@@ -149,6 +155,8 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
         q = np.ascontiguousarray(np.concatenate([
             synth.surface_queries(61, radii=(0.002, 0.002, 0.002), seed=5, sort=False),
             cloud[0][:1], np.float32([[10.0, 10.0, 10.0]])]))  # 63 queries: ragged last packet
-        fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, exact=False)
+        fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=2)
+        band, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
         assert _rel_close(fast, ref, 2e-5), npts
+        assert np.array_equal(band, fast), npts
