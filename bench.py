@@ -23,9 +23,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-skin_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
-# SURVEY.md §8d algorithmic bytes per octree record read by the Mo() gather: position 12 +
-# area 4 + 4 bytes per band of E/Et. The sharded kernel reads each record once per band group
-# (16 + 4 * bands_in_group bytes), so a step's bytes are summed over groups.
+# SURVEY.md §8d algorithmic bytes of the Mo() gather: per octree record a query needs, position
+# 12 + area 4 + 4 bytes per band of E/Et (136 B for 30 bands). The sharded kernel visits
+# records per band group, so a step's bytes = 4 B x (record, band) evaluations summed over
+# groups + 16 B x the record visits of the busiest group (position/area counted once per
+# query-record, as the reference reads them once). Re-reads the sharding adds are not counted.
 REC_HDR_BYTES = 16
 
 
@@ -127,8 +129,8 @@ def main():
             "film": (st["ms_film"], st["n_film"])}
     dom = max(kern, key=lambda k: kern[k][0])
     nbands = [sum(1 for c in grp if c >= 0) for grp in cnt["group_bands"]]
-    mo_bytes_step = sum((cnt["group_nodes"][g] + cnt["group_points"][g]) * (REC_HDR_BYTES + 4 * nbands[g])
-                        for g in range(8))  # this rank, one step
+    gvis = [cnt["group_nodes"][g] + cnt["group_points"][g] for g in range(8)]
+    mo_bytes_step = sum(gvis[g] * 4 * nbands[g] for g in range(8)) + REC_HDR_BYTES * max(gvis)  # this rank
     shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0

@@ -76,6 +76,38 @@ struct BandTree {
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
+// Rd lookups of one record for the lane's 4 bands: all 8 table loads are issued before any is
+// consumed (out-of-range bands read a clamped, valid entry and are masked), so a record costs
+// one memory round trip instead of four. acc[j] += Rd_j(d2) * e[j] * w exactly as
+// sampleProfile + the Mo() product (multipole.cpp:60-73; diffusionutil.h:185,197).
+template <bool POINT>
+__device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], const float rcp[4], float lm1,
+                                                   uint32_t smax, float d2, const float e[4], float w,
+                                                   float acc[4]) {
+    bool ok[4];
+    uint32_t s[4];
+    float t[4], va[4], vb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float f = d2 * rcp[j];
+        ok[j] = f < lm1;
+        const uint32_t sj = ok[j] ? (uint32_t)f : smax;
+        s[j] = sj;
+        t[j] = f - (float)sj;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        va[j] = tb[j][s[j]];
+        vb[j] = tb[j][s[j] + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float rd = (1.f - t[j]) * va[j] + t[j] * vb[j];
+        const float v = POINT ? rd * e[j] * w : rd * e[j];
+        acc[j] = ok[j] ? acc[j] + v : acc[j];
+    }
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float acc[4], int &k_nodes, int &k_pts) {
@@ -92,6 +124,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     const float4 *__restrict__ et_g = a.band_et + (size_t)grp * a.n_nodes;
     const float4 *__restrict__ e_g = a.band_e + (size_t)grp * a.n_points;
     const float lm1 = (float)(a.L - 1);
+    const uint32_t smax = (uint32_t)(a.L - 2);  // clamped (masked) index for out-of-range bands
     int resume = valid ? 0 : 0x7fffffff;
     int node = 0;
     while (node < a.n_nodes) {
@@ -117,16 +150,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float f = d2 * rcp[j];
-                        if (f < lm1) {
-                            const uint32_t s = (uint32_t)f;
-                            const float t = f - (float)s;
-                            const float ta = tb[j][s], tbb = tb[j][s + 1];
-                            acc[j] += ((1.f - t) * ta + t * tbb) * e[j];
-                        }
-                    }
+                    band_rd_accumulate<false>(tb, rcp, lm1, smax, d2, e, 1.f, acc);
                 } else {
                     open = true;
                 }
@@ -146,16 +170,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float f = d2 * rcp[j];
-                        if (f < lm1) {
-                            const uint32_t s = (uint32_t)f;
-                            const float t = f - (float)s;
-                            const float ta = tb[j][s], tbb = tb[j][s + 1];
-                            lacc[j] += ((1.f - t) * ta + t * tbb) * e[j] * ph.w;
-                        }
-                    }
+                    band_rd_accumulate<true>(tb, rcp, lm1, smax, d2, e, ph.w, lacc);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[j] += lacc[j];
