@@ -62,6 +62,9 @@ typedef struct {
                                   terms with one running sum per band and agree bit for bit */
     int kernel_timing;         /* 1: time every render kernel with HIP events (mpss_get_render_stats) */
     int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
+    int64_t max_batch_samples; /* camera samples per render batch; the workspace is sized for the
+                                  worst case (every sample a hit): ~280 B/sample, 4.7 GB at the
+                                  default 1 << 24 */
 } mpss_config;
 
 void mpss_config_defaults(mpss_config *cfg);
@@ -134,6 +137,12 @@ int mpss_preprocess(mpss_ctx *ctx, uint32_t seed);
  * (y1-y0)*(x1-x0) float4 {sum X, sum Y, sum Z, sum of filter weights} (ImageFilm::Pixel). */
 int mpss_render_tile(mpss_ctx *ctx, int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *xyzw_dev,
                      void *stream);
+/* Render n rectangles (rects[4*i..] = x0, x1, y0, y1) into xyzw_dev[i] in as few kernel batches
+ * as the workspace allows (mpss_config.max_batch_samples): one Mo() gather launch covers the
+ * shading points of every tile in a batch, which is what fills the GPU. Same results as n
+ * mpss_render_tile calls. */
+int mpss_render_tiles(mpss_ctx *ctx, int spp, uint32_t seed, int n, const int32_t *rects, float *const *xyzw_dev,
+                      void *stream);
 
 /* Accumulated per-kernel statistics of mpss_render_tile / mpss_preprocess since the last reset.
  * Kernel times need kernel_timing = 1; traversal counts need count_traversal = 1. Synchronizes. */
@@ -141,7 +150,7 @@ typedef struct {
     double ms_irradiance, ms_camera, ms_shade, ms_film;  /* summed kernel durations */
     int64_t n_irradiance, n_camera, n_shade, n_film;     /* launches */
     int64_t samples;      /* camera samples traced (incl. the tile's one-pixel border) */
-    int64_t sss_samples;  /* samples that evaluated Mo() */
+    int64_t sss_samples;  /* samples with a surface hit (the Mo() query list; count_traversal only) */
     int64_t mo_nodes;     /* octree node visits of the Mo() gather, summed over band groups */
     int64_t mo_points;    /* leaf point evaluations, summed over band groups */
     int64_t group_nodes[8], group_points[8];  /* the same per band group (8 groups <= 4 bands) */

@@ -47,7 +47,7 @@ public:
     void set_camera(const float *r2c, const float *c2w, int xres, int yres);
     void set_surface_points(uint32_t n, const SurfacePoint *pts);
     void preprocess(uint32_t seed);
-    void render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, hipStream_t stream);
+    void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);
     const std::vector<SurfacePoint> &surface_points() const { return points_; }
     const std::vector<float> &irradiance() const { return irradiance_; }
     bool has_octree() const { return have_octree_; }
@@ -74,12 +74,13 @@ private:
     DevBuf<struct RenderMesh> d_meshes_;
     DevBuf<struct RenderLight> d_lights_;
     DevBuf<struct RenderMaterial> d_materials_;
+    // render workspace: per camera sample (flags, slot) and per surface hit (ld, Mo query, Mo)
     DevBuf<uint32_t> ws_flags_;
     DevBuf<int32_t> ws_slot_;
     DevBuf<int> ws_count_;
     DevBuf<float4> ws_q_, ws_mo_;
     DevBuf<float> ws_ld_;
-    int64_t ws_n_ = 0;
+    int64_t ws_n_ = 0, ws_hits_ = 0;
     // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)
     struct Timed {
         hipEvent_t a, b;

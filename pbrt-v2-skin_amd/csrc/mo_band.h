@@ -76,10 +76,19 @@ struct BandTree {
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
-// Rd lookups of one record for the lane's 4 bands: all 8 table loads are issued before any is
-// consumed (out-of-range bands read a clamped, valid entry and are masked), so a record costs
-// one memory round trip instead of four. acc[j] += Rd_j(d2) * e[j] * w exactly as
-// sampleProfile + the Mo() product (multipole.cpp:60-73; diffusionutil.h:185,197).
+// The lerp pair (T[s], T[s+1]) as one 8-byte load at 4-byte alignment (gfx950 global loads
+// take unaligned dword pairs): one vector-memory instruction and one L1 access per touched
+// line instead of two -- the gather is bound by L1 (TCP) accesses, ~15 distinct lines per
+// instruction since a wave's 64 queries index thousands of entries apart.
+struct __attribute__((aligned(4))) RdPair {
+    float a, b;
+};
+
+// Rd lookups of one record for the lane's 4 bands: the table loads are issued before any is
+// consumed (lanes past a band's profile read a clamped, valid entry and are masked; a band
+// no lane needs issues no load at all), so a record costs one memory round trip.
+// acc[j] += Rd_j(d2) * e[j] * w exactly as sampleProfile + the Mo() product
+// (multipole.cpp:60-73; diffusionutil.h:185,197).
 template <bool POINT>
 __device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], const float rcp[4], float lm1,
                                                    uint32_t smax, float d2, const float e[4], float w,
@@ -97,8 +106,12 @@ __device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], con
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        va[j] = tb[j][s[j]];
-        vb[j] = tb[j][s[j] + 1];
+        va[j] = vb[j] = 0.f;
+        if (__builtin_amdgcn_ballot_w64(ok[j]) != 0) {  // wave-uniform skip
+            const RdPair v = *reinterpret_cast<const RdPair *>(tb[j] + s[j]);
+            va[j] = v.a;
+            vb[j] = v.b;
+        }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -219,12 +219,14 @@ __global__ __launch_bounds__(256) void mo_band_kernel(BandArgs a) {
     const int q = base + (int)threadIdx.x;
     const bool valid = q < nq;
     float px = 0.f, py = 0.f, pz = 0.f;
+    bool live = valid;
     if (valid) {
         if (a.queries4) {
             const float4 v = a.queries4[q];
             px = v.x;
             py = v.y;
             pz = v.z;
+            live = v.w >= 0.f;  // render hit list: w < 0 marks hits without a BSSRDF
         } else {
             px = a.queries3[3 * (size_t)q];
             py = a.queries3[3 * (size_t)q + 1];
@@ -233,8 +235,8 @@ __global__ __launch_bounds__(256) void mo_band_kernel(BandArgs a) {
     }
     float acc[4];
     int kn = 0, kp = 0;
-    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, valid, acc, kn, kp);
-    if (!valid) return;
+    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, live, acc, kn, kp);
+    if (!live) return;
     if (a.out4) {
         a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
     } else {

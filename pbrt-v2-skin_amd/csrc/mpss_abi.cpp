@@ -56,6 +56,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->exact_mo = 0;
     c->kernel_timing = 0;
     c->count_traversal = 0;
+    c->max_batch_samples = (int64_t)1 << 24;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -229,7 +230,17 @@ int mpss_preprocess(mpss_ctx *c, uint32_t seed) {
 int mpss_render_tile(mpss_ctx *c, int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, void *stream) {
     return guarded([&] {
         require(c && out, "mpss_render_tile: null argument");
-        reinterpret_cast<Context *>(c)->render_tile(spp, seed, x0, x1, y0, y1, out, (hipStream_t)stream);
+        const int32_t r[4] = {x0, x1, y0, y1};
+        float *o[1] = {out};
+        reinterpret_cast<Context *>(c)->render_tiles(spp, seed, 1, r, o, (hipStream_t)stream);
+    });
+}
+
+int mpss_render_tiles(mpss_ctx *c, int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs,
+                      void *stream) {
+    return guarded([&] {
+        require(c && n >= 0 && (n == 0 || (rects && outs)), "mpss_render_tiles: null argument");
+        reinterpret_cast<Context *>(c)->render_tiles(spp, seed, n, rects, outs, (hipStream_t)stream);
     });
 }
 

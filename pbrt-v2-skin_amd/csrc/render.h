@@ -62,13 +62,15 @@ enum : uint32_t {
     REC_MAT_SHIFT = 16
 };
 
+// Per camera sample: flags and the slot of its surface hit; per surface hit (compacted, one
+// slot per REC_SURF sample of the whole batch): direct light, Mo() query, Mo().
 struct SampleRecs {
     uint32_t *flags;
-    int32_t *slot;   // index into the compacted Mo() query list (REC_SSS samples), else -1
-    float *ld;       // [n][ROW] UniformSampleAllLights result
-    float4 *sss_q;   // [n] compacted Mo() queries: p.xyz, cos(theta_o)
-    int *sss_count;  // device counter of sss_q entries
-    float4 *mo4;     // [n][kGroups] Mo() per band group (mo_band.h layout)
+    int32_t *slot;   // hit slot of a REC_SURF sample, else -1
+    float *ld;       // [hits][ROW] UniformSampleAllLights result
+    float4 *hit_q;   // [hits] Mo() query p.xyz, cos(theta_o); w = -1 when the hit needs no Mo()
+    int *hit_count;  // device counter of hit slots (shared by every tile of a batch)
+    float4 *mo4;     // [hits][kGroups] Mo() per band group (mo_band.h layout)
 };
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,

@@ -340,20 +340,20 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
             }
         }
     }
-    // compact the Mo() queries: one atomic per wave, sample order kept inside the wave
-    const bool sss = (flags & REC_SSS) != 0;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(sss);
+    // compact the surface hits: one atomic per wave, sample order kept inside the wave
+    const bool surf = (flags & REC_SURF) != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(surf);
     const int lane = (int)(threadIdx.x & 63);
     int base = 0;
-    if (lane == 0 && m) base = atomicAdd(rec.sss_count, (int)__builtin_popcountll(m));
+    if (lane == 0 && m) base = atomicAdd(rec.hit_count, (int)__builtin_popcountll(m));
     base = __shfl(base, 0);
     const int slot = base + (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
     if (!in_range) return;
     rec.flags[sid] = flags;
-    rec.slot[sid] = sss ? slot : -1;
-    if (sss) rec.sss_q[slot] = pq;
-    if (flags & REC_SURF) {
-        float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)sid * ROW);
+    rec.slot[sid] = surf ? slot : -1;
+    if (surf) {
+        rec.hit_q[slot] = (flags & REC_SSS) ? pq : make_float4(pq.x, pq.y, pq.z, -1.f);
+        float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int c = 4 * k;
@@ -375,15 +375,15 @@ __device__ __forceinline__ void sample_xyz(const RenderScene &sc, const SampleRe
     const float *mo = nullptr;
     const RenderMaterial *mat = nullptr;
     float kss = 0.f;
+    const int slot = (flags & REC_SURF) ? rec.slot[sid] : -1;
     if (flags & REC_SSS) {
-        const int slot = rec.slot[sid];
-        const float4 q = rec.sss_q[slot];
+        const float4 q = rec.hit_q[slot];
         mat = &sc.materials[(flags >> REC_MAT_SHIFT) & 0xff];
         const float Ft = mat->is_mc ? 1.f : 1.f - rho_lookup(mat->rho, mat->n_rho, q.w);
         kss = kInvPiF * Ft;
         mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
     }
-    const float *ld = (flags & REC_SURF) ? rec.ld + (size_t)sid * ROW : nullptr;
+    const float *ld = (flags & REC_SURF) ? rec.ld + (size_t)slot * ROW : nullptr;
     bool nan = false;
     for (int c = 0; c < NB; ++c) {
         float L = 0.f;

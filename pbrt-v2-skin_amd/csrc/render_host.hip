@@ -224,15 +224,23 @@ void Context::preprocess(uint32_t seed) {
     set_irradiance_points(n, p.data(), nr.data(), irradiance_.data(), area.data());
 }
 
-// SamplerRenderer::Render restricted to the pixel rectangle [x0,x1) x [y0,y1): per row batch,
-// camera/direct kernel -> sharded Mo() gather over the compacted SSS samples -> film.
-void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1, float *out, hipStream_t stream) {
+// SamplerRenderer::Render restricted to pixel rectangles. Each rectangle is cut into row
+// pieces (a piece = the rows plus a one-pixel border of samples that the box filter carries
+// in); pieces are packed into batches of <= max_batch_samples camera samples. Per batch:
+// camera/direct kernel per piece (all pieces append their surface hits to one compacted
+// list) -> ONE sharded Mo() gather over the batch's hits -> film kernel per piece.
+void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs,
+                           hipStream_t stream) {
     if (scene_dirty_) upload_scene();
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
-    if (spp < 1 || x0 < 0 || y0 < 0 || x1 > W || y1 > H || x0 >= x1 || y0 >= y1)
-        throw Error(MPSS_ERR_INVALID, "render_tile: bad rectangle or spp");
-    if (!out) throw Error(MPSS_ERR_INVALID, "render_tile: null output");
+    if (spp < 1) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be >= 1");
+    for (int i = 0; i < n; ++i) {
+        const int32_t *r = rects + 4 * i;
+        if (r[0] < 0 || r[2] < 0 || r[1] > W || r[3] > H || r[0] >= r[1] || r[2] >= r[3])
+            throw Error(MPSS_ERR_INVALID, "render_tile: bad rectangle");
+        if (!outs[i]) throw Error(MPSS_ERR_INVALID, "render_tile: null output");
+    }
     const int sss_mat = first_bssrdf_material();
     const bool have_tree = have_octree_ && sss_mat >= 0;
     Material *m = have_tree ? materials_[sss_mat].get() : nullptr;
@@ -241,40 +249,69 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
     BandPos bp{};
     if (m)
         for (int c = 0; c < NB; ++c) bp.pos[c] = m->dev_profile.groups.pos[c];
-    const int tw = x1 - x0;
-    const int ex0 = std::max(x0 - 1, 0);
-    const int ew = std::min(x1 + 1, W) - ex0;
-    const int64_t max_samples = 1 << 21;
-    const int rows = (int)std::max<int64_t>(1, max_samples / ((int64_t)ew * spp) - 2);
-    if (!ws_count_.ptr) ws_count_.alloc(1);
-    for (int yb = y0; yb < y1; yb += rows) {
-        const int ye = std::min(y1, yb + rows);
+    const int64_t max_batch = std::max<int64_t>(cfg_.max_batch_samples, 1 << 16);
+
+    // cut rectangles into pieces of <= max_batch samples
+    struct Piece {
         TileBatch tb;
-        tb.x0 = x0;
-        tb.x1 = x1;
-        tb.y0 = yb;
-        tb.y1 = ye;
-        tb.ex0 = ex0;
-        tb.ey0 = std::max(yb - 1, 0);
-        tb.ew = ew;
-        tb.eh = std::min(ye + 1, H) - tb.ey0;
-        tb.spp = spp;
-        tb.seed = seed;
-        tb.nsamples = (int64_t)tb.ew * tb.eh * spp;
-        if (ws_n_ < tb.nsamples) {
-            ws_flags_.alloc(tb.nsamples);
-            ws_slot_.alloc(tb.nsamples);
-            ws_ld_.alloc(tb.nsamples * ROW);
-            ws_q_.alloc(tb.nsamples);
-            ws_mo_.alloc(tb.nsamples * kGroups);
-            ws_n_ = tb.nsamples;
+        float *out;
+    };
+    std::vector<Piece> pieces;
+    for (int i = 0; i < n; ++i) {
+        const int x0 = rects[4 * i], x1 = rects[4 * i + 1], y0 = rects[4 * i + 2], y1 = rects[4 * i + 3];
+        const int tw = x1 - x0;
+        const int ex0 = std::max(x0 - 1, 0);
+        const int ew = std::min(x1 + 1, W) - ex0;
+        const int rows = (int)std::max<int64_t>(1, max_batch / ((int64_t)ew * spp) - 2);
+        for (int yb = y0; yb < y1; yb += rows) {
+            const int ye = std::min(y1, yb + rows);
+            Piece p;
+            p.tb.x0 = x0;
+            p.tb.x1 = x1;
+            p.tb.y0 = yb;
+            p.tb.y1 = ye;
+            p.tb.ex0 = ex0;
+            p.tb.ey0 = std::max(yb - 1, 0);
+            p.tb.ew = ew;
+            p.tb.eh = std::min(ye + 1, H) - p.tb.ey0;
+            p.tb.spp = spp;
+            p.tb.seed = seed;
+            p.tb.nsamples = (int64_t)p.tb.ew * p.tb.eh * spp;
+            p.out = outs[i] + (size_t)(yb - y0) * tw * 4;
+            pieces.push_back(p);
         }
-        SampleRecs rec{ws_flags_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
+    }
+    if (!ws_count_.ptr) ws_count_.alloc(1);
+    size_t pi = 0;
+    while (pi < pieces.size()) {
+        // pack pieces into one batch
+        size_t pe = pi;
+        int64_t total = 0;
+        while (pe < pieces.size() && (pe == pi || total + pieces[pe].tb.nsamples <= max_batch))
+            total += pieces[pe++].tb.nsamples;
+        // hits <= samples; the hit arrays grow to the largest batch seen (<= ~290 B per hit)
+        if (ws_n_ < total) {
+            ws_flags_.alloc(total);
+            ws_slot_.alloc(total);
+            ws_n_ = total;
+        }
+        if (ws_hits_ < total) {
+            ws_ld_.alloc(total * ROW);
+            ws_q_.alloc(total);
+            ws_mo_.alloc(total * kGroups);
+            ws_hits_ = total;
+        }
         MPSS_HIP(hipMemsetAsync(ws_count_.ptr, 0, sizeof(int), stream));
+        int64_t off = 0;
         hipEvent_t ev{};
         time_begin(stream, ev);
-        hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
-                           sc, tb, rec);
+        for (size_t k = pi; k < pe; ++k) {
+            const TileBatch &tb = pieces[k].tb;
+            SampleRecs rec{ws_flags_.ptr + off, ws_slot_.ptr + off, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
+            hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0,
+                               stream, sc, tb, rec);
+            off += tb.nsamples;
+        }
         time_end(stream, ev, 1);
         if (m) {
             if (cfg_.count_traversal && !d_counts_.ptr) {
@@ -282,23 +319,30 @@ void Context::render_tile(int spp, uint32_t seed, int x0, int x1, int y0, int y1
                 MPSS_HIP(hipMemset(d_counts_.ptr, 0, 2 * kGroups * sizeof(unsigned long long)));
             }
             time_begin(stream, ev);
-            launch_mo_band(dev_octree_, m->dev_profile, max_error_, (int)tb.nsamples, ws_q_.ptr, ws_count_.ptr,
-                           ws_mo_.ptr, cfg_.count_traversal ? d_counts_.ptr : nullptr, stream);
+            launch_mo_band(dev_octree_, m->dev_profile, max_error_, (int)total, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr,
+                           cfg_.count_traversal ? d_counts_.ptr : nullptr, stream);
             time_end(stream, ev, 2);
         }
-        const int npx = tw * (ye - yb);
+        off = 0;
         time_begin(stream, ev);
-        hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec, bp,
-                           out + (size_t)(yb - y0) * tw * 4, tw);
+        for (size_t k = pi; k < pe; ++k) {
+            const TileBatch &tb = pieces[k].tb;
+            SampleRecs rec{ws_flags_.ptr + off, ws_slot_.ptr + off, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
+            const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
+            hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec, bp,
+                               pieces[k].out, tw);
+            off += tb.nsamples;
+        }
         time_end(stream, ev, 3);
         MPSS_HIP(hipGetLastError());
-        stats_.samples += tb.nsamples;
-        if (cfg_.count_traversal) {  // instrumented pass only: synchronous read of the SSS count
+        stats_.samples += total;
+        if (cfg_.count_traversal) {  // instrumented pass only: synchronous read of the hit count
             int cnt = 0;
             MPSS_HIP(hipMemcpyAsync(&cnt, ws_count_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
             MPSS_HIP(hipStreamSynchronize(stream));
             stats_.sss_samples += cnt;
         }
+        pi = pe;
     }
 }
 

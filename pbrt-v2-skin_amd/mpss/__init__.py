@@ -40,7 +40,7 @@ class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("max_depth", C.c_int), ("max_error", C.c_float),
                 ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
                 ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
-                ("kernel_timing", C.c_int), ("count_traversal", C.c_int)]
+                ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("max_batch_samples", C.c_int64)]
 
 
 class RenderStats(C.Structure):
@@ -92,6 +92,7 @@ _sig("mpss_get_render_stats", C.c_int, [vp, C.POINTER(RenderStats)])
 _sig("mpss_reset_render_stats", C.c_int, [vp])
 _sig("mpss_set_instrumentation", C.c_int, [vp, C.c_int, C.c_int])
 _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
+_sig("mpss_render_tiles", C.c_int, [vp, C.c_int, u32, C.c_int, C.POINTER(C.c_int32), C.POINTER(vp), vp])
 _sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
 _sig("mpss_host_tessellate", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32,
                                        C.c_float, C.c_int, vp, u32p])
@@ -326,3 +327,10 @@ class Context:
 
     def render_tile(self, spp, seed, x0, x1, y0, y1, out_dev, stream=None):
         check(_lib.mpss_render_tile(self.h, spp, seed, x0, x1, y0, y1, out_dev, stream))
+
+    def render_tiles(self, spp, seed, rects, outs_dev, stream=None):
+        """rects: [(x0, x1, y0, y1)], outs_dev: device pointers (one float4 XYZW tile each)."""
+        n = len(rects)
+        r = (C.c_int32 * (4 * n))(*[int(v) for rc in rects for v in rc])
+        o = (vp * n)(*outs_dev)
+        check(_lib.mpss_render_tiles(self.h, spp, seed, n, r, o, stream))

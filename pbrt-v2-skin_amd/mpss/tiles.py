@@ -24,10 +24,14 @@ def slots_per_rank(n_items, world):
 
 
 def render_items(ctx, items, tiles, spp, seeds, out, T, stream=None):
-    """Render work items (frame, tile) into out[i] (a [n, T*T*4] float32 device tensor)."""
+    """Render work items (frame, tile) into out[i] (a [n, T*T*4] float32 device tensor): one
+    mpss_render_tiles call per frame, so the tiles of a frame share Mo() gather launches."""
+    by_frame = {}
     for i, (f, t) in enumerate(items):
-        x0, x1, y0, y1 = tiles[t]
-        ctx.render_tile(spp, seeds[f], x0, x1, y0, y1, out[i].data_ptr(), stream)
+        by_frame.setdefault(f, []).append((i, t))
+    for f, lst in by_frame.items():
+        rects = [tiles[t] for _, t in lst]
+        ctx.render_tiles(spp, seeds[f], rects, [out[i].data_ptr() for i, _ in lst], stream)
 
 
 def assemble(frames_xyzw, gathered, items_by_rank, tiles, T):

@@ -96,3 +96,23 @@ def test_bad_arguments(torch_dev, small_skin, mpss):
         ctx.render_tile(4, 0, 0, sc.xres + 1, 0, 1, out.data_ptr())
     with pytest.raises(mpss.MpssError):
         ctx.render_tile(0, 0, 0, 1, 0, 1, out.data_ptr())
+
+
+@pytest.mark.parametrize("max_batch", [1 << 16, 1 << 24])
+def test_render_tiles_batching_invariance(torch_dev, small_skin, mpss, max_batch):
+    """mpss_render_tiles (several tiles, one Mo() launch per batch; a tiny batch limit forces row
+    pieces and many batches) gives the same bits as per-tile mpss_render_tile calls."""
+    from mpss import pbrtscene
+    sc, ctx = small_skin
+    ref = render(torch_dev, ctx, sc, 0, sc.xres, 0, sc.yres, sc.spp)
+    ctx2 = pbrtscene.build_context(sc, max_batch_samples=max_batch)
+    ctx2.set_surface_points(ctx.surface_points())
+    ctx2.preprocess(seed=1)
+    rects = [(0, 50, 0, 37), (50, 96, 0, 37), (0, 96, 37, 96)]
+    outs = [torch_dev.zeros(((r[1] - r[0]) * (r[3] - r[2]) * 4,), device="cuda") for r in rects]
+    ctx2.render_tiles(sc.spp, 3, rects, [o.data_ptr() for o in outs])
+    torch_dev.cuda.synchronize()
+    got = np.zeros_like(ref)
+    for r, o in zip(rects, outs):
+        got[r[2]:r[3], r[0]:r[1]] = o.cpu().numpy().reshape(r[3] - r[2], r[1] - r[0], 4)
+    assert np.array_equal(got, ref)

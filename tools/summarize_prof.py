@@ -26,7 +26,7 @@ def main(tag):
     for f in sorted(glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv"))):
         agg = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, d in agg.items():
             e = out.setdefault(k, {})
