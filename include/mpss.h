@@ -129,6 +129,12 @@ int mpss_set_camera(mpss_ctx *ctx, const float *raster_to_camera, const float *c
  * the "pointsfile" format; set before mpss_preprocess to skip tessellation. */
 int mpss_set_surface_points(mpss_ctx *ctx, uint32_t n, const void *records);
 int mpss_get_surface_points(mpss_ctx *ctx, void *records, uint32_t *n);
+/* The "pointsfile" on disk: a raw array of the 44-byte records in native byte order, as
+ * TessellateSurfacePointsRenderer writes it (surfacepoints.cpp:335-347) and Preprocess reads it
+ * (multipolesubsurface.cpp:176-181 via ReadBinaryFile, floatfile.h:45-63; a trailing partial
+ * record is ignored). load = set_surface_points from the file; save = the current points. */
+int mpss_load_pointsfile(mpss_ctx *ctx, const char *path);
+int mpss_save_pointsfile(mpss_ctx *ctx, const char *path);
 /* Irradiance E[n][30] of the last Preprocess. */
 int mpss_get_irradiance(mpss_ctx *ctx, float *E, uint32_t *n);
 /* MultipoleSubsurfaceIntegrator::Preprocess: tessellation, irradiance (GPU), octree. */

@@ -77,48 +77,51 @@ struct BandTree {
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
 // The lerp pair (T[s], T[s+1]) as one 8-byte load at 4-byte alignment (gfx950 global loads
-// take unaligned dword pairs): one vector-memory instruction and one L1 access per touched
-// line instead of two -- the gather is bound by L1 (TCP) accesses, ~15 distinct lines per
-// instruction since a wave's 64 queries index thousands of entries apart.
+// take unaligned dword pairs): one vector-memory instruction per band instead of two.
 struct __attribute__((aligned(4))) RdPair {
     float a, b;
 };
 
-// Rd lookups of one record for the lane's 4 bands: the table loads are issued before any is
-// consumed (lanes past a band's profile read a clamped, valid entry and are masked; a band
-// no lane needs issues no load at all), so a record costs one memory round trip.
-// acc[j] += Rd_j(d2) * e[j] * w exactly as sampleProfile + the Mo() product
+// Rd lookups of one record for the lane's 4 bands, straight-line: the 4 pair loads are issued
+// back to back (lanes past a band's profile read a clamped, valid entry and are masked), then
+// consumed -- one memory round trip per record and no divergent branches for the compiler to
+// serialize. t = fract(f) equals f - (float)(uint)f exactly for 0 <= f < 2^24.
+// acc[j] += Rd_j(d2) * e[j] (* w) exactly as sampleProfile + the Mo() product
 // (multipole.cpp:60-73; diffusionutil.h:185,197).
 template <bool POINT>
 __device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], const float rcp[4], float lm1,
                                                    uint32_t smax, float d2, const float e[4], float w,
                                                    float acc[4]) {
+    float f[4];
     bool ok[4];
-    uint32_t s[4];
-    float t[4], va[4], vb[4];
+    RdPair v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float f = d2 * rcp[j];
-        ok[j] = f < lm1;
-        const uint32_t sj = ok[j] ? (uint32_t)f : smax;
-        s[j] = sj;
-        t[j] = f - (float)sj;
+        f[j] = d2 * rcp[j];
+        ok[j] = f[j] < lm1;
+        const uint32_t s = ok[j] ? (uint32_t)f[j] : smax;
+        v[j] = *reinterpret_cast<const RdPair *>(tb[j] + s);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        va[j] = vb[j] = 0.f;
-        if (__builtin_amdgcn_ballot_w64(ok[j]) != 0) {  // wave-uniform skip
-            const RdPair v = *reinterpret_cast<const RdPair *>(tb[j] + s[j]);
-            va[j] = v.a;
-            vb[j] = v.b;
-        }
+        const float t = __builtin_amdgcn_fractf(f[j]);
+        const float rd = (1.f - t) * v[j].a + t * v[j].b;
+        const float val = POINT ? rd * e[j] * w : rd * e[j];
+        acc[j] += ok[j] ? val : 0.f;  // == the masked add: acc starts at +0 and never becomes -0
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float rd = (1.f - t[j]) * va[j] + t[j] * vb[j];
-        const float v = POINT ? rd * e[j] * w : rd * e[j];
-        acc[j] = ok[j] ? acc[j] + v : acc[j];
-    }
+}
+
+// sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d)
+// (v_rcp_f32, <= 1 ulp; product <= ~2.5 ulp) is trusted when it clears max_error by 2^-20
+// relative either way; the rare near-ties (and NaN/inf) take the exact division, so the decision
+// is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
+__device__ __forceinline__ bool dw_below(float a, float d, float m) {
+    const float r = a * __builtin_amdgcn_rcpf(d);
+    const float lo = m * (1.f - 0x1p-20f), hi = m * (1.f + 0x1p-20f);
+    bool below = r < lo;
+    const bool sure = below || r > hi;
+    if (!sure) below = (a / d) < m;
+    return below;
 }
 
 template <bool COUNT>
@@ -156,10 +159,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             } else {
                 const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
                 const float d2 = dx * dx + dy * dy + dz * dz;
-                const float dw = h.sum_area / d2;
                 const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
                                     pz >= h.bminz && pz <= h.bmaxz;
-                if (dw < a.max_error && !inside) {
+                if (dw_below(h.sum_area, d2, a.max_error) && !inside) {
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};

@@ -190,6 +190,34 @@ int mpss_get_surface_points(mpss_ctx *c, void *rec, uint32_t *n) {
     });
 }
 
+int mpss_load_pointsfile(mpss_ctx *c, const char *path) {
+    return guarded([&] {
+        require(c && path, "mpss_load_pointsfile: null argument");
+        FILE *f = fopen(path, "rb");
+        if (!f) throw Error(MPSS_ERR_INVALID, std::string("mpss_load_pointsfile: cannot open ") + path);
+        fseek(f, 0, SEEK_END);
+        const long size = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        std::vector<SurfacePoint> pts((size_t)(size > 0 ? size : 0) / sizeof(SurfacePoint));
+        const size_t got = pts.empty() ? 0 : fread(pts.data(), sizeof(SurfacePoint), pts.size(), f);
+        fclose(f);
+        if (got != pts.size()) throw Error(MPSS_ERR_INVALID, "mpss_load_pointsfile: short read");
+        reinterpret_cast<Context *>(c)->set_surface_points((uint32_t)pts.size(), pts.data());
+    });
+}
+
+int mpss_save_pointsfile(mpss_ctx *c, const char *path) {
+    return guarded([&] {
+        require(c && path, "mpss_save_pointsfile: null argument");
+        const auto &v = reinterpret_cast<Context *>(c)->surface_points();
+        FILE *f = fopen(path, "wb");
+        if (!f) throw Error(MPSS_ERR_INVALID, std::string("mpss_save_pointsfile: cannot open ") + path);
+        const size_t put = v.empty() ? 0 : fwrite(v.data(), sizeof(SurfacePoint), v.size(), f);
+        fclose(f);
+        if (put != v.size()) throw Error(MPSS_ERR_INVALID, "mpss_save_pointsfile: short write");
+    });
+}
+
 int mpss_get_irradiance(mpss_ctx *c, float *E, uint32_t *n) {
     return guarded([&] {
         require(c && n, "mpss_get_irradiance: null argument");

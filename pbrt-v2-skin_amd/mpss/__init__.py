@@ -87,6 +87,8 @@ _sig("mpss_set_camera", C.c_int, [vp, f32p, f32p, C.c_int, C.c_int])
 _sig("mpss_set_surface_points", C.c_int, [vp, u32, vp])
 _sig("mpss_get_surface_points", C.c_int, [vp, vp, u32p])
 _sig("mpss_get_irradiance", C.c_int, [vp, vp, u32p])
+_sig("mpss_load_pointsfile", C.c_int, [vp, C.c_char_p])
+_sig("mpss_save_pointsfile", C.c_int, [vp, C.c_char_p])
 _sig("mpss_preprocess", C.c_int, [vp, u32])
 _sig("mpss_get_render_stats", C.c_int, [vp, C.POINTER(RenderStats)])
 _sig("mpss_reset_render_stats", C.c_int, [vp])
@@ -299,6 +301,12 @@ class Context:
         out = np.zeros(n.value, SURFACE_POINT)
         check(_lib.mpss_get_surface_points(self.h, out.ctypes.data, C.byref(n)))
         return out
+
+    def load_pointsfile(self, path):
+        check(_lib.mpss_load_pointsfile(self.h, os.fsencode(path)))
+
+    def save_pointsfile(self, path):
+        check(_lib.mpss_save_pointsfile(self.h, os.fsencode(path)))
 
     def irradiance(self):
         n = C.c_uint32()

@@ -157,6 +157,7 @@ class Scene:
         self.materials = []  # list of layeredskin param dicts
         self.meshes = []     # dicts: P (world), N, S, uv, indices, o2w, w2o, reverse, material
         self.lights = []     # dicts: center, radius, L (rgb), nsamples
+        self.base_dir = "."
 
     def raster_to_camera(self):
         return camera_matrices(self.world_to_camera, self.fov, self.xres, self.yres, self.screen)
@@ -261,6 +262,7 @@ def load(path, **override):
             else:
                 raise ValueError("unsupported directive %r" % d)
 
+    sc.base_dir = base
     run(open(path).read(), base)
     for k, v in override.items():
         setattr(sc, k, v)
@@ -365,4 +367,7 @@ def build_context(sc, **cfg_kw):
         ctx.add_sphere_light(li["center"], li["radius"], mpss.host_from_rgb(li["L"]), li["nsamples"])
     r2c, c2w = sc.raster_to_camera()
     ctx.set_camera(r2c, c2w, sc.xres, sc.yres)
+    pf = sc.integrator.get("pointsfile")
+    if pf:  # MultipoleSubsurfaceIntegrator reads the points instead of tessellating
+        ctx.load_pointsfile(pf if os.path.isabs(pf) else os.path.join(sc.base_dir, pf))
     return ctx
