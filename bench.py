@@ -125,7 +125,8 @@ def main():
     samples_per_step = frames * sc.xres * sc.yres * sc.spp
     value = samples_per_step * a.steps / dt / 1e6
     # dominant kernel + Mo gather roofline (per-launch averages over the timed region)
-    kern = {"camera_direct": (st["ms_camera"], st["n_camera"]), "mo_band": (st["ms_shade"], st["n_shade"]),
+    kern = {"primary": (st["ms_camera"], st["n_camera"]), "shade_direct": (st["ms_direct"], st["n_direct"]),
+            "mo_band": (st["ms_shade"], st["n_shade"]),
             "film": (st["ms_film"], st["n_film"])}
     dom = max(kern, key=lambda k: kern[k][0])
     nbands = [sum(1 for c in grp if c >= 0) for grp in cnt["group_bands"]]

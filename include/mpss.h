@@ -161,6 +161,8 @@ typedef struct {
     int64_t mo_points;    /* leaf point evaluations, summed over band groups */
     int64_t group_nodes[8], group_points[8];  /* the same per band group (8 groups <= 4 bands) */
     int32_t group_bands[8][4];                /* band indices of each group (-1: empty slot) */
+    double ms_direct;     /* shading + direct lighting kernel (ms_camera: primary rays only) */
+    int64_t n_direct;
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal after creation (instrumented passes). */

@@ -78,7 +78,9 @@ private:
     DevBuf<uint32_t> ws_flags_;
     DevBuf<int32_t> ws_slot_;
     DevBuf<int> ws_count_;
-    DevBuf<float4> ws_q_, ws_mo_;
+    DevBuf<float4> ws_q_, ws_mo_, ws_ha_, ws_hb_, ws_xyz_;
+    DevBuf<uint32_t> ws_hs_, ws_spill_;
+    int64_t ws_px_ = 0;
     DevBuf<float> ws_ld_;
     int64_t ws_n_ = 0, ws_hits_ = 0;
     // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)

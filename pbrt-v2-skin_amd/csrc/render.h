@@ -58,6 +58,9 @@ enum : uint32_t {
     REC_SURF = 2u,  // hit a mesh: Ld valid
     REC_SSS = 4u,   // material has a MultipoleBSSRDF: pq valid
     REC_LE = 8u,    // hit an area light's front face
+    // the sample's float image position rounds onto a pixel edge, so the box filter also
+    // carries it into the neighbour: left (x-1), right (x+1), up (y-1), down (y+1)
+    REC_XLO = 16u, REC_XHI = 32u, REC_YLO = 64u, REC_YHI = 128u,
     REC_LIGHT_SHIFT = 8,
     REC_MAT_SHIFT = 16
 };
@@ -66,11 +69,16 @@ enum : uint32_t {
 // slot per REC_SURF sample of the whole batch): direct light, Mo() query, Mo().
 struct SampleRecs {
     uint32_t *flags;
+    uint32_t *spill;  // per extended-tile pixel: OR of its samples' REC_XLO..REC_YHI bits
     int32_t *slot;   // hit slot of a REC_SURF sample, else -1
     float *ld;       // [hits][ROW] UniformSampleAllLights result
+    float4 *hit_a;   // [hits] t, b1, b2, triangle id (bits)            (primary_kernel)
+    float4 *hit_b;   // [hits] ray direction, pixel index (bits)
+    uint32_t *hit_s; // [hits] sample index (bits 0-15) | material (16-23) | needs Mo() (bit 31)
     float4 *hit_q;   // [hits] Mo() query p.xyz, cos(theta_o); w = -1 when the hit needs no Mo()
     int *hit_count;  // device counter of hit slots (shared by every tile of a batch)
     float4 *mo4;     // [hits][kGroups] Mo() per band group (mo_band.h layout)
+    float4 *xyz;     // [hits] the sample's filtered XYZ (assemble_kernel)
 };
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
@@ -79,8 +87,10 @@ struct BandPos {
     int pos[NB];  // band c's float offset inside a sample's mo4 row (BandGroups::pos)
 };
 
-__global__ void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
-// Li assembly (L = Le + SSS + Ld, sample filter, ToXYZ) fused into the box-filtered film.
-__global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, BandPos bp, float *out, int out_stride_px);
+__global__ void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
+__global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits);
+// Li assembly per slot (L = Le + SSS + Ld, sample filter, ToXYZ), then the box-filtered film.
+__global__ void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits);
+__global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, float *out, int out_stride_px);
 
 }  // namespace mpss

@@ -217,8 +217,11 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
     for (int c = 0; c < NB; ++c) E_out[(size_t)i * NB + c] = E[c];
 }
 
-// ------------------------------------------------------------------ camera + direct lighting
-__global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, TileBatch tb, SampleRecs rec) {
+// ------------------------------------------------------------------ camera rays (primary)
+// SamplerRendererTask::Run's per-sample head: image sample -> PerspectiveCamera::GenerateRay ->
+// Scene::Intersect. Surface hits are compacted (one atomic per wave, sample order kept inside
+// the wave) so the shading kernel runs on full waves; a miss or an area-light hit ends here.
+__global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
     const int64_t sid0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -237,112 +240,34 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
     film_extent(Y, sc.yres, ly, hy);
     const bool live = in_range && lx < tb.x1 && hx >= tb.x0 && ly < tb.y1 && hy >= tb.y0;
     uint32_t flags = 0;
-    float4 pq = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ld[NB];
-    for (int c = 0; c < NB; ++c) ld[c] = 0.f;
+    Hit h;
+    h.tri = INT_MIN;
+    V3 d = V3{0.f, 0.f, 0.f};
     if (live) {
         flags |= REC_LIVE;
+        const uint32_t edge = (lx < px ? REC_XLO : 0u) | (hx > px ? REC_XHI : 0u) | (ly < py ? REC_YLO : 0u) |
+                              (hy > py ? REC_YHI : 0u);
+        if (edge) {
+            flags |= edge;
+            atomicOr(&rec.spill[li], edge);
+        }
         // PerspectiveCamera::GenerateRay (cameras/perspective.cpp)
-        const V3 pras = V3{X, Y, 0.f};
-        const V3 pcam = xform_point(sc.raster_to_camera, pras);
-        const V3 dcam = normalize(pcam);
+        const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
         const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
-        const V3 d = xform_vector(sc.camera_to_world, dcam);
-        const Hit h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 256);
+        d = xform_vector(sc.camera_to_world, normalize(pcam));
+        h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 256);
         if (h.tri != INT_MIN && h.tri < 0) {  // an area light's own surface: Le only
             const int l = -1 - h.tri;
             if (dot(h.lnn, -d) > 0.f) flags |= REC_LE | ((uint32_t)l << REC_LIGHT_SHIFT);
         } else if (h.tri != INT_MIN) {
-            const int mi = sc.tri_mesh[h.tri], lt = sc.tri_local[h.tri];
-            const RenderMesh &mesh = sc.meshes[mi];
-            const V3 p = o + d * h.t;  // Ray::operator()
-            const float reps = 1e-3f * h.t;
-            const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
-            const V3 wo = -d;
-            const RenderMaterial &mat = sc.materials[mesh.material];
-            if (mat.has_bssrdf && sc.have_octree) {
-                float ct = absdot(wo, fr.nn);
-                ct = ct < 1.f ? ct : 1.f;
-                flags |= REC_SSS | (mesh.material << REC_MAT_SHIFT);
-                pq = make_float4(fr.p.x, fr.p.y, fr.p.z, ct);
-            }
-            flags |= REC_SURF;
-            // UniformSampleAllLights (integrator.cpp:45-77) with EstimateDirect (:117-174)
-            const V3 wo_l = to_local(fr, wo);
-            const float ng_wo = dot(wo, fr.ng);
-            for (int l = 0; l < sc.nlights; ++l) {
-                const RenderLight &L = sc.lights[l];
-                const int ns = L.nsamples_round;
-                float Ld[NB];
-                for (int c = 0; c < NB; ++c) Ld[c] = 0.f;
-                const uint32_t xr = (tb.spp & (tb.spp - 1)) == 0 ? (hash3(tb.seed, pix, 16u * l + 9u) & (tb.spp - 1)) : 0u;
-                const uint32_t base = (uint32_t)(s ^ xr) * (uint32_t)ns;
-                const uint32_t sl0 = hash3(tb.seed, pix, 16u * l + DIM_LIGHT_POS),
-                               sl1 = hash3(tb.seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
-                               sb0 = hash3(tb.seed, pix, 16u * l + DIM_BSDF_DIR),
-                               sb1 = hash3(tb.seed, pix, 16u * l + DIM_BSDF_DIR + 8u);
-                for (int j = 0; j < ns; ++j) {
-                    const uint32_t nidx = base + (uint32_t)j;
-                    float ed[NB];
-                    for (int c = 0; c < NB; ++c) ed[c] = 0.f;
-                    // --- light sampling
-                    const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
-                    float lightPdf = ls.pdf;
-                    if (lightPdf > 0.f && ls.nonblack && mat.has_refl) {
-                        const V3 wi_l = to_local(fr, ls.wi);
-                        const bool refl = dot(ls.wi, fr.ng) * ng_wo > 0.f;  // BSDF::f ng test
-                        const MfTerms mt = microfacet_terms(mat.mf, wo_l, wi_l);
-                        bool fblack = true;
-                        float f[NB];
-                        for (int c = 0; c < NB; ++c) {
-                            f[c] = (refl && !mt.zero) ? mat.R[c] * mt.D * mt.G * mt.F / mt.den : 0.f;
-                            fblack = fblack && f[c] == 0.f;
-                        }
-                        if (!fblack && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
-                            const float bsdfPdf = microfacet_pdf(mat.mf, wo_l, wi_l);
-                            const float w = power_heuristic(lightPdf, bsdfPdf);
-                            const float sc1 = absdot(ls.wi, fr.nn) * w / lightPdf;
-                            for (int c = 0; c < NB; ++c) ed[c] += f[c] * L.Lemit[c] * sc1;
-                        }
-                    }
-                    // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733)
-                    if (mat.has_refl) {
-                        V3 wi_l;
-                        float bsdfPdf;
-                        beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
-                        if (bsdfPdf != 0.f) {
-                            const V3 wi = to_world(fr, wi_l);
-                            const bool refl = dot(wi, fr.ng) * ng_wo > 0.f;
-                            const MfTerms mt = microfacet_terms(mat.mf, wo_l, wi_l);
-                            bool fblack = true;
-                            float f[NB];
-                            for (int c = 0; c < NB; ++c) {
-                                f[c] = (refl && !mt.zero) ? mat.R[c] * mt.D * mt.G * mt.F / mt.den : 0.f;
-                                fblack = fblack && f[c] == 0.f;
-                            }
-                            if (!fblack && bsdfPdf > 0.f) {
-                                lightPdf = sphere_pdf(L.s, fr.p, wi);
-                                if (lightPdf != 0.f) {
-                                    const float w = power_heuristic(bsdfPdf, lightPdf);
-                                    const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
-                                    // Li = lightIsect.Le(-wi) when the hit primitive is this light
-                                    if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
-                                        const float adn = absdot(wi, fr.nn);
-                                        for (int c = 0; c < NB; ++c) ed[c] += f[c] * L.Lemit[c] * adn * w / bsdfPdf;
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    for (int c = 0; c < NB; ++c) Ld[c] += ed[c];
-                }
-                for (int c = 0; c < NB; ++c) ld[c] += Ld[c] / (float)ns;
-            }
+            const uint32_t mid = sc.meshes[sc.tri_mesh[h.tri]].material;
+            flags |= REC_SURF | (mid << REC_MAT_SHIFT);
+            if (sc.materials[mid].has_bssrdf && sc.have_octree) flags |= REC_SSS;
         }
     }
-    // compact the surface hits: one atomic per wave, sample order kept inside the wave
-    const bool surf = (flags & REC_SURF) != 0;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(surf);
+    // every sample with radiance (a surface hit, or an area light seen directly) gets a slot
+    const bool surf = (flags & REC_SURF) != 0, has_l = surf || (flags & REC_LE);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(has_l);
     const int lane = (int)(threadIdx.x & 63);
     int base = 0;
     if (lane == 0 && m) base = atomicAdd(rec.hit_count, (int)__builtin_popcountll(m));
@@ -350,40 +275,173 @@ __global__ __launch_bounds__(256) void camera_direct_kernel(RenderScene sc, Tile
     const int slot = base + (int)__builtin_popcountll(m & ((1ull << lane) - 1ull));
     if (!in_range) return;
     rec.flags[sid] = flags;
-    rec.slot[sid] = surf ? slot : -1;
+    rec.slot[sid] = has_l ? slot : -1;
     if (surf) {
-        rec.hit_q[slot] = (flags & REC_SSS) ? pq : make_float4(pq.x, pq.y, pq.z, -1.f);
-        float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int c = 4 * k;
-            row[k] = make_float4(ld[c], ld[c + 1], c + 2 < NB ? ld[c + 2] : 0.f, c + 3 < NB ? ld[c + 3] : 0.f);
+        rec.hit_a[slot] = make_float4(h.t, h.b1, h.b2, __int_as_float(h.tri));
+        rec.hit_b[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(pix));
+        // sample index (16 bits) | material (8 bits) | SSS bit 31
+        rec.hit_s[slot] = (uint32_t)s | (flags & (0xffu << REC_MAT_SHIFT)) | ((flags & REC_SSS) ? 0x80000000u : 0u);
+    } else if (has_l) {
+        // light seen directly: light index (8 bits) | bit 30
+        rec.hit_s[slot] = (((flags >> REC_LIGHT_SHIFT) & 0xffu) << REC_MAT_SHIFT) | 0x40000000u;
+    }
+}
+
+// ------------------------------------------------------------------ shading + direct light
+// The rest of MultipoleSubsurfaceIntegrator::Li for one compacted surface hit (full waves):
+// shading geometry, the Mo() query of a BSSRDF hit, and UniformSampleAllLights (integrator.cpp:
+// 47-77) with EstimateDirect (:117-174). Spectra are not held per light sample: a BSDF value is
+// R[c] * D * G * F / den (Microfacet::f) with scalar D, G, F, den, so each sample keeps only its
+// scalars and the per-band sums are formed in the reference's operation order in one pass.
+__global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
+                                                           int max_hits) {
+    __shared__ int stk_all[kStack * 256];
+    int *stk = stk_all + threadIdx.x;
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if ((int)(blockIdx.x * blockDim.x) >= nhits) return;
+    if (slot >= nhits || slot >= max_hits) return;
+    const uint32_t hs = rec.hit_s[slot];
+    if (hs & 0x40000000u) {  // an area light seen directly: no shading point, no Mo()
+        rec.hit_q[slot] = make_float4(0.f, 0.f, 0.f, -1.f);
+        return;
+    }
+    const float4 ha = rec.hit_a[slot], hb = rec.hit_b[slot];
+    const int s = (int)(hs & 0xffffu);
+    const uint32_t mid = (hs >> REC_MAT_SHIFT) & 0xffu;
+    const bool sss = (hs >> 31) != 0;
+    const int tri = __float_as_int(ha.w);
+    const uint32_t pix = __float_as_uint(hb.w);
+    const V3 d = V3{hb.x, hb.y, hb.z};
+    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
+    const int mi = sc.tri_mesh[tri], lt = sc.tri_local[tri];
+    const RenderMesh &mesh = sc.meshes[mi];
+    const V3 p = o + d * ha.x;  // Ray::operator()
+    const float reps = 1e-3f * ha.x;
+    const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - ha.y - ha.z, ha.y, ha.z);
+    const V3 wo = -d;
+    const RenderMaterial &mat = sc.materials[mid];
+    float ct = absdot(wo, fr.nn);
+    ct = ct < 1.f ? ct : 1.f;
+    rec.hit_q[slot] = make_float4(fr.p.x, fr.p.y, fr.p.z, sss ? ct : -1.f);
+    float ld[NB];
+    for (int c = 0; c < NB; ++c) ld[c] = 0.f;
+    const V3 wo_l = to_local(fr, wo);
+    const float ng_wo = dot(wo, fr.ng);
+    for (int l = 0; l < sc.nlights; ++l) {
+        const RenderLight &L = sc.lights[l];
+        const int ns = L.nsamples_round;
+        float Ld[NB];
+        for (int c = 0; c < NB; ++c) Ld[c] = 0.f;
+        const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
+        const uint32_t base = (uint32_t)(s ^ (int)xr) * (uint32_t)ns;
+        const uint32_t sl0 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS),
+                       sl1 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
+                       sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR),
+                       sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u);
+        for (int j = 0; j < ns; ++j) {
+            const uint32_t nidx = base + (uint32_t)j;
+            // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
+            MfTerms t1{0.f, 0.f, 0.f, 1.f, true};
+            float k1 = 0.f;
+            bool use1 = false;
+            const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
+            float lightPdf = ls.pdf;
+            if (lightPdf > 0.f && ls.nonblack && mat.has_refl) {
+                const V3 wi_l = to_local(fr, ls.wi);
+                const bool refl = dot(ls.wi, fr.ng) * ng_wo > 0.f;  // BSDF::f ng test
+                t1 = microfacet_terms(mat.mf, wo_l, wi_l);
+                bool fblack = !refl || t1.zero;
+                if (!fblack) {
+                    fblack = true;
+                    for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t1.D * t1.G * t1.F / t1.den) == 0.f;
+                }
+                if (!fblack && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
+                    const float bsdfPdf = microfacet_pdf(mat.mf, wo_l, wi_l);
+                    const float w = power_heuristic(lightPdf, bsdfPdf);
+                    k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
+                    use1 = true;
+                }
+            }
+            // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
+            MfTerms t2{0.f, 0.f, 0.f, 1.f, true};
+            float adn = 0.f, w2 = 0.f, pdf2 = 1.f;
+            bool use2 = false;
+            if (mat.has_refl) {
+                V3 wi_l;
+                float bsdfPdf;
+                beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+                if (bsdfPdf != 0.f) {
+                    const V3 wi = to_world(fr, wi_l);
+                    const bool refl = dot(wi, fr.ng) * ng_wo > 0.f;
+                    t2 = microfacet_terms(mat.mf, wo_l, wi_l);
+                    bool fblack = !refl || t2.zero;
+                    if (!fblack) {
+                        fblack = true;
+                        for (int c = 0; c < NB; ++c)
+                            fblack = fblack && (mat.R[c] * t2.D * t2.G * t2.F / t2.den) == 0.f;
+                    }
+                    if (!fblack && bsdfPdf > 0.f) {
+                        lightPdf = sphere_pdf(L.s, fr.p, wi);
+                        if (lightPdf != 0.f) {
+                            const float w = power_heuristic(bsdfPdf, lightPdf);
+                            const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
+                            // Li = lightIsect.Le(-wi) when the hit primitive is this light
+                            if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
+                                adn = absdot(wi, fr.nn);
+                                w2 = w;
+                                pdf2 = bsdfPdf;
+                                use2 = true;
+                            }
+                        }
+                    }
+                }
+            }
+            if (use1 || use2) {  // else ed = 0 and Ld += 0 changes nothing (Ld is never -0)
+                for (int c = 0; c < NB; ++c) {
+                    float ed = 0.f;
+                    if (use1) ed += (mat.R[c] * t1.D * t1.G * t1.F / t1.den) * L.Lemit[c] * k1;
+                    if (use2) ed += (mat.R[c] * t2.D * t2.G * t2.F / t2.den) * L.Lemit[c] * adn * w2 / pdf2;
+                    Ld[c] += ed;
+                }
+            }
         }
+        for (int c = 0; c < NB; ++c) ld[c] += Ld[c] / (float)ns;
+    }
+    float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int c = 4 * k;
+        row[k] = make_float4(ld[c], ld[c + 1], c + 2 < NB ? ld[c + 2] : 0.f, c + 3 < NB ? ld[c + 3] : 0.f);
     }
 }
 
 // ------------------------------------------------------------------ film
-// Li of one camera sample (MultipoleSubsurfaceIntegrator::Li, multipolesubsurface.cpp:253-303):
-// L = 0 + Le; L += ((INV_PI * Ft) * Mo * Pow(albedo, 1 - mix)).Clamp(0); L += Ld -- then the
-// SamplerRenderer sample filter (NaN / y < -1e-5 / inf -> 0) and Spectrum::ToXYZ, band order.
-__device__ __forceinline__ void sample_xyz(const RenderScene &sc, const SampleRecs &rec, const BandPos &bp,
-                                           int64_t sid, float &X, float &Y, float &Z) {
-    const uint32_t flags = rec.flags[sid];
-    X = Y = Z = 0.f;
-    if (!(flags & (REC_SURF | REC_LE))) return;
-    const float *le = (flags & REC_LE) ? sc.lights[(flags >> REC_LIGHT_SHIFT) & 0xff].Lemit : nullptr;
-    const float *mo = nullptr;
+// Li of one camera sample with radiance (MultipoleSubsurfaceIntegrator::Li,
+// multipolesubsurface.cpp:253-303): L = 0 + Le; L += ((INV_PI * Ft) * Mo * Pow(albedo, 1 - mix))
+// .Clamp(0); L += Ld -- then the SamplerRenderer sample filter (NaN / y < -1e-5 / inf -> 0,
+// samplerrenderer.cpp:119-133) and Spectrum::ToXYZ in band order. One lane per slot.
+__global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits) {
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if (slot >= nhits || slot >= max_hits) return;
+    const uint32_t hs = rec.hit_s[slot];
+    const float *le = nullptr, *mo = nullptr, *ld = nullptr;
     const RenderMaterial *mat = nullptr;
     float kss = 0.f;
-    const int slot = (flags & REC_SURF) ? rec.slot[sid] : -1;
-    if (flags & REC_SSS) {
-        const float4 q = rec.hit_q[slot];
-        mat = &sc.materials[(flags >> REC_MAT_SHIFT) & 0xff];
-        const float Ft = mat->is_mc ? 1.f : 1.f - rho_lookup(mat->rho, mat->n_rho, q.w);
-        kss = kInvPiF * Ft;
-        mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
+    if (hs & 0x40000000u) {
+        le = sc.lights[(hs >> REC_MAT_SHIFT) & 0xffu].Lemit;
+    } else {
+        ld = rec.ld + (size_t)slot * ROW;
+        if (hs >> 31) {
+            const float4 q = rec.hit_q[slot];
+            mat = &sc.materials[(hs >> REC_MAT_SHIFT) & 0xffu];
+            const float Ft = mat->is_mc ? 1.f : 1.f - rho_lookup(mat->rho, mat->n_rho, q.w);
+            kss = kInvPiF * Ft;
+            mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
+        }
     }
-    const float *ld = (flags & REC_SURF) ? rec.ld + (size_t)slot * ROW : nullptr;
+    float X = 0.f, Y = 0.f, Z = 0.f;
     bool nan = false;
     for (int c = 0; c < NB; ++c) {
         float L = 0.f;
@@ -404,45 +462,60 @@ __device__ __forceinline__ void sample_xyz(const RenderScene &sc, const SampleRe
     X *= scale;
     Y *= scale;
     Z *= scale;
-    if (nan || y < -1e-5f || __builtin_isinf(y)) X = Y = Z = 0.f;  // samplerrenderer.cpp:119-133
+    if (nan || y < -1e-5f || __builtin_isinf(y)) X = Y = Z = 0.f;
+    rec.xyz[slot] = make_float4(X, Y, Z, 0.f);
 }
 
-__global__ __launch_bounds__(256) void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, BandPos bp,
+__global__ __launch_bounds__(256) void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec,
                                                    float *__restrict__ out, int out_stride_px) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int tw = tb.x1 - tb.x0, th = tb.y1 - tb.y0;
     if (i >= tw * th) return;
-    const int xres = sc.xres, yres = sc.yres;
     const int px = tb.x0 + i % tw, py = tb.y0 + i / tw;
     float X = 0.f, Y = 0.f, Z = 0.f, W = 0.f;
     // own samples (always inside this pixel's filter support), then the 8 neighbours' samples
     // in row-major order whose float image position rounds onto the shared edge
-    // (ImageFilm::AddSample with the 0.5-wide box filter, image.cpp:77-137)
+    // (ImageFilm::AddSample with the 0.5-wide box filter, image.cpp:77-137). Samples that hit
+    // nothing add exactly 0 to X, Y, Z (never -0), so only their weight is accumulated.
     for (int q = 0; q < 9; ++q) {
         const int dx = q == 0 ? 0 : ((q - 1 + (q > 4)) % 3) - 1;
         const int dy = q == 0 ? 0 : ((q - 1 + (q > 4)) / 3) - 1;
         const int qx = px + dx, qy = py + dy;
         if (qx < tb.ex0 || qy < tb.ey0 || qx >= tb.ex0 + tb.ew || qy >= tb.ey0 + tb.eh) continue;
         const int64_t li = (int64_t)(qy - tb.ey0) * tb.ew + (qx - tb.ex0);
-        const uint32_t pix = (uint32_t)qy * (uint32_t)xres + (uint32_t)qx;
-        const uint32_t su = hash3(tb.seed, pix, DIM_IMAGE), sv = hash3(tb.seed, pix, DIM_IMAGE + 1);
-        for (int s = 0; s < tb.spp; ++s) {
-            if (q > 0) {
-                int lo, hi;
-                if (dx != 0) {
-                    film_extent((float)qx + van_der_corput((uint32_t)s, su), xres, lo, hi);
-                    if (px < lo || px > hi) continue;
-                }
-                if (dy != 0) {
-                    film_extent((float)qy + sobol2((uint32_t)s, sv), yres, lo, hi);
-                    if (py < lo || py > hi) continue;
+        // bits the neighbour's samples need to reach this pixel
+        const uint32_t need = (dx < 0 ? REC_XHI : dx > 0 ? REC_XLO : 0u) | (dy < 0 ? REC_YHI : dy > 0 ? REC_YLO : 0u);
+        if (q == 0) {
+            const int32_t *sl = rec.slot + li * tb.spp;
+            for (int s0 = 0; s0 < tb.spp; s0 += 8) {
+                int32_t v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = s0 + k < tb.spp ? sl[s0 + k] : -2;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (v[k] == -2) break;
+                    if (v[k] >= 0) {
+                        const float4 x = rec.xyz[v[k]];
+                        X += 1.f * x.x;
+                        Y += 1.f * x.y;
+                        Z += 1.f * x.z;
+                    }
+                    W += 1.f;
                 }
             }
-            float sx, sy, sz;
-            sample_xyz(sc, rec, bp, li * tb.spp + s, sx, sy, sz);
-            X += 1.f * sx;
-            Y += 1.f * sy;
-            Z += 1.f * sz;
+            continue;
+        }
+        if ((rec.spill[li] & need) != need) continue;
+        for (int s = 0; s < tb.spp; ++s) {
+            const int64_t sid = li * tb.spp + s;
+            if ((rec.flags[sid] & need) != need) continue;
+            const int32_t v = rec.slot[sid];
+            if (v >= 0) {
+                const float4 x = rec.xyz[v];
+                X += 1.f * x.x;
+                Y += 1.f * x.y;
+                Z += 1.f * x.z;
+            }
             W += 1.f;
         }
     }

@@ -234,7 +234,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     if (scene_dirty_) upload_scene();
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
-    if (spp < 1) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be >= 1");
+    if (spp < 1 || spp > 65535) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be in [1, 65535]");
     for (int i = 0; i < n; ++i) {
         const int32_t *r = rects + 4 * i;
         if (r[0] < 0 || r[2] < 0 || r[1] > W || r[3] > H || r[0] >= r[1] || r[2] >= r[3])
@@ -299,20 +299,38 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             ws_ld_.alloc(total * ROW);
             ws_q_.alloc(total);
             ws_mo_.alloc(total * kGroups);
+            ws_ha_.alloc(total);
+            ws_hb_.alloc(total);
+            ws_hs_.alloc(total);
+            ws_xyz_.alloc(total);
             ws_hits_ = total;
         }
+        if (ws_px_ < total / spp) {
+            ws_spill_.alloc(total / spp);
+            ws_px_ = total / spp;
+        }
         MPSS_HIP(hipMemsetAsync(ws_count_.ptr, 0, sizeof(int), stream));
+        MPSS_HIP(hipMemsetAsync(ws_spill_.ptr, 0, sizeof(uint32_t) * (size_t)(total / spp), stream));
         int64_t off = 0;
         hipEvent_t ev{};
         time_begin(stream, ev);
         for (size_t k = pi; k < pe; ++k) {
             const TileBatch &tb = pieces[k].tb;
-            SampleRecs rec{ws_flags_.ptr + off, ws_slot_.ptr + off, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
-            hipLaunchKernelGGL(camera_direct_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0,
+            SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
+                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+            hipLaunchKernelGGL(primary_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0,
                                stream, sc, tb, rec);
             off += tb.nsamples;
         }
         time_end(stream, ev, 1);
+        {
+            SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
+                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+            time_begin(stream, ev);
+            hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
+                               rec, spp, seed, (int)total);
+            time_end(stream, ev, 4);
+        }
         if (m) {
             if (cfg_.count_traversal && !d_counts_.ptr) {
                 d_counts_.alloc(2 * kGroups);
@@ -325,11 +343,18 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         }
         off = 0;
         time_begin(stream, ev);
+        {
+            SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
+                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+            hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
+                               bp, (int)total);
+        }
         for (size_t k = pi; k < pe; ++k) {
             const TileBatch &tb = pieces[k].tb;
-            SampleRecs rec{ws_flags_.ptr + off, ws_slot_.ptr + off, ws_ld_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr};
+            SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
+                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
             const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
-            hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec, bp,
+            hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec,
                                pieces[k].out, tw);
             off += tb.nsamples;
         }
@@ -368,8 +393,9 @@ mpss_render_stats Context::render_stats() {
         MPSS_HIP(hipEventElapsedTime(&ms, t.a, t.b));
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
-        double *dst[4] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film};
-        int64_t *cnt[4] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film};
+        double *dst[5] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film,
+                          &stats_.ms_direct};
+        int64_t *cnt[5] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film, &stats_.n_direct};
         *dst[t.kind] += ms;
         *cnt[t.kind] += 1;
     }

@@ -49,7 +49,8 @@ class RenderStats(C.Structure):
                 ("ms_film", C.c_double), ("n_irradiance", C.c_int64), ("n_camera", C.c_int64),
                 ("n_shade", C.c_int64), ("n_film", C.c_int64), ("samples", C.c_int64), ("sss_samples", C.c_int64),
                 ("mo_nodes", C.c_int64), ("mo_points", C.c_int64), ("group_nodes", C.c_int64 * 8),
-                ("group_points", C.c_int64 * 8), ("group_bands", (C.c_int32 * 4) * 8)]
+                ("group_points", C.c_int64 * 8), ("group_bands", (C.c_int32 * 4) * 8), ("ms_direct", C.c_double),
+                ("n_direct", C.c_int64)]
 
 
 class LayeredSkin(C.Structure):
