@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default=None, help="write rank 0's first frame as .pfm/.exr")
+    ap.add_argument("--pmc-json", default=None,
+                    help="rocprofv3 PMC summary (tools/summarize_prof.py) of this bench command; default: the "
+                         "newest profiles/*_pmc.json with a FETCH_SIZE entry for mo_band_kernel")
     return ap.parse_args()
 
 
@@ -140,6 +143,12 @@ def main():
                 "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
                 "dominant_kernel": dom,
                 "kernel_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in kern.items()}}
+    pt = pmc_traffic(a.pmc_json, shade_launch_ms)
+    if pt:
+        roofline["traffic"] = pt["traffic"]
+        roofline["traffic_source"] = pt["source"] + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"
+        if "l2" in pt:
+            roofline["l2_request_roofline"] = pt["l2"]
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -170,6 +179,34 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+L2_PEAK_REQ_PER_S = 34.5e12 / 128  # MI355X L2 ~34.5 TB/s aggregate (MI355X_MICROARCH.md), 128-B lines
+
+
+def pmc_traffic(path, launch_ms):
+    """HBM-side traffic of one mo_band_kernel launch from a committed rocprofv3 PMC summary of
+    the same bench command: FETCH_SIZE x 2 (the gfx950 correction, MI355X_MICROARCH.md), and
+    the L2 request rate (TCC_HIT + TCC_MISS per launch / launch time)."""
+    import glob
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
+                                       key=os.path.getmtime, reverse=True)
+    for f in cands:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        e = d.get("void mpss::mo_band_kernel<false>")
+        if not e or "fetch_bytes_corrected_mean" not in e:
+            continue
+        out = {"traffic": e["fetch_bytes_corrected_mean"], "source": os.path.relpath(f, ROOT)}
+        if "TCC_HIT_sum" in e and launch_ms > 0:
+            req = e["TCC_HIT_sum"]["mean"] + e["TCC_MISS_sum"]["mean"]
+            out["l2"] = {"requests_per_launch": req, "achieved_req_per_s": req / (launch_ms * 1e-3),
+                         "peak_req_per_s": L2_PEAK_REQ_PER_S,
+                         "frac": req / (launch_ms * 1e-3) / L2_PEAK_REQ_PER_S, "hit_rate": e.get("l2_hit_rate")}
+        return out
+    return None
 
 
 def cpu_baseline(sc, ctx, a):

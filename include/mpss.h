@@ -169,6 +169,16 @@ int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 int mpss_set_instrumentation(mpss_ctx *ctx, int kernel_timing, int count_traversal);
 int mpss_reset_render_stats(mpss_ctx *ctx);
 
+/* ---- Monte-Carlo layered profile (renderer "mcprofile", src/renderers/mcprofile.cpp) ---- */
+typedef struct { float mua, musp, ior, thickness; } mpss_layer; /* core/layer.h:35-46, "layer layers" order */
+/* MonteCarloProfileRenderer::Render (mcprofile.cpp:443-533) on the ctx's GPU: nphotons random walks
+ * (FP64), rings of width extent/nsegments with extent = mfp_range * mean_l 1/(mua+musp). Outputs
+ * are normalised per photon and ring area; totals per photon. seed selects the photon streams.
+ * events (nullable) = free-flight events simulated. Synchronous on stream. */
+int mpss_mc_profile(mpss_ctx *ctx, const mpss_layer *layers, int nlayers, float mfp_range, int nsegments,
+                    uint64_t nphotons, uint64_t seed, double *reflectance, double *transmittance, double *total_r,
+                    double *total_t, uint64_t *events, void *stream);
+
 /* ---- host-side utilities (no HIP device needed): the product's own parse-time builders,
  * exposed so their results can be checked on a CPU-only machine. ---- */
 /* SampledSpectrum::FromRGB (spectrum.cpp:103-187); pbrt's "color"/"rgb" parameters use

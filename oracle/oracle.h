@@ -111,6 +111,13 @@ void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, con
 void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw);
 void o_scene_free(o_scene *s);
 
+/* ---- Monte-Carlo layered profile (mc.c; src/renderers/mcprofile.cpp:120-341,443-498) ---- */
+typedef struct { float mua, musp, ior, thickness; } o_mc_layer;
+/* Traces photons [photon_begin, photon_end) of nphotons and ADDS un-normalised ring tallies to
+ * raw_r / raw_t [nseg]; extent_out = mfp_range * mean mfp. */
+int o_mc_profile(const o_mc_layer *layers, int n, float mfp_range, int nseg, uint64_t nphotons, uint64_t seed,
+                 uint64_t photon_begin, uint64_t photon_end, double *raw_r, double *raw_t, double *extent_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,259 @@
+// mc_profile.hip -- ProfileRendererTask::TraceSinglePhoton (reference src/renderers/
+// mcprofile.cpp:229-326) as a persistent-lane GPU kernel, plus the host driver that normalises
+// the tallies like MonteCarloProfileRenderer::Render (:482-533).
+//
+// Each lane owns one photon at a time and advances it one event per loop trip (a free-flight
+// sample ends either in a scatter inside the layer or on an interface). A lane whose photon
+// has finished takes the next photon id from a global counter (one atomic per wave), so lanes
+// stay busy however long individual random walks run. Ring tallies accumulate in LDS doubles
+// (ds_add_f64) and are flushed to HBM once per workgroup. All arithmetic is FP64 as in the
+// reference (DVector / DRay / DPoint, mcprofile.cpp:46-49).
+#include "mc_profile.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace mpss {
+
+namespace {
+
+constexpr int kMcMaxSegments = 2048;
+
+// UniformSampleSphereD (mcprofile.cpp:51-58); u1 is drawn before u2
+__device__ __forceinline__ void sample_sphere_d(double u1, double u2, double &x, double &y, double &z) {
+    z = 1. - 2. * u1;
+    const double r = sqrt(fmax(0., 1. - z * z));
+    const double phi = 2. * 3.14159265358979323846 * u2;
+    x = r * cos(phi);
+    y = r * sin(phi);
+}
+
+// FrDiel<double> (core/reflection.cpp:72-80) with etat = 1
+__device__ __forceinline__ double fr_diel_d(double cosi, double cost, double etai, double etat) {
+    const double rparl = ((etat * cosi) - (etai * cost)) / ((etat * cosi) + (etai * cost));
+    const double rperp = ((etai * cosi) - (etat * cost)) / ((etai * cosi) + (etat * cost));
+    return (rparl * rparl + rperp * rperp) / 2.;
+}
+
+struct McArgs {
+    McScene sc;
+    uint64_t nphotons, seed;
+    unsigned long long *next;  // photon counter
+    double *refl, *trans;      // [nsegments] global tallies
+    unsigned long long *events;  // nullable: total free-flight events
+};
+
+__global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
+    __shared__ double h_r[kMcMaxSegments], h_t[kMcMaxSegments];
+    const McScene &sc = a.sc;
+    for (int i = threadIdx.x; i < sc.nsegments; i += blockDim.x) h_r[i] = h_t[i] = 0.;
+    __syncthreads();
+    const int lane = (int)(threadIdx.x & 63);
+    bool alive = false, exhausted = false;
+    double ox = 0., oy = 0., oz = 0., dx = 0., dy = 0., dz = 1.;
+    double thr = 1., len = 0., mfp = 1.;
+    int layer = 0;
+    McRng rng;
+    rng.s = 0;
+    unsigned long long nev = 0;
+    for (;;) {
+        // refill lanes whose photon has finished (one atomic per wave)
+        if (!exhausted) {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(!alive);
+            if (need) {
+                unsigned long long base = 0;
+                if (lane == (int)__builtin_ctzll(need))
+                    base = atomicAdd(a.next, (unsigned long long)__builtin_popcountll(need));
+                base = __shfl(base, (int)__builtin_ctzll(need));
+                if (!alive) {
+                    const uint64_t id = base + (uint64_t)__builtin_popcountll(need & ((1ull << lane) - 1ull));
+                    if (id < a.nphotons) {
+                        // TraceSinglePhoton setup (:233-241), then the outer loop's head (:245-248)
+                        rng.init(a.seed, id);
+                        ox = oy = oz = 0.;
+                        dx = dy = 0.;
+                        dz = 1.;
+                        thr = 1.;
+                        len = 0.;
+                        layer = 0;
+                        mfp = 1. / (double)sc.layer[0].musp;
+                        len *= mfp;
+                        alive = true;
+                    }
+                }
+                if (base + (unsigned long long)__builtin_popcountll(need) >= a.nphotons) exhausted = true;
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(alive) == 0) break;
+        if (!alive) continue;
+        ++nev;
+        const McLayer &L = sc.layer[layer];
+        // free flight (:251-252)
+        if (len == 0.) len = fmin(-log((double)1.f - rng.next()), 1e7) * mfp;
+        // MiniScene::Intersect (:153-185) with maxt = len
+        bool hit = false;
+        int iface = 0;
+        double t = 0., inv = 1.;
+        const double ct = dz;
+        if (ct != 0.) {
+            if (dz > 0.) {
+                const double nd = sc.depth[layer + 1];
+                if (nd - oz < ct * len) {
+                    hit = true;
+                    iface = layer + 1;
+                    t = (nd - oz) / ct;
+                    const double nior = (layer + 1 == sc.nlayers) ? 1. : (double)sc.layer[layer + 1].ior;
+                    inv = (double)L.ior / nior;
+                }
+            } else {
+                const double nd = sc.depth[layer];
+                if (nd - oz > ct * len) {
+                    hit = true;
+                    iface = layer;
+                    t = (nd - oz) / ct;
+                    const double nior = (layer == 0) ? 1. : (double)sc.layer[layer - 1].ior;
+                    inv = (double)L.ior / nior;
+                }
+            }
+        }
+        if (hit) {
+            const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            const double ex = px - ox, ey = py - oy, ez = pz - oz;
+            const double dist = sqrt(ex * ex + ey * ey + ez * ez);
+            thr *= exp((double)-L.mua * dist);
+            len = fmax(1e-7 * mfp, len - dist);
+            const double cosi = fmin(fmax(dz, -1.), 1.);
+            const bool up = dz < 0.;
+            const double sint2 = (1. - cosi * cosi) * inv * inv;
+            double cost = 0.;
+            bool reflect;
+            if (sint2 >= 1.) {
+                reflect = true;  // total internal reflection
+            } else {
+                cost = sqrt(fmax(0., 1. - sint2));
+                const double F = fr_diel_d(fabs(cosi), cost, inv, 1.);
+                reflect = rng.next() < F;
+            }
+            int target = layer;
+            if (reflect) {
+                dz = -dz;
+            } else {
+                target = up ? layer - 1 : layer + 1;
+                dx = inv * dx;
+                dy = inv * dy;
+                dz = up ? -cost : cost;
+            }
+            ox = px;
+            oy = py;
+            oz = pz;
+            if (target != layer) {
+                // book-keeping (:303-316)
+                if (iface == 0 || iface == sc.nlayers) {
+                    const double rd = sqrt(px * px + py * py + 0. * 0.);
+                    const int seg = (int)(rd * sc.nsegments / sc.extent);
+                    if (rd < sc.extent && seg < sc.nsegments) atomicAdd(iface == 0 ? &h_r[seg] : &h_t[seg], thr);
+                }
+                // outer loop tail (:330-340): roulette, then remaining length in the old layer's mfp units
+                bool dead = false;
+                if (thr < 1e-5) {
+                    const double q = thr * 1e5;
+                    if (rng.next() > q)
+                        dead = true;
+                    else
+                        thr /= q;
+                }
+                if (!dead) {
+                    len *= (double)L.musp;
+                    layer = target;
+                    if (layer < 0 || layer >= sc.nlayers) {
+                        dead = true;
+                    } else {
+                        mfp = 1. / (double)sc.layer[layer].musp;  // next outer loop's head
+                        len *= mfp;
+                    }
+                }
+                if (dead) alive = false;
+            }
+        } else {
+            // scatter inside the layer (:319-327)
+            ox = ox + dx * len;
+            oy = oy + dy * len;
+            oz = oz + dz * len;
+            thr *= exp((double)-L.mua * len);
+            len = 0.;
+            const double u1 = rng.next(), u2 = rng.next();
+            sample_sphere_d(u1, u2, dx, dy, dz);
+        }
+    }
+    if (a.events) atomicAdd(a.events, nev);
+    __syncthreads();
+    for (int i = threadIdx.x; i < sc.nsegments; i += blockDim.x) {
+        if (h_r[i] != 0.) atomicAdd(&a.refl[i], h_r[i]);
+        if (h_t[i] != 0.) atomicAdd(&a.trans[i], h_t[i]);
+    }
+}
+
+}  // namespace
+
+McScene make_mc_scene(const McLayer *layers, int n, double mfp_range, int nsegments) {
+    if (n < 1 || n > kMcMaxLayers) throw Error(-1, "mc_profile: 1..8 layers supported");
+    if (nsegments < 1 || nsegments > kMcMaxSegments) throw Error(-1, "mc_profile: 1..2048 segments supported");
+    McScene sc{};
+    sc.nlayers = n;
+    double depth = 0., mfp_total = 0.;
+    sc.depth[0] = 0.;
+    for (int i = 0; i < n; ++i) {
+        if (!(layers[i].musp > 0.f) || !(layers[i].mua >= 0.f) || !(layers[i].thickness > 0.f))
+            throw Error(-1, "mc_profile: layers need musp > 0, mua >= 0, thickness > 0");
+        sc.layer[i] = layers[i];
+        sc.depth[i + 1] = depth += (double)layers[i].thickness;
+        mfp_total += 1. / ((double)layers[i].mua + (double)layers[i].musp);  // Render (:460-464)
+    }
+    sc.extent = mfp_range * (mfp_total / (double)n);
+    sc.nsegments = nsegments;
+    return sc;
+}
+
+void run_mc_profile(const McScene &sc, uint64_t nphotons, uint64_t seed, double *refl, double *trans,
+                    double *total_r, double *total_t, uint64_t *events, hipStream_t stream) {
+    DevBuf<double> d_r, d_t;
+    DevBuf<unsigned long long> d_cnt;
+    d_r.alloc(sc.nsegments);
+    d_t.alloc(sc.nsegments);
+    d_cnt.alloc(2);
+    MPSS_HIP(hipMemsetAsync(d_r.ptr, 0, sizeof(double) * sc.nsegments, stream));
+    MPSS_HIP(hipMemsetAsync(d_t.ptr, 0, sizeof(double) * sc.nsegments, stream));
+    MPSS_HIP(hipMemsetAsync(d_cnt.ptr, 0, sizeof(unsigned long long) * 2, stream));
+    McArgs a{sc, nphotons, seed, d_cnt.ptr, d_r.ptr, d_t.ptr, d_cnt.ptr + 1};
+    int dev = 0, ncu = 0;
+    MPSS_HIP(hipGetDevice(&dev));
+    MPSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const uint64_t lanes_needed = (nphotons + 255) / 256;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ncu * 8, lanes_needed));
+    if (nphotons > 0) hipLaunchKernelGGL(mc_profile_kernel, dim3(blocks), dim3(256), 0, stream, a);
+    MPSS_HIP(hipGetLastError());
+    std::vector<double> r(sc.nsegments), t(sc.nsegments);
+    unsigned long long cnt[2];
+    MPSS_HIP(hipMemcpyAsync(r.data(), d_r.ptr, sizeof(double) * sc.nsegments, hipMemcpyDeviceToHost, stream));
+    MPSS_HIP(hipMemcpyAsync(t.data(), d_t.ptr, sizeof(double) * sc.nsegments, hipMemcpyDeviceToHost, stream));
+    MPSS_HIP(hipMemcpyAsync(cnt, d_cnt.ptr, sizeof(cnt), hipMemcpyDeviceToHost, stream));
+    MPSS_HIP(hipStreamSynchronize(stream));
+    // normalise by photons and ring area (Render, :482-498)
+    double tr = 0., tt = 0.;
+    for (int i = 0; i < sc.nsegments; ++i) {
+        const double sum = (double)(2 * i + 1) * sc.extent / sc.nsegments;
+        const double h = sc.extent / sc.nsegments;
+        const double area = 3.14159265358979323846 * sum * h;
+        const double factor = (double)nphotons * area;
+        tr += r[i];
+        tt += t[i];
+        refl[i] = r[i] / factor;
+        trans[i] = t[i] / factor;
+    }
+    *total_r = tr / (double)nphotons;
+    *total_t = tt / (double)nphotons;
+    if (events) *events = cnt[1];
+}
+
+}  // namespace mpss

@@ -6,6 +6,7 @@
 
 #include "../../include/mpss.h"
 #include "context.h"
+#include "mc_profile.h"
 #include "spectral.h"
 
 using namespace mpss;
@@ -276,6 +277,19 @@ int mpss_render_tiles(mpss_ctx *c, int spp, uint32_t seed, int n, const int32_t 
 
 // ---------------------------------------------------------------- host-side utilities
 extern "C" {
+
+int mpss_mc_profile(mpss_ctx *c, const mpss_layer *layers, int n, float mfp_range, int nseg, uint64_t nphotons,
+                    uint64_t seed, double *refl, double *trans, double *tr, double *tt, uint64_t *events,
+                    void *stream) {
+    return guarded([&] {
+        require(c && layers && refl && trans && tr && tt, "mpss_mc_profile: null argument");
+        Context &ctx = *reinterpret_cast<Context *>(c);
+        MPSS_HIP(hipSetDevice(ctx.config().device));
+        static_assert(sizeof(mpss_layer) == sizeof(McLayer), "layer layout");
+        const McScene sc = make_mc_scene(reinterpret_cast<const McLayer *>(layers), n, (double)mfp_range, nseg);
+        run_mc_profile(sc, nphotons, seed, refl, trans, tr, tt, events, (hipStream_t)stream);
+    });
+}
 
 int mpss_host_tessellate(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
                          const int32_t *idx, const float *o2w, const float *w2o, int flip, uint32_t mat,

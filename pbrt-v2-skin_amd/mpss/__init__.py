@@ -97,6 +97,8 @@ _sig("mpss_set_instrumentation", C.c_int, [vp, C.c_int, C.c_int])
 _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
 _sig("mpss_render_tiles", C.c_int, [vp, C.c_int, u32, C.c_int, C.POINTER(C.c_int32), C.POINTER(vp), vp])
 _sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
+_sig("mpss_mc_profile", C.c_int, [vp, f32p, C.c_int, C.c_float, C.c_int, C.c_uint64, C.c_uint64, vp, vp,
+                                  C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64), vp])
 _sig("mpss_host_tessellate", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32,
                                        C.c_float, C.c_int, vp, u32p])
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
@@ -308,6 +310,16 @@ class Context:
 
     def save_pointsfile(self, path):
         check(_lib.mpss_save_pointsfile(self.h, os.fsencode(path)))
+
+    def mc_profile(self, layers, mfp_range=16.0, nsegments=1024, nphotons=100, seed=89, stream=None):
+        """Monte-Carlo layered profile; layers: [(mua, musp, ior, thickness), ...]."""
+        lay = np.ascontiguousarray(layers, np.float32).reshape(-1, 4)
+        r = np.zeros(nsegments, np.float64)
+        t = np.zeros(nsegments, np.float64)
+        tr, tt, ev = C.c_double(), C.c_double(), C.c_uint64()
+        check(_lib.mpss_mc_profile(self.h, lay, len(lay), mfp_range, nsegments, nphotons, seed, r.ctypes.data,
+                                   t.ctypes.data, C.byref(tr), C.byref(tt), C.byref(ev), stream))
+        return dict(reflectance=r, transmittance=t, total_r=tr.value, total_t=tt.value, events=ev.value)
 
     def irradiance(self):
         n = C.c_uint32()
