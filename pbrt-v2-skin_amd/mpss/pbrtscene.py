@@ -158,6 +158,7 @@ class Scene:
         self.meshes = []     # dicts: P (world), N, S, uv, indices, o2w, w2o, reverse, material
         self.lights = []     # dicts: center, radius, L (rgb), nsamples
         self.base_dir = "."
+        self.renderer = None  # ("mcprofile", ParamSet) when the file selects the MC profile renderer
 
     def raster_to_camera(self):
         return camera_matrices(self.world_to_camera, self.fov, self.xres, self.yres, self.screen)
@@ -241,6 +242,10 @@ def load(path, **override):
                     if cls != "multipolesubsurface":
                         raise ValueError("SurfaceIntegrator %r is outside this path" % cls)
                     sc.integrator = {k: v[1][0] for k, v in ps.items()}
+                elif d == "Renderer":
+                    if cls not in ("sampler", "mcprofile"):
+                        raise ValueError("Renderer %r is outside this path" % cls)
+                    sc.renderer = (cls, ps) if cls == "mcprofile" else None
                 elif d in ("PixelFilter",):
                     if cls != "box" or ps.one("xwidth", 0.5) != 0.5 or ps.one("ywidth", 0.5) != 0.5:
                         raise ValueError("only the default 0.5-wide box filter is supported")

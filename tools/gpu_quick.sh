@@ -9,3 +9,5 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q $KARG > gpurun_out/pytest_
 tail -2 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
 cat gpurun_out/bench.log | grep metric
+timeout -k 10 300 python tools/bench_mc.py --cpu-seconds 5 > gpurun_out/bench_mc.log 2>&1 || { echo "bench_mc failed"; tail -30 gpurun_out/bench_mc.log; exit 1; }
+cat gpurun_out/bench_mc.log
