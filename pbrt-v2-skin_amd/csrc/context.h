@@ -80,6 +80,8 @@ private:
     DevBuf<int> ws_count_;
     DevBuf<float4> ws_q_, ws_mo_, ws_ha_, ws_hb_, ws_xyz_;
     DevBuf<uint32_t> ws_hs_, ws_spill_;
+    DevBuf<unsigned char> ws_terms_;
+    int64_t ws_terms_n_ = 0;
     int64_t ws_px_ = 0;
     DevBuf<float> ws_ld_;
     int64_t ws_n_ = 0, ws_hits_ = 0;

@@ -25,6 +25,8 @@
 namespace mpss {
 
 constexpr int kGroups = 8;
+constexpr int kBandBlock = 1024;  // queries per workgroup (16 waves of one band group)
+constexpr int kLdsRd = 4096;      // leading Rd entries of each of the group's 4 bands kept in LDS (64 KB)
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -88,10 +90,12 @@ struct __attribute__((aligned(4))) RdPair {
 // serialize. t = fract(f) equals f - (float)(uint)f exactly for 0 <= f < 2^24.
 // acc[j] += Rd_j(d2) * e[j] (* w) exactly as sampleProfile + the Mo() product
 // (multipole.cpp:60-73; diffusionutil.h:185,197).
+// The first kLdsRd entries of each band (the near field: leaf points and close clusters, about
+// 40 % of the red bands' lookups) come from the workgroup's LDS copy, the rest from L2.
 template <bool POINT>
 __device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], const float rcp[4], float lm1,
                                                    uint32_t smax, float d2, const float e[4], float w,
-                                                   float acc[4]) {
+                                                   float acc[4], const float (*lt)[kLdsRd]) {
     float f[4];
     bool ok[4];
     RdPair v[4];
@@ -100,7 +104,14 @@ __device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], con
         f[j] = d2 * rcp[j];
         ok[j] = f[j] < lm1;
         const uint32_t s = ok[j] ? (uint32_t)f[j] : smax;
-        v[j] = *reinterpret_cast<const RdPair *>(tb[j] + s);
+        // two unconditional loads and a select (a branch here makes the compiler merge both
+        // paths into flat loads): lanes served by LDS point their L2 load at one shared line
+        const bool in_lds = s + 1 < (uint32_t)kLdsRd;
+        const uint32_t sl = in_lds ? s : 0u, sg = in_lds ? smax : s;
+        const float la = lt[j][sl], lb = lt[j][sl + 1];
+        const RdPair g = *reinterpret_cast<const RdPair *>(tb[j] + sg);
+        v[j].a = in_lds ? la : g.a;
+        v[j].b = in_lds ? lb : g.b;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -126,7 +137,7 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 
 template <bool COUNT>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
-                                                 float acc[4], int &k_nodes, int &k_pts) {
+                                                 float acc[4], int &k_nodes, int &k_pts, const float (*lt)[kLdsRd]) {
     float rcp[4];
     const float *tb[4];
 #pragma unroll
@@ -165,7 +176,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-                    band_rd_accumulate<false>(tb, rcp, lm1, smax, d2, e, 1.f, acc);
+                    band_rd_accumulate<false>(tb, rcp, lm1, smax, d2, e, 1.f, acc, lt);
                 } else {
                     open = true;
                 }
@@ -185,7 +196,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-                    band_rd_accumulate<true>(tb, rcp, lm1, smax, d2, e, ph.w, lacc);
+                    band_rd_accumulate<true>(tb, rcp, lm1, smax, d2, e, ph.w, lacc, lt);
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[j] += lacc[j];

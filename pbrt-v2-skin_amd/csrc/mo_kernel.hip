@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
 
 // ---------------------------------------------------------------------------------------
 // Spectrally sharded gather (mo_band.h): block b runs band group b % 8 for queries
-// [256 * (b / 8), +256); query count read on the device (render path: compacted list).
+// [1024 * (b / 8), +1024); query count read on the device (render path: compacted list).
 // ---------------------------------------------------------------------------------------
 struct BandArgs {
     BandTree t;
@@ -211,11 +211,17 @@ struct BandArgs {
 };
 
 template <bool COUNT>
-__global__ __launch_bounds__(256) void mo_band_kernel(BandArgs a) {
+__global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
+    __shared__ float lt[4][kLdsRd];
     const int grp = (int)(blockIdx.x & (kGroups - 1));
-    const int base = (int)(blockIdx.x / kGroups) * 256;
+    const int base = (int)(blockIdx.x / kGroups) * kBandBlock;
     const int nq = a.count ? *a.count : a.nq;
     if (base >= nq) return;
+    for (int i = (int)threadIdx.x; i < 4 * kLdsRd; i += kBandBlock) {  // the group's near-field Rd entries
+        const int j = i / kLdsRd, k = i % kLdsRd, c = a.t.groups.band[grp][j];
+        lt[j][k] = (c >= 0 && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+    }
+    __syncthreads();
     const int q = base + (int)threadIdx.x;
     const bool valid = q < nq;
     float px = 0.f, py = 0.f, pz = 0.f;
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(256) void mo_band_kernel(BandArgs a) {
     }
     float acc[4];
     int kn = 0, kp = 0;
-    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, live, acc, kn, kp);
+    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, live, acc, kn, kp, lt);
     if (!live) return;
     if (a.out4) {
         a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -346,11 +352,11 @@ void launch_mo_band(DeviceOctree &t, const DeviceProfile &p, float max_error, in
     a.nq = nq_max;
     a.out4 = out4;
     a.counts = counts;
-    const unsigned blocks = (unsigned)((nq_max + 255) / 256) * kGroups;
+    const unsigned blocks = (unsigned)((nq_max + kBandBlock - 1) / kBandBlock) * kGroups;
     if (counts)
-        hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
     else
-        hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
     MPSS_HIP(hipGetLastError());
 }
 
@@ -389,11 +395,11 @@ void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_
         b.out = out;
         b.out_stride = out_stride;
         b.counters = counters;
-        const unsigned blocks = (unsigned)((nq + 255) / 256) * kGroups;
+        const unsigned blocks = (unsigned)((nq + kBandBlock - 1) / kBandBlock) * kGroups;
         if (count)
-            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(256), 0, stream, b);
+            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, b);
         else
-            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(256), 0, stream, b);
+            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, b);
         MPSS_HIP(hipGetLastError());
         return;
     }

@@ -88,7 +88,12 @@ struct BandPos {
 };
 
 __global__ void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
-__global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits);
+struct DirectTerms;
+__global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits, int ns_max,
+                                    DirectTerms *terms);
+__global__ void shade_nolight_kernel(RenderScene sc, SampleRecs rec, int max_hits);
+__global__ void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
+                                      const DirectTerms *terms);
 // Li assembly per slot (L = Le + SSS + Ld, sample filter, ToXYZ), then the box-filtered film.
 __global__ void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits);
 __global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, float *out, int out_stride_px);

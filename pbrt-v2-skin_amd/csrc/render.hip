@@ -288,24 +288,40 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
 }
 
 // ------------------------------------------------------------------ shading + direct light
-// The rest of MultipoleSubsurfaceIntegrator::Li for one compacted surface hit (full waves):
-// shading geometry, the Mo() query of a BSSRDF hit, and UniformSampleAllLights (integrator.cpp:
-// 47-77) with EstimateDirect (:117-174). Spectra are not held per light sample: a BSDF value is
-// R[c] * D * G * F / den (Microfacet::f) with scalar D, G, F, den, so each sample keeps only its
-// scalars and the per-band sums are formed in the reference's operation order in one pass.
+// The rest of MultipoleSubsurfaceIntegrator::Li for the compacted surface hits, with one lane
+// per (hit, light, light-sample j) of UniformSampleAllLights (integrator.cpp:47-77): each lane
+// runs one EstimateDirect (:117-174) -- light sample + shadow ray, BSDF sample + ray -- and
+// stores its scalars; direct_combine_kernel then forms the per-band sums in the reference's
+// order (j ascending inside a light, lights ascending). A BSDF value is R[c] * D * G * F / den
+// (Microfacet::f) with scalar D, G, F, den, so no lane carries a 30-band spectrum.
+struct DirectTerms {       // 16 floats: one EstimateDirect
+    float D1, G1, F1, den1, k1;            // light sampling: f * Li * k1
+    float D2, G2, F2, den2, adn, w2, pdf2; // BSDF sampling: f * Li * adn * w2 / pdf2
+    uint32_t use;                          // bit 0: light term, bit 1: BSDF term
+    float pad[3];
+};
+static_assert(sizeof(DirectTerms) == 64, "one 64-B record per light sample");
+
 __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
-                                                           int max_hits) {
+                                                           int max_hits, int ns_max, DirectTerms *terms) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
-    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int per_hit = sc.nlights * ns_max;
     const int nhits = *rec.hit_count;
-    if ((int)(blockIdx.x * blockDim.x) >= nhits) return;
+    if ((int64_t)blockIdx.x * blockDim.x >= (int64_t)nhits * per_hit) return;
+    const int slot = (int)(gid / per_hit);
     if (slot >= nhits || slot >= max_hits) return;
+    const int lj = (int)(gid % per_hit), l = lj / ns_max, j = lj % ns_max;
     const uint32_t hs = rec.hit_s[slot];
     if (hs & 0x40000000u) {  // an area light seen directly: no shading point, no Mo()
-        rec.hit_q[slot] = make_float4(0.f, 0.f, 0.f, -1.f);
+        if (lj == 0) rec.hit_q[slot] = make_float4(0.f, 0.f, 0.f, -1.f);
         return;
     }
+    const RenderLight &L = sc.lights[l];
+    const int ns = L.nsamples_round;
+    DirectTerms out{};
+    if (j >= ns && lj != 0) return;
     const float4 ha = rec.hit_a[slot], hb = rec.hit_b[slot];
     const int s = (int)(hs & 0xffffu);
     const uint32_t mid = (hs >> REC_MAT_SHIFT) & 0xffu;
@@ -321,99 +337,119 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - ha.y - ha.z, ha.y, ha.z);
     const V3 wo = -d;
     const RenderMaterial &mat = sc.materials[mid];
-    float ct = absdot(wo, fr.nn);
-    ct = ct < 1.f ? ct : 1.f;
-    rec.hit_q[slot] = make_float4(fr.p.x, fr.p.y, fr.p.z, sss ? ct : -1.f);
-    float ld[NB];
-    for (int c = 0; c < NB; ++c) ld[c] = 0.f;
+    if (lj == 0) {
+        float ct = absdot(wo, fr.nn);
+        ct = ct < 1.f ? ct : 1.f;
+        rec.hit_q[slot] = make_float4(fr.p.x, fr.p.y, fr.p.z, sss ? ct : -1.f);
+        if (j >= ns) return;
+    }
     const V3 wo_l = to_local(fr, wo);
     const float ng_wo = dot(wo, fr.ng);
-    for (int l = 0; l < sc.nlights; ++l) {
-        const RenderLight &L = sc.lights[l];
-        const int ns = L.nsamples_round;
-        float Ld[NB];
-        for (int c = 0; c < NB; ++c) Ld[c] = 0.f;
-        const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
-        const uint32_t base = (uint32_t)(s ^ (int)xr) * (uint32_t)ns;
-        const uint32_t sl0 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS),
-                       sl1 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
-                       sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR),
-                       sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u);
-        for (int j = 0; j < ns; ++j) {
-            const uint32_t nidx = base + (uint32_t)j;
-            // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
-            MfTerms t1{0.f, 0.f, 0.f, 1.f, true};
-            float k1 = 0.f;
-            bool use1 = false;
-            const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
-            float lightPdf = ls.pdf;
-            if (lightPdf > 0.f && ls.nonblack && mat.has_refl) {
-                const V3 wi_l = to_local(fr, ls.wi);
-                const bool refl = dot(ls.wi, fr.ng) * ng_wo > 0.f;  // BSDF::f ng test
-                t1 = microfacet_terms(mat.mf, wo_l, wi_l);
-                bool fblack = !refl || t1.zero;
-                if (!fblack) {
-                    fblack = true;
-                    for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t1.D * t1.G * t1.F / t1.den) == 0.f;
-                }
-                if (!fblack && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
-                    const float bsdfPdf = microfacet_pdf(mat.mf, wo_l, wi_l);
-                    const float w = power_heuristic(lightPdf, bsdfPdf);
-                    k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
-                    use1 = true;
-                }
+    const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
+    const uint32_t nidx = (uint32_t)(s ^ (int)xr) * (uint32_t)ns + (uint32_t)j;
+    const uint32_t sl0 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS), sl1 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
+                   sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR), sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u);
+    // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
+    const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
+    float lightPdf = ls.pdf;
+    if (lightPdf > 0.f && ls.nonblack && mat.has_refl) {
+        const V3 wi_l = to_local(fr, ls.wi);
+        const bool refl = dot(ls.wi, fr.ng) * ng_wo > 0.f;  // BSDF::f ng test
+        const MfTerms t1 = microfacet_terms(mat.mf, wo_l, wi_l);
+        bool fblack = !refl || t1.zero;
+        if (!fblack) {
+            fblack = true;
+            for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t1.D * t1.G * t1.F / t1.den) == 0.f;
+        }
+        if (!fblack && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
+            const float bsdfPdf = microfacet_pdf(mat.mf, wo_l, wi_l);
+            const float w = power_heuristic(lightPdf, bsdfPdf);
+            out.D1 = t1.D;
+            out.G1 = t1.G;
+            out.F1 = t1.F;
+            out.den1 = t1.den;
+            out.k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
+            out.use |= 1u;
+        }
+    }
+    // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
+    if (mat.has_refl) {
+        V3 wi_l;
+        float bsdfPdf;
+        beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+        if (bsdfPdf != 0.f) {
+            const V3 wi = to_world(fr, wi_l);
+            const bool refl = dot(wi, fr.ng) * ng_wo > 0.f;
+            const MfTerms t2 = microfacet_terms(mat.mf, wo_l, wi_l);
+            bool fblack = !refl || t2.zero;
+            if (!fblack) {
+                fblack = true;
+                for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t2.D * t2.G * t2.F / t2.den) == 0.f;
             }
-            // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
-            MfTerms t2{0.f, 0.f, 0.f, 1.f, true};
-            float adn = 0.f, w2 = 0.f, pdf2 = 1.f;
-            bool use2 = false;
-            if (mat.has_refl) {
-                V3 wi_l;
-                float bsdfPdf;
-                beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
-                if (bsdfPdf != 0.f) {
-                    const V3 wi = to_world(fr, wi_l);
-                    const bool refl = dot(wi, fr.ng) * ng_wo > 0.f;
-                    t2 = microfacet_terms(mat.mf, wo_l, wi_l);
-                    bool fblack = !refl || t2.zero;
-                    if (!fblack) {
-                        fblack = true;
-                        for (int c = 0; c < NB; ++c)
-                            fblack = fblack && (mat.R[c] * t2.D * t2.G * t2.F / t2.den) == 0.f;
+            if (!fblack && bsdfPdf > 0.f) {
+                lightPdf = sphere_pdf(L.s, fr.p, wi);
+                if (lightPdf != 0.f) {
+                    const float w = power_heuristic(bsdfPdf, lightPdf);
+                    const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
+                    // Li = lightIsect.Le(-wi) when the hit primitive is this light
+                    if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
+                        out.D2 = t2.D;
+                        out.G2 = t2.G;
+                        out.F2 = t2.F;
+                        out.den2 = t2.den;
+                        out.adn = absdot(wi, fr.nn);
+                        out.w2 = w;
+                        out.pdf2 = bsdfPdf;
+                        out.use |= 2u;
                     }
-                    if (!fblack && bsdfPdf > 0.f) {
-                        lightPdf = sphere_pdf(L.s, fr.p, wi);
-                        if (lightPdf != 0.f) {
-                            const float w = power_heuristic(bsdfPdf, lightPdf);
-                            const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
-                            // Li = lightIsect.Le(-wi) when the hit primitive is this light
-                            if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
-                                adn = absdot(wi, fr.nn);
-                                w2 = w;
-                                pdf2 = bsdfPdf;
-                                use2 = true;
-                            }
-                        }
-                    }
-                }
-            }
-            if (use1 || use2) {  // else ed = 0 and Ld += 0 changes nothing (Ld is never -0)
-                for (int c = 0; c < NB; ++c) {
-                    float ed = 0.f;
-                    if (use1) ed += (mat.R[c] * t1.D * t1.G * t1.F / t1.den) * L.Lemit[c] * k1;
-                    if (use2) ed += (mat.R[c] * t2.D * t2.G * t2.F / t2.den) * L.Lemit[c] * adn * w2 / pdf2;
-                    Ld[c] += ed;
                 }
             }
         }
-        for (int c = 0; c < NB; ++c) ld[c] += Ld[c] / (float)ns;
     }
+    terms[gid] = out;
+}
+
+// A scene without lights: no direct light and (Preprocess returned early) no octree.
+__global__ __launch_bounds__(256) void shade_nolight_kernel(RenderScene sc, SampleRecs rec, int max_hits) {
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if (slot >= nhits || slot >= max_hits) return;
+    rec.hit_q[slot] = make_float4(0.f, 0.f, 0.f, -1.f);
     float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int c = 4 * k;
-        row[k] = make_float4(ld[c], ld[c + 1], c + 2 < NB ? ld[c + 2] : 0.f, c + 3 < NB ? ld[c + 3] : 0.f);
+    for (int k = 0; k < 8; ++k) row[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ld[c] = sum over lights of (sum over j of (0 + light term + BSDF term)) / ns, band by band in
+// the order UniformSampleAllLights accumulates (Ld += EstimateDirect; L += Ld / nSamples).
+__global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
+                                                             const DirectTerms *__restrict__ terms) {
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if (slot >= nhits || slot >= max_hits) return;
+    if (rec.hit_s[slot] & 0x40000000u) return;
+    const RenderMaterial &mat = sc.materials[(rec.hit_s[slot] >> REC_MAT_SHIFT) & 0xffu];
+    const DirectTerms *t = terms + (size_t)slot * sc.nlights * ns_max;
+    float *row = rec.ld + (size_t)slot * ROW;
+    for (int c = 0; c < NB; ++c) {
+        float ld = 0.f;
+        for (int l = 0; l < sc.nlights; ++l) {
+            const RenderLight &L = sc.lights[l];
+            const int ns = L.nsamples_round;
+            float Ld = 0.f;
+            for (int j = 0; j < ns; ++j) {
+                const DirectTerms &e = t[l * ns_max + j];
+                if (!e.use) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
+                float ed = 0.f;
+                if (e.use & 1u) ed += (mat.R[c] * e.D1 * e.G1 * e.F1 / e.den1) * L.Lemit[c] * e.k1;
+                if (e.use & 2u) ed += (mat.R[c] * e.D2 * e.G2 * e.F2 / e.den2) * L.Lemit[c] * e.adn * e.w2 / e.pdf2;
+                Ld += ed;
+            }
+            ld += Ld / (float)ns;
+        }
+        row[c] = ld;
     }
+    row[30] = 0.f;
+    row[31] = 0.f;
 }
 
 // ------------------------------------------------------------------ film

@@ -326,9 +326,24 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         {
             SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
                            ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+            int ns_max = 1;
+            for (const SphereLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
+            const int64_t lanes = total * std::max<int64_t>(1, (int64_t)scene_.lights.size()) * ns_max;
+            if (ws_terms_n_ < lanes) {
+                ws_terms_.alloc((size_t)lanes * 64);
+                ws_terms_n_ = lanes;
+            }
+            DirectTerms *terms = reinterpret_cast<DirectTerms *>(ws_terms_.ptr);
             time_begin(stream, ev);
-            hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
-                               rec, spp, seed, (int)total);
+            if (!scene_.lights.empty()) {
+                hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream,
+                                   sc, rec, spp, seed, (int)total, ns_max, terms);
+                hipLaunchKernelGGL(direct_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                                   sc, rec, (int)total, ns_max, (const DirectTerms *)terms);
+            } else {
+                hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                                   sc, rec, (int)total);
+            }
             time_end(stream, ev, 4);
         }
         if (m) {
