@@ -92,3 +92,23 @@ def test_image_parity_ragged_tile(pair):
     got = _render_gpu(torch, ctx, sc, x0, x1, y0, y1, 9)
     ref = o.render_tile(sc.spp, 9, x0, x1, y0, y1)
     _check(got, ref)
+
+
+def test_c1_tissue_full_frame(mpss, oracle):
+    """Config C1 (BASELINE.json configs[0]): scenes/tissue.pbrt at its full 256x256, 8 spp, the
+    reference's CPU-runnable case -- the whole frame on the GPU against the CPU restatement."""
+    import torch
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "tissue.pbrt"))
+    assert (sc.xres, sc.yres, sc.spp) == (256, 256, 8)
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=2)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    assert pts.tobytes() == o.tessellate().tobytes()
+    E = o.irradiance(pts, 2)
+    np.testing.assert_allclose(ctx.irradiance(), E, rtol=1e-5, atol=1e-6 * float(E.max()))
+    o.set_octree(pts, E)
+    got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 13)
+    ref = o.render_tile(sc.spp, 13, 0, sc.xres, 0, sc.yres)
+    _check(got, ref)
