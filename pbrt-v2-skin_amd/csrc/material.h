@@ -41,6 +41,9 @@ struct RhoTable {
 void skin_layer_params(const SkinParams &p, LayerParams &out);
 void build_profile(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
                    int nthreads = 0);
+// The same profile built on the current HIP device (profile_gpu.hip); out is filled on the host.
+void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
+                       hipStream_t stream = 0);
 void build_rho_table(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
                      RhoTable &out, int nthreads = 0);
 

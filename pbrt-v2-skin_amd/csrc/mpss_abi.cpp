@@ -57,6 +57,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->exact_mo = 0;
     c->kernel_timing = 0;
     c->count_traversal = 0;
+    c->profile_on_host = 0;
     c->max_batch_samples = (int64_t)1 << 24;
 }
 
