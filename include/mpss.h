@@ -85,8 +85,7 @@ typedef struct {
     float layer_ior[2];                 /* "skinlayer layers" ior */
     float albedo[MPSS_NBANDS];          /* constant "albedo" texture value (default Spectrum(1)) */
     float Kr[MPSS_NBANDS];              /* "Kr" (default Spectrum(1)): Microfacet reflection */
-    float Kt[MPSS_NBANDS];              /* "Kt" (default Spectrum(1)); non-black is rejected for now
-                                           (MicrofacetTransmission not ported; skin scenes set [0 0 0]) */
+    float Kt[MPSS_NBANDS];              /* "Kt" (default Spectrum(1)): MicrofacetTransmission */
     int desired_length;   /* "desiredlength" = 512 */
     int lerp_on_thin_slab;/* "lerponthinslab" = true */
     int double_ref_sslf;  /* "doublerefsslf" = false (FixedFresnelDielectric) */

@@ -98,9 +98,9 @@ typedef struct {  /* SurfacePoint, renderers/surfacepoints.h:45-55 (44-byte reco
 } o_surface_point;
 typedef struct o_scene o_scene;
 o_scene *o_scene_create(int xres, int yres, const float *raster_to_camera, const float *camera_to_world);
-int o_scene_add_material(o_scene *s, const float *R, const float *albedo, float mix, float roughness, float eta,
-                         int fixed_fresnel, const float *rho, int n_rho, int is_mc, const float *rd_table, int L,
-                         const float *rcp);
+int o_scene_add_material(o_scene *s, const float *R, const float *T /* nullable: black */, const float *albedo,
+                         float mix, float roughness, float eta, int fixed_fresnel, const float *rho, int n_rho,
+                         int is_mc, const float *rd_table, int L, const float *rcp);
 int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
                      const int32_t *idx, const float *o2w, const float *w2o, int flip, int material);
 int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples);

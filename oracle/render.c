@@ -117,7 +117,7 @@ static float sobol(uint32_t n, uint32_t scramble) { /* montecarlo.h Sobol2 */
     return r < ONE_MINUS_EPS ? r : ONE_MINUS_EPS;
 }
 /* dimension ids of one camera sample (see DESIGN.md "replay mode") */
-enum { D_IMAGE = 0, D_LIGHT_POS = 2, D_BSDF_DIR = 4, D_IRR_POS = 6, D_PERM = 9 };
+enum { D_IMAGE = 0, D_LIGHT_POS = 2, D_BSDF_DIR = 4, D_BSDF_COMP = 5, D_IRR_POS = 6, D_PERM = 9 };
 
 /* ------------------------------------------------------------------ scene */
 typedef struct {
@@ -136,9 +136,9 @@ typedef struct {
 } o_light;
 
 typedef struct {
-    float R[O_NB], alb_mix[O_NB], alb_1mmix[O_NB];
+    float R[O_NB], T[O_NB], alb_mix[O_NB], alb_1mmix[O_NB];
     float rough2, eta;
-    int fixed_fresnel, is_mc, has_refl;
+    int fixed_fresnel, is_mc, has_refl, has_trans;
     float *rho;
     int n_rho;
     float *rd;
@@ -180,16 +180,19 @@ static float *dupf(const float *a, size_t n) {
     return r;
 }
 
-int o_scene_add_material(o_scene *s, const float *R, const float *albedo, float mix, float roughness, float eta,
-                         int fixed_fresnel, const float *rho, int n_rho, int is_mc, const float *rd, int L,
-                         const float *rcp) {
+int o_scene_add_material(o_scene *s, const float *R, const float *T, const float *albedo, float mix,
+                         float roughness, float eta, int fixed_fresnel, const float *rho, int n_rho, int is_mc,
+                         const float *rd, int L, const float *rcp) {
     s->mats = (o_mat *)realloc(s->mats, (s->nmats + 1) * sizeof(o_mat));
     o_mat *m = &s->mats[s->nmats];
     memset(m, 0, sizeof(*m));
     m->has_refl = 0;
+    m->has_trans = 0;
     for (int c = 0; c < O_NB; ++c) {
         m->R[c] = R[c];
+        m->T[c] = T ? T[c] : 0.f;
         if (R[c] != 0.f) m->has_refl = 1;
+        if (m->T[c] != 0.f) m->has_trans = 1;
         m->alb_mix[c] = fpowf_(albedo[c], mix);          /* Pow(albedo, mix): IrradianceTask */
         m->alb_1mmix[c] = fpowf_(albedo[c], 1.f - mix);  /* Pow(albedo, 1 - mix): Li */
         m->rcp[c] = rcp[c];
@@ -505,8 +508,8 @@ static float fresnel(float cosi, float eta_i, float eta_t, int fixed) {
 static float geomG(v3 wo, v3 wi, v3 wh) {
     float a = fabsf(wh.z), wowh = absdot(wo, wh);
     float g1 = 2.f * a * fabsf(wo.z) / wowh, g2 = 2.f * a * fabsf(wi.z) / wowh;
-    float m = g1 < g2 ? g1 : g2;
-    return 1.f < m ? 1.f : m;
+    float m = g2 < g1 ? g2 : g1; /* std::min(g1, g2) */
+    return m < 1.f ? m : 1.f;    /* std::min(1.f, m) */
 }
 /* Microfacet::f per band: R * D * G * F / (4 cos_i cos_o); returns 0 if the lobe is zero */
 static int mf_f(const o_mat *m, v3 wo, v3 wi, float f[O_NB]) {
@@ -545,16 +548,93 @@ static v3 to_world(const frame_t *f, v3 v) {
     return mk(f->sn.x * v.x + f->tn.x * v.y + f->nn.x * v.z, f->sn.y * v.x + f->tn.y * v.y + f->nn.y * v.z,
               f->sn.z * v.x + f->tn.z * v.y + f->nn.z * v.z);
 }
-/* BSDF::f with the ng hemisphere test: a BRDF contributes only on the reflection side.
+/* MicrofacetTransmission (reflection.cpp:242-281, 405-459) with Beckmann + (Fixed)FresnelDielectric */
+static float beck_pdf_raw(float r2, v3 wo, v3 wi) { /* Beckmann::Pdf */
+    v3 wh = nrm(add(wo, wi));
+    float ct = fabsf(wh.z);
+    float p = beck_D(r2, wh) * ct / (4.f * dot(wo, wh));
+    if (dot(wo, wh) <= 0.f || p < 1e-20f) p = 0.f;
+    return p;
+}
+static float mtG(v3 wo, v3 wi, v3 wh) {
+    float nh = fabsf(wh.z), no = fabsf(wo.z), ni = fabsf(wi.z), oh = absdot(wo, wh), ih = absdot(wi, wh);
+    float a = 2.f * nh * no / oh, b = 2.f * nh * ni / ih;
+    float mm = b < a ? b : a;
+    return mm < 1.f ? mm : 1.f;
+}
+static int mt_f(const o_mat *m, v3 wo, v3 wi, float f[O_NB]) {
+    float ci = fabsf(wi.z), co = fabsf(wo.z);
+    if (ci == 0.f || co == 0.f) return 0;
+    int entering = wo.z > 0.f;
+    float et = entering ? m->eta : 1.f / m->eta;
+    v3 wh = neg(add(wo, mul(wi, et)));
+    float den = lensq(wh);
+    if (den == 0.f) return 0;
+    wh = nrm(wh);
+    float chi = dot(wi, wh), cho = dot(wo, wh);
+    if (chi == 0.f || cho == 0.f) return 0;
+    float F = fresnel(entering ? fabsf(cho) : -fabsf(cho), 1.f, m->eta, m->fixed_fresnel);
+    float s = fabsf(chi * cho) * et * et * beck_D(m->rough2, wh) * mtG(wo, wi, wh) / (ci * co * den);
+    for (int c = 0; c < O_NB; ++c) f[c] = (m->T[c] * s) * (1.f - F);
+    return 1;
+}
+static float mt_pdf(const o_mat *m, v3 wo, v3 wi) {
+    if (wo.z * wi.z > 0.f) return 0.f;
+    int entering = wo.z > 0.f;
+    float et = entering ? m->eta : 1.f / m->eta;
+    v3 wh = neg(add(wo, mul(wi, et)));
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return 0.f;
+    float den = lensq(wh);
+    wh = nrm(wh);
+    v3 wir = add(neg(wo), mul(wh, 2.f * dot(wo, wh)));
+    float pdf = beck_pdf_raw(m->rough2, wo, wir);
+    float cosi = dot(wo, wh);
+    pdf *= 4 * cosi * cosi * et * et / den;
+    return pdf;
+}
+static void mf_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *pdf);
+static void mt_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *pdf) {
+    mf_sample(m, wo, u1, u2, wi, pdf);
+    int entering = wo.z > 0.f;
+    float et = entering ? m->eta : 1.f / m->eta;
+    v3 wh = add(wo, *wi);
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return;
+    wh = nrm(wh);
+    float cosi = dot(wo, wh);
+    float sini2 = fmaxf(0.f, 1.f - cosi * cosi);
+    float eta = 1.f / et;
+    float sint2 = eta * eta * sini2;
+    if (sint2 >= 1.f) { *pdf = 0.f; return; }
+    float cost = sqrtf(fmaxf(0.f, 1.f - sint2));
+    *wi = add(mul(wo, -eta), mul(wh, eta * cosi - cost));
+    float den = lensq(add(wo, mul(*wi, et)));
+    if (den == 0.f) { *pdf = 0.f; return; }
+    *pdf *= 4 * cosi * cosi * et * et / den;
+}
+
+/* BSDF::f with the ng hemisphere test: BRDFs on the reflection side, BTDFs on the other.
  * wol / wil are the local-frame directions the BxDF sees (BSDF::Sample_f keeps the sampled
  * local wi rather than re-projecting the world one). */
 static int bsdf_f(const o_mat *m, const frame_t *fr, v3 woW, v3 wiW, v3 wol, v3 wil, float f[O_NB]) {
-    if (!m->has_refl) return 0;
-    if (!(dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)) return 0;
-    if (!mf_f(m, wol, wil, f)) return 0;
+    int ok;
+    if (dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)
+        ok = m->has_refl && mf_f(m, wol, wil, f);
+    else
+        ok = m->has_trans && mt_f(m, wol, wil, f);
+    if (!ok) return 0;
     for (int c = 0; c < O_NB; ++c)
         if (f[c] != 0.f) return 1;
     return 0;
+}
+
+/* BSDF::Pdf (reflection.cpp:736-751): mean over the matching lobes, R then T */
+static float bsdf_pdf(const o_mat *m, v3 wo, v3 wi) {
+    int n = m->has_refl + m->has_trans;
+    if (n == 0) return 0.f;
+    float pdf = 0.f;
+    if (m->has_refl) pdf += mf_pdf(m, wo, wi);
+    if (m->has_trans) pdf += mt_pdf(m, wo, wi);
+    return pdf / (float)n;
 }
 static float power_h(float fp, float gp) { float f = 1 * fp, g = 1 * gp; return (f * f) / (f * f + g * g); }
 
@@ -1000,27 +1080,38 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
         uint32_t base = (uint32_t)(si ^ xr) * (uint32_t)ns;
         uint32_t a0 = hash3(seed, pix, 16u * l + D_LIGHT_POS), a1 = hash3(seed, pix, 16u * l + D_LIGHT_POS + 8u);
         uint32_t b0 = hash3(seed, pix, 16u * l + D_BSDF_DIR), b1 = hash3(seed, pix, 16u * l + D_BSDF_DIR + 8u);
+        uint32_t bc = hash3(seed, pix, 16u * l + D_BSDF_COMP);
         for (int j = 0; j < ns; ++j) {
             uint32_t k = base + (uint32_t)j;
             float ed[O_NB], f[O_NB];
             for (int c = 0; c < O_NB; ++c) ed[c] = 0.f;
             lsamp ls = light_sample(Lt, fr.p, reps, vdc(k, a0), sobol(k, a1));
             float lightPdf = ls.pdf;
-            if (lightPdf > 0.f && ls.nonblack) {
+            if (lightPdf > 0.f && ls.nonblack && (mat->has_refl || mat->has_trans)) {
                 if (bsdf_f(mat, &fr, wo, ls.wi, to_local(&fr, wo), to_local(&fr, ls.wi), f) &&
                     !occluded(s, ls.so, ls.sd, ls.smint, ls.smaxt)) {
-                    float bsdfPdf = mf_pdf(mat, to_local(&fr, wo), to_local(&fr, ls.wi));
+                    float bsdfPdf = bsdf_pdf(mat, to_local(&fr, wo), to_local(&fr, ls.wi));
                     float w = power_h(lightPdf, bsdfPdf);
                     float k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
                     for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Lt->Le[c] * k1;
                 }
             }
-            if (mat->has_refl) {
-                v3 wil;
+            int ncomp = mat->has_refl + mat->has_trans;
+            if (ncomp > 0) {
+                /* BSDF::Sample_f: component by uComponent, R before T */
+                int which = (int)floorf(vdc(k, bc) * (float)ncomp);
+                if (which > ncomp - 1) which = ncomp - 1;
+                int pick_t = !mat->has_refl || which == 1;
+                v3 wil, wol = to_local(&fr, wo);
                 float bsdfPdf;
-                mf_sample(mat, to_local(&fr, wo), vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
+                if (pick_t) mt_sample(mat, wol, vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
+                else mf_sample(mat, wol, vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
                 if (bsdfPdf != 0.f) {
                     v3 wi = to_world(&fr, wil);
+                    if (ncomp > 1) {
+                        bsdfPdf += pick_t ? mf_pdf(mat, wol, wil) : mt_pdf(mat, wol, wil);
+                        bsdfPdf /= (float)ncomp;
+                    }
                     if (bsdf_f(mat, &fr, wo, wi, to_local(&fr, wo), wil, f) && bsdfPdf > 0.f) {
                         lightPdf = light_pdf(Lt, fr.p, wi);
                         if (lightPdf != 0.f) {

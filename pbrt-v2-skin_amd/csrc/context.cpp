@@ -56,9 +56,7 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
     memcpy(mat->albedo, m.albedo, sizeof(mat->albedo));
     memcpy(mat->Kr, m.Kr, sizeof(mat->Kr));
-    for (int c = 0; c < NB; ++c)
-        if (m.Kt[c] != 0.f)
-            throw Error(MPSS_ERR_INVALID, "layeredskin: a non-black Kt (MicrofacetTransmission) is not supported yet");
+    memcpy(mat->Kt, m.Kt, sizeof(mat->Kt));
     mat->roughness = m.roughness;
     mat->ior = m.layer_ior[0];
     mat->double_ref_sslf = m.double_ref_sslf != 0;
@@ -83,6 +81,7 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
     for (int c = 0; c < NB; ++c) {
         mat->albedo[c] = albedo ? albedo[c] : 1.f;
         mat->Kr[c] = 1.f;
+        mat->Kt[c] = 0.f;
     }
     mat->is_monte_carlo = is_mc;
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);

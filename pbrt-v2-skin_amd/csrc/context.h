@@ -19,7 +19,8 @@ struct Material {
     ProfileTables profile;
     RhoTable rho;
     float albedo[NB];
-    float Kr[NB];              // Microfacet reflectance (layeredskin "Kr"); Kt must be black
+    float Kr[NB];              // Microfacet reflectance (layeredskin "Kr")
+    float Kt[NB];              // MicrofacetTransmission transmittance (layeredskin "Kt")
     float roughness = 0.4f, ior = 1.4f;
     bool double_ref_sslf = false;
     bool is_monte_carlo = false;

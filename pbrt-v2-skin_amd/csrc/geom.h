@@ -320,8 +320,8 @@ MPSS_HD float fresnel_dielectric(float cosi, float eta_i, float eta_t, int fixed
 MPSS_HD float microfacet_G(V3 wo, V3 wi, V3 wh) {  // reflection.h:430-437
     const float a = fabsf(wh.z), wowh = absdot(wo, wh);
     const float g1 = 2.f * a * fabsf(wo.z) / wowh, g2 = 2.f * a * fabsf(wi.z) / wowh;
-    const float m = g1 < g2 ? g1 : g2;
-    return 1.f < m ? 1.f : m;
+    const float m = g2 < g1 ? g2 : g1;  // std::min(g1, g2): (b < a) ? b : a
+    return m < 1.f ? m : 1.f;            // std::min(1.f, m)
 }
 
 // Microfacet::f with R factored out: returns (D, G, F, denominator) so that per band
@@ -367,6 +367,93 @@ MPSS_HD void beckmann_sample(const Microfacet &m, V3 wo, float u1, float u2, V3 
     float p = beckmann_D(m, wh) * ct / (4.f * dot(wo, wh));
     if (dot(wo, wh) <= 0.f || p < 1e-20f) p = 0.f;
     pdf = p;
+}
+
+// ---------------------------------------------------------------- MicrofacetTransmission
+// reflection.cpp:242-281, 405-459 with the Beckmann distribution and the layer's (Fixed)
+// FresnelDielectric(1, ior). Its f is T * s * (1 - F) with a scalar s (factored like MfTerms).
+struct MtTerms {
+    float s, F;
+    bool zero;
+};
+
+MPSS_HD float beckmann_pdf(const Microfacet &m, V3 wo, V3 wi) {  // Beckmann::Pdf (no hemisphere test)
+    const V3 wh = normalize(wo + wi);
+    const float ct = fabsf(wh.z);
+    float p = beckmann_D(m, wh) * ct / (4.f * dot(wo, wh));
+    if (dot(wo, wh) <= 0.f || p < 1e-20f) p = 0.f;
+    return p;
+}
+
+MPSS_HD float mt_G(V3 wo, V3 wi, V3 wh) {  // MicrofacetTransmission::G (reflection.cpp:273-281)
+    const float nwh = fabsf(wh.z), nwo = fabsf(wo.z), nwi = fabsf(wi.z);
+    const float owh = absdot(wo, wh), iwh = absdot(wi, wh);
+    const float a = 2.f * nwh * nwo / owh, b = 2.f * nwh * nwi / iwh;
+    const float m = b < a ? b : a;  // std::min semantics, as microfacet_G
+    return m < 1.f ? m : 1.f;
+}
+
+MPSS_HD MtTerms mt_terms(const Microfacet &m, V3 wo, V3 wi) {  // MicrofacetTransmission::f (:251-270)
+    MtTerms r{0.f, 0.f, true};
+    const float ci = fabsf(wi.z), co = fabsf(wo.z);
+    if (ci == 0.f || co == 0.f) return r;
+    const bool entering = wo.z > 0.f;
+    const float et = entering ? m.eta : 1.f / m.eta;
+    V3 wh = -(wo + wi * et);
+    const float den = len2(wh);
+    if (den == 0.f) return r;
+    wh = normalize(wh);
+    const float chi = dot(wi, wh), cho = dot(wo, wh);
+    if (chi == 0.f || cho == 0.f) return r;
+    r.F = fresnel_dielectric(entering ? fabsf(cho) : -fabsf(cho), 1.f, m.eta, m.fixed_fresnel);
+    r.s = fabsf(chi * cho) * et * et * beckmann_D(m, wh) * mt_G(wo, wi, wh) / (ci * co * den);
+    r.zero = false;
+    return r;
+}
+
+MPSS_HD float mt_pdf(const Microfacet &m, V3 wo, V3 wi) {  // MicrofacetTransmission::Pdf (:444-459)
+    if (wo.z * wi.z > 0.f) return 0.f;  // SameHemisphere
+    const bool entering = wo.z > 0.f;
+    const float et = entering ? m.eta : 1.f / m.eta;
+    V3 wh = -(wo + wi * et);
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return 0.f;
+    const float den = len2(wh);
+    wh = normalize(wh);
+    const V3 wir = -wo + wh * (2.f * dot(wo, wh));
+    float pdf = beckmann_pdf(m, wo, wir);
+    const float cosi = dot(wo, wh);
+    pdf *= 4 * cosi * cosi * et * et / den;
+    return pdf;
+}
+
+// MicrofacetTransmission::Sample_f (:405-441): wi and pdf (pdf stays the distribution's when the
+// half vector degenerates or wi lands in wo's hemisphere, as in the reference)
+MPSS_HD void mt_sample(const Microfacet &m, V3 wo, float u1, float u2, V3 &wi, float &pdf) {
+    beckmann_sample(m, wo, u1, u2, wi, pdf);
+    const bool entering = wo.z > 0.f;
+    const float et = entering ? m.eta : 1.f / m.eta;
+    V3 wh = wo + wi;
+    if (wh.x == 0.f && wh.y == 0.f && wh.z == 0.f) return;
+    wh = normalize(wh);
+    const float cosi = dot(wo, wh);
+    const float x = 1.f - cosi * cosi;
+    const float sini2 = x > 0.f ? x : 0.f;
+    const float eta = 1.f / et;
+    const float sint2 = eta * eta * sini2;
+    if (sint2 >= 1.f) {
+        pdf = 0.f;
+        return;
+    }
+    const float y = 1.f - sint2;
+    const float cost = sqrtf(y > 0.f ? y : 0.f);
+    const float so = eta;
+    wi = wo * -so + wh * (so * cosi - cost);
+    const float den = len2(wo + wi * et);
+    if (den == 0.f) {
+        pdf = 0.f;
+        return;
+    }
+    pdf *= 4 * cosi * cosi * et * et / den;
 }
 
 MPSS_HD V3 to_local(const ShadingFrame &f, V3 v) { return V3{dot(v, f.sn), dot(v, f.tn), dot(v, f.nn)}; }

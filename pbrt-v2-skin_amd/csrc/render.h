@@ -25,11 +25,12 @@ struct RenderLight {
 
 struct RenderMaterial {
     float R[NB];          // Kr (Microfacet reflectance), layeredskin.cpp:154-158
+    float T[NB];          // Kt (MicrofacetTransmission), layeredskin.cpp:159-161
     float alb_mix[NB];    // Pow(albedo, mix)      (IrradianceTask, file line 224)
     float alb_1mmix[NB];  // Pow(albedo, 1 - mix)  (Li, file line 371)
     Microfacet mf;
     const float *rho;     // device rho_hd table
-    int n_rho, has_bssrdf, has_refl, is_mc;
+    int n_rho, has_bssrdf, has_refl, has_trans, is_mc;
 };
 
 struct RenderScene {

@@ -294,11 +294,59 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
 // stores its scalars; direct_combine_kernel then forms the per-band sums in the reference's
 // order (j ascending inside a light, lights ascending). A BSDF value is R[c] * D * G * F / den
 // (Microfacet::f) with scalar D, G, F, den, so no lane carries a 30-band spectrum.
-struct DirectTerms {       // 16 floats: one EstimateDirect
-    float D1, G1, F1, den1, k1;            // light sampling: f * Li * k1
-    float D2, G2, F2, den2, adn, w2, pdf2; // BSDF sampling: f * Li * adn * w2 / pdf2
-    uint32_t use;                          // bit 0: light term, bit 1: BSDF term
-    float pad[3];
+// One lobe value of the layer-0 BSDF for a direction pair (BSDF::f, reflection.cpp:765-779):
+// kind 1 = Microfacet (R * D * G * F / den), kind 2 = MicrofacetTransmission (T * s * (1 - F)).
+struct Lobe {
+    uint32_t kind;
+    float a, b, c, d;
+};
+
+__device__ __forceinline__ Lobe bsdf_lobe(const RenderMaterial &mat, bool refl, V3 wo_l, V3 wi_l) {
+    Lobe L{0u, 0.f, 0.f, 0.f, 1.f};
+    if (refl) {  // the ng test keeps BRDFs only
+        if (mat.has_refl) {
+            const MfTerms t = microfacet_terms(mat.mf, wo_l, wi_l);
+            if (!t.zero) L = Lobe{1u, t.D, t.G, t.F, t.den};
+        }
+    } else if (mat.has_trans) {  // ... or BTDFs only
+        const MtTerms t = mt_terms(mat.mf, wo_l, wi_l);
+        if (!t.zero) L = Lobe{2u, t.s, t.F, 0.f, 1.f};
+    }
+    return L;
+}
+
+__device__ __forceinline__ float lobe_value(const RenderMaterial &mat, const Lobe &L, int c) {
+    return L.kind == 1u ? mat.R[c] * L.a * L.b * L.c / L.d : (mat.T[c] * L.a) * (1.f - L.b);
+}
+
+__device__ __forceinline__ bool lobe_black(const RenderMaterial &mat, const Lobe &L) {
+    if (L.kind == 0u) return true;
+    for (int c = 0; c < NB; ++c)
+        if (lobe_value(mat, L, c) != 0.f) return false;
+    return true;
+}
+
+// BSDF::Pdf (reflection.cpp:736-751): mean of the matching lobes' pdfs, R then T
+__device__ __forceinline__ float bsdf_pdf(const RenderMaterial &mat, V3 wo_l, V3 wi_l) {
+    const int n = mat.has_refl + mat.has_trans;
+    if (n == 0) return 0.f;
+    float pdf = 0.f;
+    if (mat.has_refl) pdf += microfacet_pdf(mat.mf, wo_l, wi_l);
+    if (mat.has_trans) pdf += mt_pdf(mat.mf, wo_l, wi_l);
+    return pdf / (float)n;
+}
+
+// ------------------------------------------------------------------ shading + direct light
+// The rest of MultipoleSubsurfaceIntegrator::Li for the compacted surface hits, with one lane
+// per (hit, light, light-sample j) of UniformSampleAllLights (integrator.cpp:47-77): each lane
+// runs one EstimateDirect (:117-174) -- light sample + shadow ray, BSDF sample + ray -- and
+// stores its scalars; direct_combine_kernel then forms the per-band sums in the reference's
+// order (j ascending inside a light, lights ascending). BSDF values are a 30-band factor times
+// scalars (Lobe), so no lane carries a spectrum.
+struct DirectTerms {       // 16 words: one EstimateDirect
+    float k1, adn, w2, pdf2;   // light term f * Li * k1; BSDF term f * Li * adn * w2 / pdf2
+    Lobe l1, l2;               // the BSDF lobe value of each term (kind 0: term absent)
+    float pad[2];
 };
 static_assert(sizeof(DirectTerms) == 64, "one 64-B record per light sample");
 
@@ -343,64 +391,56 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
         rec.hit_q[slot] = make_float4(fr.p.x, fr.p.y, fr.p.z, sss ? ct : -1.f);
         if (j >= ns) return;
     }
+    const int ncomp = mat.has_refl + mat.has_trans;
     const V3 wo_l = to_local(fr, wo);
     const float ng_wo = dot(wo, fr.ng);
     const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
     const uint32_t nidx = (uint32_t)(s ^ (int)xr) * (uint32_t)ns + (uint32_t)j;
     const uint32_t sl0 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS), sl1 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
-                   sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR), sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u);
+                   sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR), sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u),
+                   sbc = hash3(seed, pix, 16u * l + DIM_BSDF_COMP);
     // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
     const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
     float lightPdf = ls.pdf;
-    if (lightPdf > 0.f && ls.nonblack && mat.has_refl) {
+    if (lightPdf > 0.f && ls.nonblack && ncomp > 0) {
         const V3 wi_l = to_local(fr, ls.wi);
-        const bool refl = dot(ls.wi, fr.ng) * ng_wo > 0.f;  // BSDF::f ng test
-        const MfTerms t1 = microfacet_terms(mat.mf, wo_l, wi_l);
-        bool fblack = !refl || t1.zero;
-        if (!fblack) {
-            fblack = true;
-            for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t1.D * t1.G * t1.F / t1.den) == 0.f;
-        }
-        if (!fblack && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
-            const float bsdfPdf = microfacet_pdf(mat.mf, wo_l, wi_l);
+        const Lobe f1 = bsdf_lobe(mat, dot(ls.wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
+        if (!lobe_black(mat, f1) && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
+            const float bsdfPdf = bsdf_pdf(mat, wo_l, wi_l);
             const float w = power_heuristic(lightPdf, bsdfPdf);
-            out.D1 = t1.D;
-            out.G1 = t1.G;
-            out.F1 = t1.F;
-            out.den1 = t1.den;
             out.k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
-            out.use |= 1u;
+            out.l1 = f1;
         }
     }
     // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
-    if (mat.has_refl) {
+    if (ncomp > 0) {
+        int which = (int)floorf(van_der_corput(nidx, sbc) * (float)ncomp);
+        which = which < ncomp - 1 ? which : ncomp - 1;
+        const bool pick_t = !mat.has_refl || which == 1;
         V3 wi_l;
         float bsdfPdf;
-        beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+        if (pick_t)
+            mt_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+        else
+            beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
         if (bsdfPdf != 0.f) {
             const V3 wi = to_world(fr, wi_l);
-            const bool refl = dot(wi, fr.ng) * ng_wo > 0.f;
-            const MfTerms t2 = microfacet_terms(mat.mf, wo_l, wi_l);
-            bool fblack = !refl || t2.zero;
-            if (!fblack) {
-                fblack = true;
-                for (int c = 0; c < NB; ++c) fblack = fblack && (mat.R[c] * t2.D * t2.G * t2.F / t2.den) == 0.f;
+            if (ncomp > 1) {
+                bsdfPdf += pick_t ? microfacet_pdf(mat.mf, wo_l, wi_l) : mt_pdf(mat.mf, wo_l, wi_l);
+                bsdfPdf /= (float)ncomp;
             }
-            if (!fblack && bsdfPdf > 0.f) {
+            const Lobe f2 = bsdf_lobe(mat, dot(wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
+            if (!lobe_black(mat, f2) && bsdfPdf > 0.f) {
                 lightPdf = sphere_pdf(L.s, fr.p, wi);
                 if (lightPdf != 0.f) {
                     const float w = power_heuristic(bsdfPdf, lightPdf);
                     const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
                     // Li = lightIsect.Le(-wi) when the hit primitive is this light
                     if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
-                        out.D2 = t2.D;
-                        out.G2 = t2.G;
-                        out.F2 = t2.F;
-                        out.den2 = t2.den;
                         out.adn = absdot(wi, fr.nn);
                         out.w2 = w;
                         out.pdf2 = bsdfPdf;
-                        out.use |= 2u;
+                        out.l2 = f2;
                     }
                 }
             }
@@ -438,10 +478,10 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
             float Ld = 0.f;
             for (int j = 0; j < ns; ++j) {
                 const DirectTerms &e = t[l * ns_max + j];
-                if (!e.use) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
+                if (!e.l1.kind && !e.l2.kind) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
                 float ed = 0.f;
-                if (e.use & 1u) ed += (mat.R[c] * e.D1 * e.G1 * e.F1 / e.den1) * L.Lemit[c] * e.k1;
-                if (e.use & 2u) ed += (mat.R[c] * e.D2 * e.G2 * e.F2 / e.den2) * L.Lemit[c] * e.adn * e.w2 / e.pdf2;
+                if (e.l1.kind) ed += lobe_value(mat, e.l1, c) * L.Lemit[c] * e.k1;
+                if (e.l2.kind) ed += lobe_value(mat, e.l2, c) * L.Lemit[c] * e.adn * e.w2 / e.pdf2;
                 Ld += ed;
             }
             ld += Ld / (float)ns;

@@ -132,6 +132,10 @@ void Context::upload_scene() {
         bool black = true;
         for (int c = 0; c < NB; ++c) black = black && m.Kr[c] == 0.f;
         r.has_refl = !black;
+        memcpy(r.T, m.Kt, sizeof(r.T));
+        bool tblack = true;
+        for (int c = 0; c < NB; ++c) tblack = tblack && m.Kt[c] == 0.f;
+        r.has_trans = !tblack;
         for (int c = 0; c < NB; ++c) {
             r.alb_mix[c] = m_pow(m.albedo[c], cfg_.mix);
             r.alb_1mmix[c] = m_pow(m.albedo[c], 1.f - cfg_.mix);

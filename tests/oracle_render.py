@@ -26,8 +26,8 @@ def _lib():
     L.o_scene_create.restype = vp
     L.o_scene_create.argtypes = [C.c_int, C.c_int, f32p, f32p]
     L.o_scene_add_material.restype = C.c_int
-    L.o_scene_add_material.argtypes = [vp, f32p, f32p, C.c_float, C.c_float, C.c_float, C.c_int, f32p, C.c_int,
-                                       C.c_int, f32p, C.c_int, f32p]
+    L.o_scene_add_material.argtypes = [vp, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float, C.c_int, f32p,
+                                       C.c_int, C.c_int, f32p, C.c_int, f32p]
     L.o_scene_add_mesh.restype = C.c_int
     L.o_scene_add_mesh.argtypes = [vp, C.c_int, f32p, vp, vp, vp, C.c_int, oracle_lib.i32p, f32p, f32p, C.c_int,
                                    C.c_int]
@@ -81,9 +81,10 @@ class OracleScene:
             kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
             skin = mpss.default_skin(**kw)
             Kr = mpss.host_from_rgb(m["Kr"]) if "Kr" in m else np.ones(NB, np.float32)
+            Kt = mpss.host_from_rgb(m["Kt"]) if "Kt" in m else np.ones(NB, np.float32)
             alb = mpss.host_from_rgb(m["albedo"]) if "albedo" in m else np.ones(NB, np.float32)
             tab, rcp, rho = tables[mid]
-            L.o_scene_add_material(self.h, Kr, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
+            L.o_scene_add_material(self.h, Kr, Kt, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
                                    int(skin.double_ref_sslf), rho, len(rho), 0,
                                    np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
         for me in sc.meshes:

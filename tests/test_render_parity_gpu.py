@@ -112,3 +112,28 @@ def test_c1_tissue_full_frame(mpss, oracle):
     got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 13)
     ref = o.render_tile(sc.spp, 13, 0, sc.xres, 0, sc.yres)
     _check(got, ref)
+
+
+@pytest.mark.parametrize("scene,kt", [("skin.pbrt", None), ("tissue.pbrt", [0.6, 0.8, 1.0])])
+def test_image_parity_transmission_lobe(mpss, oracle, scene, kt):
+    """LayeredSkin with a non-black Kt (CreateLayeredSkinMaterial's default Spectrum(1), or a
+    coloured one): the BSDF gains MicrofacetTransmission, so BSDF sampling picks a lobe with
+    uComponent and the MIS pdfs average both lobes (reflection.cpp:675-751)."""
+    import torch
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", scene), xres=48, yres=48, spp=4)
+    sc.integrator["minsampledistance"] = 0.008
+    for m in sc.materials:
+        m["desired_length"] = 128
+        if kt is None:
+            m.pop("Kt", None)   # the default Spectrum(1)
+        else:
+            m["Kt"] = kt
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=4)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    o.set_octree(pts, o.irradiance(pts, 4))
+    got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 21)
+    ref = o.render_tile(sc.spp, 21, 0, sc.xres, 0, sc.yres)
+    _check(got, ref)
