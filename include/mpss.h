@@ -124,6 +124,13 @@ int mpss_add_mesh(mpss_ctx *ctx, uint32_t nverts, const float *P, const float *N
                   int reverse_orientation, uint32_t material_id);
 /* AreaLightSource "area" + Shape "sphere" placed by a translation (lights/diffuse.cpp:45-67). */
 int mpss_add_sphere_light(mpss_ctx *ctx, const float *center, float radius, const float *Lemit, int nsamples);
+/* LightSource "infinite" without "mapname" (CreateInfiniteLight, lights/infinite.cpp:180-188): L is
+ * the 30-band L * scale; the light keeps L.ToRGBSpectrum() as its 1x1 radiance map and returns
+ * Spectrum(map lookup, SPECTRUM_ILLUMINANT) for Le / Sample_L (infinite.cpp:66-234).
+ * light_to_world / world_to_light: row-major 4x4 (only the rotation part is used). Lights join
+ * scene->lights in call order, mixed with sphere lights; at most 254 lights. */
+int mpss_add_infinite_light(mpss_ctx *ctx, const float *L, int nsamples, const float *light_to_world,
+                            const float *world_to_light);
 /* PerspectiveCamera (cameras/perspective.cpp): RasterToCamera and CameraToWorld, row-major 4x4. */
 int mpss_set_camera(mpss_ctx *ctx, const float *raster_to_camera, const float *camera_to_world, int xres, int yres);
 /* SurfacePoint records (44 B: p[3] n[3] u v materialId area rayEpsilon, renderers/surfacepoints.h:45-55),

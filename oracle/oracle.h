@@ -33,6 +33,8 @@ extern "C" {
 float o_average_spectrum_samples(const float *lambda, const float *vals, int n, float l0, float l1);
 void o_from_sampled(const float *lambda, const float *vals, int n, float out[O_NB]);
 void o_from_rgb(const float rgb[3], int illuminant, float out[O_NB]);
+/* SampledSpectrum::ToRGB = ToXYZ + XYZToRGB (spectrum.h:51-55, 374-398) */
+void o_to_rgb(const float s[O_NB], float rgb[3]);
 float o_y(const float s[O_NB]);
 void o_to_xyz(const float s[O_NB], float xyz[3]);
 
@@ -104,6 +106,7 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T /* nullable:
 int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
                      const int32_t *idx, const float *o2w, const float *w2o, int flip, int material);
 int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples);
+int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l);
 long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_point *out, long cap);
 void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E);
 void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, const float *E, const float *area,

@@ -129,10 +129,13 @@ typedef struct {
 } o_mesh;
 
 typedef struct {
+    int kind; /* 0 sphere area light, 1 infinite light with a constant (1x1) map */
     v3 c;
     float r, phimax, thetamin, thetamax, area;
     float Le[O_NB];
     int ns_pow2;
+    float rgb[3], l2w[9], w2l[9]; /* kind 1: the texel, LightToWorld, WorldToLight */
+    float f;                      /* kind 1: Distribution2D's img[0] = texel.y() * sin(pi/2) */
 } o_light;
 
 typedef struct {
@@ -233,6 +236,7 @@ static int round_up_pow2(int v) { int r = 1; while (r < v) r <<= 1; return r; }
 int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples) {
     s->lights = (o_light *)realloc(s->lights, (s->nlights + 1) * sizeof(o_light));
     o_light *l = &s->lights[s->nlights];
+    memset(l, 0, sizeof(*l));
     l->c = mk(c[0], c[1], c[2]);
     l->r = r;
     /* Sphere ctor (sphere.cpp): zmin = -r, zmax = r, phiMax = 360 degrees */
@@ -241,6 +245,27 @@ int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *L
     l->thetamax = facos(1.f);
     l->area = l->phimax * r * (r - -r);
     memcpy(l->Le, Le, sizeof(l->Le));
+    l->ns_pow2 = round_up_pow2(nsamples);
+    return s->nlights++;
+}
+
+/* CreateInfiniteLight + InfiniteAreaLight ctor without a map (lights/infinite.cpp:66-106, 180-188):
+ * L is the 30-band L * scale; the map's one texel is L.ToRGBSpectrum() */
+int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l) {
+    s->lights = (o_light *)realloc(s->lights, (s->nlights + 1) * sizeof(o_light));
+    o_light *l = &s->lights[s->nlights];
+    memset(l, 0, sizeof(*l));
+    l->kind = 1;
+    o_to_rgb(L, l->rgb);
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            l->l2w[3 * r + k] = l2w[4 * r + k];
+            l->w2l[3 * r + k] = w2l[4 * r + k];
+        }
+    /* img[u + v*width] = radianceMap->Lookup(up, vp, filter).y() * sinTheta; filter 1 on a 1x1
+     * map is level 0's texel (mipmap.h:239-255); RGBSpectrum::y() */
+    float y = 0.212671f * l->rgb[0] + 0.715160f * l->rgb[1] + 0.072169f * l->rgb[2];
+    l->f = y * fsin(PI_F * (float)(0 + .5f) / (float)1);
     l->ns_pow2 = round_up_pow2(nsamples);
     return s->nlights++;
 }
@@ -461,9 +486,86 @@ static float light_pdf(const o_light *s, v3 p, v3 wi) { /* ShapeSet::Pdf of one 
     return (0.f + s->area * pdf) / s->area;
 }
 
+/* ------------------------------------------------------------------ infinite light */
+static v3 xvec3(const float *m, v3 v) { /* Transform::operator()(Vector), transform.h:215-220 */
+    return mk(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+              m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+
+/* Spectrum(radianceMap->Lookup(s, t), SPECTRUM_ILLUMINANT): MIPMap::Lookup with width 0 is
+ * triangle(0, s, t) (mipmap.h:239-269) over TEXTURE_REPEAT copies of the one texel */
+static void inf_le(const o_light *L, float s, float t, float out[O_NB]) {
+    s = s * (float)1u - 0.5f;
+    t = t * (float)1u - 0.5f;
+    int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    float ds = s - s0, dt = t - t0;
+    float rgb[3];
+    for (int k = 0; k < 3; ++k) {
+        float c = L->rgb[k];
+        rgb[k] = (1.f - ds) * (1.f - dt) * c + (1.f - ds) * dt * c + ds * (1.f - dt) * c + ds * dt * c;
+    }
+    o_from_rgb(rgb, 1, out);
+}
+
+/* InfiniteAreaLight::Le (infinite.cpp:115-120) */
+static void inf_le_dir(const o_light *L, v3 d, float out[O_NB]) {
+    v3 wh = nrm(xvec3(L->w2l, d));
+    float z = wh.z < -1.f ? -1.f : (wh.z > 1.f ? 1.f : wh.z);
+    float theta = facos(z);
+    float phi = fatan2(wh.y, wh.x);
+    if (phi < 0.f) phi = phi + 2 * PI_F;
+    inf_le(L, phi * 0.15915494309189533577f, theta * INV_PI_F, out);
+}
+
+static int black(const float *x) {
+    for (int c = 0; c < O_NB; ++c)
+        if (x[c] != 0.f) return 0;
+    return 1;
+}
+
+/* Distribution1D of one value f (montecarlo.h): SampleContinuous's pdf = func / funcInt */
+static float d1_pdf(float f) { return f / f; } /* 0 / 0 = NaN when funcInt == 0 */
+
+/* InfiniteAreaLight::Pdf (infinite.cpp:222-232) with Distribution2D::Pdf of the 1x1 map */
+static float inf_pdf(const o_light *L, v3 w) {
+    v3 wi = xvec3(L->w2l, w);
+    float z = wi.z < -1.f ? -1.f : (wi.z > 1.f ? 1.f : wi.z);
+    float theta = facos(z);
+    float sintheta = fsin(theta);
+    if (sintheta == 0.f) return 0.f;
+    float fi = L->f * L->f;
+    float dp = fi == 0.f ? 0.f : (L->f * L->f) / fi;
+    return dp / (2.f * PI_F * PI_F * sintheta);
+}
+
+/* Sample_L of either light kind: wi, pdf, shadow ray, radiance non-black flag, and for the
+ * infinite light the radiance itself */
+typedef struct { v3 wi, so, sd; float pdf, smint, smaxt; int nonblack; float Li[O_NB]; } lsamp;
+
+/* InfiniteAreaLight::Sample_L (infinite.cpp:195-218) + VisibilityTester::SetRay */
+static lsamp inf_sample(const o_light *L, v3 p, float peps, float u0, float u1) {
+    lsamp r;
+    /* Distribution2D::SampleContinuous on 1x1: uv = (u0, u1) (du = (u - 0) / (1 - 0)) */
+    float uv0 = (0 + (u0 - 0.f) / (1.f - 0.f)) / 1, uv1 = (0 + (u1 - 0.f) / (1.f - 0.f)) / 1;
+    float mapPdf = d1_pdf(L->f) * d1_pdf(L->f);
+    float theta = uv1 * PI_F, phi = uv0 * 2.f * PI_F;
+    float costheta = fcos(theta), sintheta = fsin(theta);
+    float sinphi = fsin(phi), cosphi = fcos(phi);
+    r.wi = xvec3(L->l2w, mk(sintheta * cosphi, sintheta * sinphi, costheta));
+    r.pdf = mapPdf / (2.f * PI_F * PI_F * sintheta);
+    if (sintheta == 0.f) r.pdf = 0.f;
+    r.so = p;
+    r.sd = r.wi;
+    r.smint = peps;
+    r.smaxt = INFINITY;
+    inf_le(L, uv0, uv1, r.Li);
+    r.nonblack = !black(r.Li);
+    return r;
+}
+
 /* DiffuseAreaLight::Sample_L: wi, pdf, shadow segment, radiance non-black flag */
-typedef struct { v3 wi, so, sd; float pdf, smint, smaxt; int nonblack; } lsamp;
 static lsamp light_sample(const o_light *L, v3 p, float peps, float u0, float u1) {
+    if (L->kind) return inf_sample(L, p, peps, u0, u1);
     lsamp r;
     v3 ns;
     v3 ps = light_sample_point(L, p, u0, u1, &ns);
@@ -475,6 +577,7 @@ static lsamp light_sample(const o_light *L, v3 p, float peps, float u0, float u1
     r.smint = peps;
     r.smaxt = dist * (1.f - 1e-3f);
     r.nonblack = dot(ns, neg(r.wi)) > 0.f;
+    memcpy(r.Li, L->Le, sizeof(r.Li));
     return r;
 }
 
@@ -779,6 +882,7 @@ static hit_t intersect(const o_scene *s, v3 o, v3 d, float mint, float maxt) {
     for (int l = 0; l < s->nlights; ++l) {
         float t;
         v3 nn;
+        if (s->lights[l].kind) continue;
         if (sphere_hit(&s->lights[l], o, d, mint, h.t, &t, &nn)) {
             h.t = t;
             h.tri = -1 - l;
@@ -791,7 +895,7 @@ static hit_t intersect(const o_scene *s, v3 o, v3 d, float mint, float maxt) {
 static int occluded(const o_scene *s, v3 o, v3 d, float mint, float maxt) {
     for (int l = 0; l < s->nlights; ++l) {
         float t;
-        if (sphere_hit(&s->lights[l], o, d, mint, maxt, &t, NULL)) return 1;
+        if (!s->lights[l].kind && sphere_hit(&s->lights[l], o, d, mint, maxt, &t, NULL)) return 1;
     }
     v3 inv = mk(1.f / d.x, 1.f / d.y, 1.f / d.z);
     int stack[128], sp = 0;
@@ -974,7 +1078,7 @@ static void *irr_worker(void *arg) {
                     float ct = absdot(ls.wi, n);
                     ct = ct < 1.f ? ct : 1.f;
                     float Ft = mat ? 1.f - rho_at(mat, ct) : 1.f;
-                    for (int c = 0; c < O_NB; ++c) El[c] += Ft * L->Le[c] * ct / ls.pdf;
+                    for (int c = 0; c < O_NB; ++c) El[c] += Ft * ls.Li[c] * ct / ls.pdf;
                 }
             }
             for (int c = 0; c < O_NB; ++c) E[c] += El[c] / (float)ns;
@@ -1041,7 +1145,16 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
     v3 o = xpoint(s->c2w, mk(0.f, 0.f, 0.f));
     v3 d = xvector(s->c2w, dcam);
     hit_t h = intersect(s, o, d, 0.f, INFINITY);
-    if (h.tri == NO_HIT) { to_xyz(L, xyz); return; }
+    if (h.tri == NO_HIT) { /* SamplerRenderer::Li: Li += lights[i]->Le(ray) (area lights: 0) */
+        for (int l = 0; l < s->nlights; ++l) {
+            float le[O_NB];
+            if (s->lights[l].kind) inf_le_dir(&s->lights[l], d, le);
+            else memset(le, 0, sizeof(le));
+            for (int c = 0; c < O_NB; ++c) L[c] += le[c];
+        }
+        to_xyz(L, xyz);
+        return;
+    }
     if (h.tri < 0) { /* an area light's own surface: emitted radiance only */
         const o_light *Lt = &s->lights[-1 - h.tri];
         if (dot(h.lnn, neg(d)) > 0.f)
@@ -1093,7 +1206,7 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
                     float bsdfPdf = bsdf_pdf(mat, to_local(&fr, wo), to_local(&fr, ls.wi));
                     float w = power_h(lightPdf, bsdfPdf);
                     float k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
-                    for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Lt->Le[c] * k1;
+                    for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * ls.Li[c] * k1;
                 }
             }
             int ncomp = mat->has_refl + mat->has_trans;
@@ -1113,13 +1226,20 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
                         bsdfPdf /= (float)ncomp;
                     }
                     if (bsdf_f(mat, &fr, wo, wi, to_local(&fr, wo), wil, f) && bsdfPdf > 0.f) {
-                        lightPdf = light_pdf(Lt, fr.p, wi);
+                        lightPdf = Lt->kind ? inf_pdf(Lt, wi) : light_pdf(Lt, fr.p, wi);
                         if (lightPdf != 0.f) {
                             float w = power_h(bsdfPdf, lightPdf);
                             hit_t hl = intersect(s, fr.p, wi, reps, INFINITY);
-                            if (hl.tri == -1 - l && dot(hl.lnn, neg(wi)) > 0.f) {
+                            float Li[O_NB];
+                            memset(Li, 0, sizeof(Li));
+                            if (hl.tri != NO_HIT) { /* Li = lightIsect.Le(-wi) if it is this light */
+                                if (hl.tri == -1 - l && dot(hl.lnn, neg(wi)) > 0.f) memcpy(Li, Lt->Le, sizeof(Li));
+                            } else if (Lt->kind) { /* Li = light->Le(ray) */
+                                inf_le_dir(Lt, wi, Li);
+                            }
+                            if (!black(Li)) {
                                 float adn = absdot(wi, fr.nn);
-                                for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Lt->Le[c] * adn * w / bsdfPdf;
+                                for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Li[c] * adn * w / bsdfPdf;
                             }
                         }
                     }

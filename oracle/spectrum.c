@@ -89,3 +89,22 @@ void o_to_xyz(const float s[O_NB], float xyz[3]) {
     xyz[1] *= scale;
     xyz[2] *= scale;
 }
+
+/* spectrum.h:374-398 (ToXYZ) and :51-55 (XYZToRGB) */
+void o_to_rgb(const float s[O_NB], float rgb[3]) {
+    static const float X[O_NB] = MPSS_BAND_CIE_X_INIT, Y[O_NB] = MPSS_BAND_CIE_Y_INIT, Z[O_NB] = MPSS_BAND_CIE_Z_INIT;
+    float xyz[3];
+    xyz[0] = xyz[1] = xyz[2] = 0.f;
+    for (int i = 0; i < O_NB; ++i) {
+        xyz[0] += X[i] * s[i];
+        xyz[1] += Y[i] * s[i];
+        xyz[2] += Z[i] * s[i];
+    }
+    float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * O_NB);
+    xyz[0] *= scale;
+    xyz[1] *= scale;
+    xyz[2] *= scale;
+    rgb[0] = 3.240479f * xyz[0] - 1.537150f * xyz[1] - 0.498535f * xyz[2];
+    rgb[1] = -0.969256f * xyz[0] + 1.875991f * xyz[1] + 0.041556f * xyz[2];
+    rgb[2] = 0.055648f * xyz[0] - 0.204043f * xyz[1] + 1.057311f * xyz[2];
+}

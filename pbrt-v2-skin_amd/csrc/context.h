@@ -45,6 +45,7 @@ public:
     void add_mesh(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
                   const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material);
     void add_sphere_light(const float *c, float r, const float *Lemit, int nsamples);
+    void add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l);
     void set_camera(const float *r2c, const float *c2w, int xres, int yres);
     void set_surface_points(uint32_t n, const SurfacePoint *pts);
     void preprocess(uint32_t seed);
@@ -83,6 +84,8 @@ private:
     DevBuf<uint32_t> ws_hs_, ws_spill_;
     DevBuf<unsigned char> ws_terms_;
     int64_t ws_terms_n_ = 0;
+    DevBuf<float4> ws_st_;  // infinite lights: radiance-map coordinates per direct-light lane
+    int64_t ws_st_n_ = 0;
     int64_t ws_px_ = 0;
     DevBuf<float> ws_ld_;
     int64_t ws_n_ = 0, ws_hits_ = 0;

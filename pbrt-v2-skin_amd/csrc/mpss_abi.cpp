@@ -169,6 +169,13 @@ int mpss_add_sphere_light(mpss_ctx *c, const float *center, float r, const float
     });
 }
 
+int mpss_add_infinite_light(mpss_ctx *c, const float *L, int ns, const float *l2w, const float *w2l) {
+    return guarded([&] {
+        require(c && L && l2w && w2l, "mpss_add_infinite_light: null argument");
+        reinterpret_cast<Context *>(c)->add_infinite_light(L, ns, l2w, w2l);
+    });
+}
+
 int mpss_set_camera(mpss_ctx *c, const float *r2c, const float *c2w, int xres, int yres) {
     return guarded([&] {
         require(c && r2c && c2w, "mpss_set_camera: null argument");

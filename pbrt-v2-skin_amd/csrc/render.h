@@ -21,6 +21,13 @@ struct RenderLight {
     float Lemit[NB];
     int nsamples_pow2;   // RoundUpPow2(nSamples): IrradianceTask (file line 196)
     int nsamples_round;  // LDSampler::RoundSize(nSamples): RequestSamples (file line 248)
+    // kind 1 (LightSource "infinite", constant map): the texel, LightToWorld / WorldToLight, and
+    // the 1x1 map's Distribution2D pdfs: SampleContinuous's mapPdf = (f/f)*(f/f) and Pdf()'s
+    // (f*f)/(f*f) (0 when f*f == 0), f = texel.y() * sin(pi/2) (infinite.cpp:92-101, montecarlo.h)
+    int kind;
+    float map_pdf_sample, map_pdf_eval;
+    float rgb[3];
+    float l2w[9], w2l[9];
 };
 
 struct RenderMaterial {
@@ -42,6 +49,7 @@ struct RenderScene {
     const RenderMaterial *materials;
     int nlights, nmaterials, xres, yres;
     int have_octree;  // Preprocess built an octree: BSSRDF hits evaluate Mo()
+    int n_infinite;   // lights of kind 1: camera rays that miss everything see their Le
     float raster_to_camera[16], camera_to_world[16];
 };
 
@@ -58,7 +66,7 @@ enum : uint32_t {
     REC_LIVE = 1u,
     REC_SURF = 2u,  // hit a mesh: Ld valid
     REC_SSS = 4u,   // material has a MultipoleBSSRDF: pq valid
-    REC_LE = 8u,    // hit an area light's front face
+    REC_LE = 8u,    // hit an area light's front face, or (light field 0xff) missed with infinite lights
     // the sample's float image position rounds onto a pixel edge, so the box filter also
     // carries it into the neighbour: left (x-1), right (x+1), up (y-1), down (y+1)
     REC_XLO = 16u, REC_XHI = 32u, REC_YLO = 64u, REC_YHI = 128u,
@@ -90,13 +98,16 @@ struct BandPos {
 
 __global__ void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
 struct DirectTerms;
+// inf_st (null without infinite lights): per lane, the radiance-map lookup coordinates (s, t)
+// of the light-sampled and the BSDF-sampled direction of an infinite light's EstimateDirect
 __global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits, int ns_max,
-                                    DirectTerms *terms);
+                                    DirectTerms *terms, float4 *inf_st);
 __global__ void shade_nolight_kernel(RenderScene sc, SampleRecs rec, int max_hits);
 __global__ void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
-                                      const DirectTerms *terms);
+                                      const DirectTerms *terms, const float4 *inf_st);
 // Li assembly per slot (L = Le + SSS + Ld, sample filter, ToXYZ), then the box-filtered film.
 __global__ void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits);
+__global__ void sky_kernel(RenderScene sc, SampleRecs rec, int max_hits);
 __global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, float *out, int out_stride_px);
 
 }  // namespace mpss

@@ -23,6 +23,11 @@ namespace mpss {
 __constant__ float kCieX[NB] = MPSS_BAND_CIE_X_INIT;
 __constant__ float kCieY[NB] = MPSS_BAND_CIE_Y_INIT;
 __constant__ float kCieZ[NB] = MPSS_BAND_CIE_Z_INIT;
+// rgbIllum2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue} (spectrum.cpp:316-370)
+__constant__ float kIllum[7][NB] = {MPSS_BAND_RGBILLUM2SPECTWHITE_INIT,  MPSS_BAND_RGBILLUM2SPECTCYAN_INIT,
+                                    MPSS_BAND_RGBILLUM2SPECTMAGENTA_INIT, MPSS_BAND_RGBILLUM2SPECTYELLOW_INIT,
+                                    MPSS_BAND_RGBILLUM2SPECTRED_INIT,     MPSS_BAND_RGBILLUM2SPECTGREEN_INIT,
+                                    MPSS_BAND_RGBILLUM2SPECTBLUE_INIT};
 
 namespace {
 
@@ -91,6 +96,7 @@ __device__ Hit trace_closest(const RenderScene &sc, V3 o, V3 d, float mint, floa
         }
     }
     for (int l = 0; l < sc.nlights; ++l) {
+        if (sc.lights[l].kind) continue;  // an infinite light has no shape
         float t;
         V3 nn;
         if (sphere_intersect(sc.lights[l].s, o, d, mint, h.t, t, &nn)) {
@@ -106,7 +112,7 @@ __device__ Hit trace_closest(const RenderScene &sc, V3 o, V3 d, float mint, floa
 __device__ bool trace_any(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, int *stk, int sstride) {
     for (int l = 0; l < sc.nlights; ++l) {
         float t;
-        if (sphere_intersect(sc.lights[l].s, o, d, mint, maxt, t, nullptr)) return true;
+        if (!sc.lights[l].kind && sphere_intersect(sc.lights[l].s, o, d, mint, maxt, t, nullptr)) return true;
     }
     const V3 inv = V3{1.f / d.x, 1.f / d.y, 1.f / d.z};
     const int neg[3] = {inv.x < 0.f, inv.y < 0.f, inv.z < 0.f};
@@ -162,6 +168,106 @@ __device__ __forceinline__ LightSampleOut sample_light(const RenderLight &L, V3 
     return r;
 }
 
+// ---- InfiniteAreaLight with the 1x1 radiance map of a light without "mapname"
+__device__ __forceinline__ V3 xform3(const float *m, V3 v) {  // Transform::operator()(Vector)
+    return V3{(m[0] * v.x + m[1] * v.y) + m[2] * v.z, (m[3] * v.x + m[4] * v.y) + m[5] * v.z,
+              (m[6] * v.x + m[7] * v.y) + m[8] * v.z};
+}
+
+// MIPMap<RGBSpectrum>::Lookup(s, t) = triangle(0, s, t) (mipmap.h:239-269): four TEXTURE_REPEAT
+// copies of the one texel, weighted (1-ds)(1-dt), (1-ds)dt, ds(1-dt), ds dt and summed in order
+__device__ __forceinline__ void inf_lookup(const RenderLight &L, float s, float t, float rgb[3]) {
+    s = s - 0.5f;
+    t = t - 0.5f;
+    const float ds = s - (float)(int)floorf(s), dt = t - (float)(int)floorf(t);
+    const float w0 = (1.f - ds) * (1.f - dt), w1 = (1.f - ds) * dt, w2 = ds * (1.f - dt), w3 = ds * dt;
+    for (int k = 0; k < 3; ++k) {
+        const float c = L.rgb[k];
+        rgb[k] = ((c * w0 + c * w1) + c * w2) + c * w3;
+    }
+}
+
+// band c of Spectrum(rgb, SPECTRUM_ILLUMINANT) = SampledSpectrum::FromRGB (spectrum.cpp:103-187)
+__device__ __forceinline__ float illum_band(const float rgb[3], int c) {
+    const float R = rgb[0], G = rgb[1], B = rgb[2];
+    float r = 0.f;
+    if (R <= G && R <= B) {
+        r += kIllum[0][c] * R;
+        if (G <= B) {
+            r += kIllum[1][c] * (G - R);
+            r += kIllum[6][c] * (B - G);
+        } else {
+            r += kIllum[1][c] * (B - R);
+            r += kIllum[5][c] * (G - B);
+        }
+    } else if (G <= R && G <= B) {
+        r += kIllum[0][c] * G;
+        if (R <= B) {
+            r += kIllum[2][c] * (R - G);
+            r += kIllum[6][c] * (B - R);
+        } else {
+            r += kIllum[2][c] * (B - G);
+            r += kIllum[4][c] * (R - B);
+        }
+    } else {
+        r += kIllum[0][c] * B;
+        if (R <= G) {
+            r += kIllum[3][c] * (R - B);
+            r += kIllum[5][c] * (G - R);
+        } else {
+            r += kIllum[3][c] * (G - B);
+            r += kIllum[4][c] * (R - G);
+        }
+    }
+    const float v = r * .86445f;
+    return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
+}
+
+__device__ __forceinline__ bool inf_nonblack(const RenderLight &L, float s, float t) {  // !Le.IsBlack()
+    float rgb[3];
+    inf_lookup(L, s, t, rgb);
+    for (int c = 0; c < NB; ++c)
+        if (illum_band(rgb, c) != 0.f) return true;
+    return false;
+}
+
+// InfiniteAreaLight::Le (infinite.cpp:115-120): map coordinates of a world direction
+__device__ __forceinline__ void inf_coords(const RenderLight &L, V3 d, float &s, float &t) {
+    const V3 wh = normalize(xform3(L.w2l, d));
+    float ph = m_atan2(wh.y, wh.x);  // SphericalPhi
+    ph = ph < 0.f ? ph + 2.f * kPiF : ph;
+    s = ph * 0.15915494309189533577f;  // INV_TWOPI
+    const float z = wh.z < -1.f ? -1.f : (wh.z > 1.f ? 1.f : wh.z);
+    t = m_acos(z) * kInvPiF;  // SphericalTheta * INV_PI
+}
+
+// InfiniteAreaLight::Sample_L (infinite.cpp:195-218): the 1x1 map's Distribution2D returns
+// uv = (u0, u1) with mapPdf = map_pdf_sample; VisibilityTester::SetRay (light.h:93-96)
+__device__ __forceinline__ LightSampleOut sample_infinite(const RenderLight &L, V3 p, float peps, float u0, float u1) {
+    LightSampleOut r;
+    const float theta = u1 * kPiF, phi = (u0 * 2.f) * kPiF;
+    const float costheta = m_cos(theta), sintheta = m_sin(theta);
+    const float sinphi = m_sin(phi), cosphi = m_cos(phi);
+    r.wi = xform3(L.l2w, V3{sintheta * cosphi, sintheta * sinphi, costheta});
+    r.pdf = L.map_pdf_sample / (((2.f * kPiF) * kPiF) * sintheta);
+    if (sintheta == 0.f) r.pdf = 0.f;
+    r.so = p;
+    r.sd = r.wi;
+    r.smint = peps;
+    r.smaxt = INFINITY;
+    r.nonblack = inf_nonblack(L, u0, u1);
+    return r;
+}
+
+// InfiniteAreaLight::Pdf (infinite.cpp:222-232)
+__device__ __forceinline__ float infinite_pdf(const RenderLight &L, V3 w) {
+    const V3 wi = xform3(L.w2l, w);
+    const float z = wi.z < -1.f ? -1.f : (wi.z > 1.f ? 1.f : wi.z);
+    const float sintheta = m_sin(m_acos(z));
+    if (sintheta == 0.f) return 0.f;
+    return L.map_pdf_eval / (((2.f * kPiF) * kPiF) * sintheta);
+}
+
 __device__ __forceinline__ float rho_lookup(const float *hd, int n, float ct) {  // multipole.cpp:458-463
     const float fid = ct * (float)(n - 1);
     int id = (int)fid;
@@ -200,14 +306,20 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
         const uint32_t scr1 = hash3(seed, (uint32_t)i, 16u * l + DIM_IRR_POS + 8u);
         for (int s = 0; s < ns; ++s) {
             const float u0 = van_der_corput((uint32_t)s, scr0), u1 = sobol2((uint32_t)s, scr1);  // Sample02
-            const LightSampleOut ls = sample_light(L, p, eps, u0, u1);
+            const LightSampleOut ls = L.kind ? sample_infinite(L, p, eps, u0, u1) : sample_light(L, p, eps, u0, u1);
             if (dot(ls.wi, nrm) <= 0.f) continue;
             if (!ls.nonblack || ls.pdf == 0.f) continue;
             if (!trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
                 float ct = absdot(ls.wi, nrm);
                 ct = ct < 1.f ? ct : 1.f;
                 const float Ft = bss ? 1.f - rho_lookup(mat->rho, mat->n_rho, ct) : 1.f;
-                for (int c = 0; c < NB; ++c) El[c] += Ft * L.Lemit[c] * ct / ls.pdf;
+                if (L.kind) {  // Li = Spectrum(map lookup at uv = (u0, u1), SPECTRUM_ILLUMINANT)
+                    float rgb[3];
+                    inf_lookup(L, u0, u1, rgb);
+                    for (int c = 0; c < NB; ++c) El[c] += Ft * illum_band(rgb, c) * ct / ls.pdf;
+                } else {
+                    for (int c = 0; c < NB; ++c) El[c] += Ft * L.Lemit[c] * ct / ls.pdf;
+                }
             }
         }
         for (int c = 0; c < NB; ++c) E[c] += El[c] / (float)ns;
@@ -256,7 +368,9 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
         const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
         d = xform_vector(sc.camera_to_world, normalize(pcam));
         h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 256);
-        if (h.tri != INT_MIN && h.tri < 0) {  // an area light's own surface: Le only
+        if (h.tri == INT_MIN) {  // SamplerRenderer::Li: Li += lights[i]->Le(ray) for every light
+            if (sc.n_infinite > 0) flags |= REC_LE | (0xffu << REC_LIGHT_SHIFT);
+        } else if (h.tri < 0) {  // an area light's own surface: Le only
             const int l = -1 - h.tri;
             if (dot(h.lnn, -d) > 0.f) flags |= REC_LE | ((uint32_t)l << REC_LIGHT_SHIFT);
         } else if (h.tri != INT_MIN) {
@@ -282,8 +396,9 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
         // sample index (16 bits) | material (8 bits) | SSS bit 31
         rec.hit_s[slot] = (uint32_t)s | (flags & (0xffu << REC_MAT_SHIFT)) | ((flags & REC_SSS) ? 0x80000000u : 0u);
     } else if (has_l) {
-        // light seen directly: light index (8 bits) | bit 30
+        // light seen directly: light index (8 bits; 0xff = the infinite lights of a miss) | bit 30
         rec.hit_s[slot] = (((flags >> REC_LIGHT_SHIFT) & 0xffu) << REC_MAT_SHIFT) | 0x40000000u;
+        rec.hit_b[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(pix));
     }
 }
 
@@ -351,7 +466,8 @@ struct DirectTerms {       // 16 words: one EstimateDirect
 static_assert(sizeof(DirectTerms) == 64, "one 64-B record per light sample");
 
 __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
-                                                           int max_hits, int ns_max, DirectTerms *terms) {
+                                                           int max_hits, int ns_max, DirectTerms *terms,
+                                                           float4 *__restrict__ inf_st) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -400,8 +516,10 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                    sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR), sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u),
                    sbc = hash3(seed, pix, 16u * l + DIM_BSDF_COMP);
     // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
-    const LightSampleOut ls = sample_light(L, fr.p, reps, van_der_corput(nidx, sl0), sobol2(nidx, sl1));
+    const float lu0 = van_der_corput(nidx, sl0), lu1 = sobol2(nidx, sl1);
+    const LightSampleOut ls = L.kind ? sample_infinite(L, fr.p, reps, lu0, lu1) : sample_light(L, fr.p, reps, lu0, lu1);
     float lightPdf = ls.pdf;
+    float4 st = make_float4(lu0, lu1, 0.f, 0.f);
     if (lightPdf > 0.f && ls.nonblack && ncomp > 0) {
         const V3 wi_l = to_local(fr, ls.wi);
         const Lobe f1 = bsdf_lobe(mat, dot(ls.wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
@@ -431,12 +549,23 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
             }
             const Lobe f2 = bsdf_lobe(mat, dot(wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
             if (!lobe_black(mat, f2) && bsdfPdf > 0.f) {
-                lightPdf = sphere_pdf(L.s, fr.p, wi);
+                lightPdf = L.kind ? infinite_pdf(L, wi) : sphere_pdf(L.s, fr.p, wi);
                 if (lightPdf != 0.f) {
                     const float w = power_heuristic(bsdfPdf, lightPdf);
                     const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
-                    // Li = lightIsect.Le(-wi) when the hit primitive is this light
-                    if (hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f) {
+                    // Li = lightIsect.Le(-wi) when the hit primitive is this light; light->Le(ray)
+                    // when the ray escapes (0 for an area light)
+                    bool lit;
+                    if (L.kind) {
+                        lit = hl.tri == INT_MIN;
+                        if (lit) {
+                            inf_coords(L, wi, st.z, st.w);
+                            lit = inf_nonblack(L, st.z, st.w);
+                        }
+                    } else {
+                        lit = hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f;
+                    }
+                    if (lit) {
                         out.adn = absdot(wi, fr.nn);
                         out.w2 = w;
                         out.pdf2 = bsdfPdf;
@@ -447,6 +576,7 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
         }
     }
     terms[gid] = out;
+    if (L.kind) inf_st[gid] = st;
 }
 
 // A scene without lights: no direct light and (Preprocess returned early) no octree.
@@ -462,7 +592,8 @@ __global__ __launch_bounds__(256) void shade_nolight_kernel(RenderScene sc, Samp
 // ld[c] = sum over lights of (sum over j of (0 + light term + BSDF term)) / ns, band by band in
 // the order UniformSampleAllLights accumulates (Ld += EstimateDirect; L += Ld / nSamples).
 __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
-                                                             const DirectTerms *__restrict__ terms) {
+                                                             const DirectTerms *__restrict__ terms,
+                                                             const float4 *__restrict__ inf_st) {
     const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int nhits = *rec.hit_count;
     if (slot >= nhits || slot >= max_hits) return;
@@ -479,9 +610,18 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
             for (int j = 0; j < ns; ++j) {
                 const DirectTerms &e = t[l * ns_max + j];
                 if (!e.l1.kind && !e.l2.kind) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
+                float Li1 = L.Lemit[c], Li2 = L.Lemit[c];
+                if (L.kind) {  // Spectrum(map lookup, SPECTRUM_ILLUMINANT) at each term's direction
+                    const float4 st = inf_st[(size_t)slot * sc.nlights * ns_max + l * ns_max + j];
+                    float rgb[3];
+                    inf_lookup(L, st.x, st.y, rgb);
+                    Li1 = illum_band(rgb, c);
+                    inf_lookup(L, st.z, st.w, rgb);
+                    Li2 = illum_band(rgb, c);
+                }
                 float ed = 0.f;
-                if (e.l1.kind) ed += lobe_value(mat, e.l1, c) * L.Lemit[c] * e.k1;
-                if (e.l2.kind) ed += lobe_value(mat, e.l2, c) * L.Lemit[c] * e.adn * e.w2 / e.pdf2;
+                if (e.l1.kind) ed += lobe_value(mat, e.l1, c) * Li1 * e.k1;
+                if (e.l2.kind) ed += lobe_value(mat, e.l2, c) * Li2 * e.adn * e.w2 / e.pdf2;
                 Ld += ed;
             }
             ld += Ld / (float)ns;
@@ -505,6 +645,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
     const float *le = nullptr, *mo = nullptr, *ld = nullptr;
     const RenderMaterial *mat = nullptr;
     float kss = 0.f;
+    if ((hs & 0x40000000u) && ((hs >> REC_MAT_SHIFT) & 0xffu) == 0xffu) return;  // escaped: sky_kernel
     if (hs & 0x40000000u) {
         le = sc.lights[(hs >> REC_MAT_SHIFT) & 0xffu].Lemit;
     } else {
@@ -528,6 +669,48 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
             L += t;
         }
         if (ld) L += ld[c];
+        nan = nan || (L != L);
+        X += kCieX[c] * L;
+        Y += kCieY[c] * L;
+        Z += kCieZ[c] * L;
+    }
+    const float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
+    const float y = Y * (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
+    X *= scale;
+    Y *= scale;
+    Z *= scale;
+    if (nan || y < -1e-5f || __builtin_isinf(y)) X = Y = Z = 0.f;
+    rec.xyz[slot] = make_float4(X, Y, Z, 0.f);
+}
+
+// Camera rays that escaped with infinite lights in the scene (SamplerRenderer::Li,
+// samplerrenderer.cpp:144-151): L = 0 + sum over lights of Le(ray), area lights adding 0; then
+// the sample filter and ToXYZ as in assemble_kernel. A separate launch keeps assemble_kernel's
+// registers (and occupancy) independent of the 30-band sky sum.
+__global__ __launch_bounds__(256) void sky_kernel(RenderScene sc, SampleRecs rec, int max_hits) {
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if (slot >= nhits || slot >= max_hits) return;
+    const uint32_t hs = rec.hit_s[slot];
+    if (!((hs & 0x40000000u) && ((hs >> REC_MAT_SHIFT) & 0xffu) == 0xffu)) return;
+    const float4 hb = rec.hit_b[slot];
+    float Ls[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) Ls[c] = 0.f;
+    for (int l = 0; l < sc.nlights; ++l) {
+        const RenderLight &Lt = sc.lights[l];
+        if (!Lt.kind) continue;
+        float s, t, rgb[3];
+        inf_coords(Lt, V3{hb.x, hb.y, hb.z}, s, t);
+        inf_lookup(Lt, s, t, rgb);
+#pragma unroll
+        for (int c = 0; c < NB; ++c) Ls[c] += illum_band(rgb, c);
+    }
+    float X = 0.f, Y = 0.f, Z = 0.f;
+    bool nan = false;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        const float L = Ls[c];
         nan = nan || (L != L);
         X += kCieX[c] * L;
         Y += kCieY[c] * L;

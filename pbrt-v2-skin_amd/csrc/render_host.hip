@@ -49,11 +49,34 @@ void Context::add_mesh(uint32_t nv, const float *P, const float *N, const float 
 void Context::add_sphere_light(const float *c, float r, const float *Lemit, int nsamples) {
     if (!(r > 0.f)) throw Error(MPSS_ERR_INVALID, "add_sphere_light: radius must be positive");
     if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_sphere_light: nsamples must be >= 1");
-    SphereLight l;
+    if (scene_.lights.size() >= 254) throw Error(MPSS_ERR_INVALID, "add_sphere_light: at most 254 lights");
+    SceneLight l;
     memcpy(l.center, c, sizeof(l.center));
     l.radius = r;
     memcpy(l.Lemit, Lemit, sizeof(l.Lemit));
     l.nsamples = cfg_.quick_render ? std::max(1, nsamples / 4) : nsamples;  // CreateDiffuseAreaLight
+    scene_.lights.push_back(l);
+    scene_dirty_ = true;
+}
+
+// CreateInfiniteLight + the InfiniteAreaLight ctor without a map (lights/infinite.cpp:66-90,
+// 180-188): texels[0] = L.ToRGBSpectrum(); Le and Sample_L convert map lookups back with
+// Spectrum(rgb, SPECTRUM_ILLUMINANT) on the device (render.hip).
+void Context::add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l) {
+    if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_infinite_light: nsamples must be >= 1");
+    if (scene_.lights.size() >= 254) throw Error(MPSS_ERR_INVALID, "add_infinite_light: at most 254 lights");
+    SceneLight l;
+    l.kind = 1;
+    l.center[0] = l.center[1] = l.center[2] = 0.f;
+    l.radius = 0.f;
+    memcpy(l.Lemit, L, sizeof(l.Lemit));
+    spectrum_to_rgb(L, l.rgb);
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) {
+            l.l2w[3 * r + k] = l2w[4 * r + k];
+            l.w2l[3 * r + k] = w2l[4 * r + k];
+        }
+    l.nsamples = cfg_.quick_render ? std::max(1, nsamples / 4) : nsamples;  // CreateInfiniteLight
     scene_.lights.push_back(l);
     scene_dirty_ = true;
 }
@@ -110,7 +133,7 @@ void Context::upload_scene() {
     }
     d_meshes_.upload(rm.data(), rm.size());
     std::vector<RenderLight> rl;
-    for (const SphereLight &l : scene_.lights) {
+    for (const SceneLight &l : scene_.lights) {
         RenderLight r{};
         r.s.c = V3{l.center[0], l.center[1], l.center[2]};
         r.s.r = l.radius;
@@ -119,6 +142,19 @@ void Context::upload_scene() {
         r.s.theta_max = m_acos(1.f);
         r.s.area = r.s.phi_max * l.radius * (l.radius - -l.radius);  // Sphere::Area
         memcpy(r.Lemit, l.Lemit, sizeof(r.Lemit));
+        r.kind = l.kind;
+        if (l.kind == 1) {
+            memcpy(r.rgb, l.rgb, sizeof(r.rgb));
+            memcpy(r.l2w, l.l2w, sizeof(r.l2w));
+            memcpy(r.w2l, l.w2l, sizeof(r.w2l));
+            // img[0] = radianceMap->Lookup(0, 0, 1).y() * sinf(M_PI * 0.5f): the texel's y() times 1
+            const float f = ((0.212671f * l.rgb[0] + 0.715160f * l.rgb[1]) + 0.072169f * l.rgb[2]) *
+                            m_sin(kPiF * (0.5f / 1.f));
+            r.map_pdf_sample = (f / f) * (f / f);
+            const float ff = f * f;
+            r.map_pdf_eval = ff == 0.f ? 0.f : ff / ff;
+            r.s.r = 0.f;
+        }
         r.nsamples_pow2 = round_up_pow2(l.nsamples);
         r.nsamples_round = round_up_pow2(l.nsamples);
         rl.push_back(r);
@@ -165,6 +201,7 @@ RenderScene Context::render_scene() const {
     sc.lights = d_lights_.ptr;
     sc.materials = d_materials_.ptr;
     sc.nlights = (int)scene_.lights.size();
+    for (const SceneLight &l : scene_.lights) sc.n_infinite += l.kind == 1;
     sc.nmaterials = (int)materials_.size();
     sc.xres = scene_.camera.xres;
     sc.yres = scene_.camera.yres;
@@ -331,19 +368,27 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
                            ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
             int ns_max = 1;
-            for (const SphereLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
+            for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
             const int64_t lanes = total * std::max<int64_t>(1, (int64_t)scene_.lights.size()) * ns_max;
             if (ws_terms_n_ < lanes) {
                 ws_terms_.alloc((size_t)lanes * 64);
                 ws_terms_n_ = lanes;
             }
             DirectTerms *terms = reinterpret_cast<DirectTerms *>(ws_terms_.ptr);
+            float4 *inf_st = nullptr;
+            if (sc.n_infinite > 0) {
+                if (ws_st_n_ < lanes) {
+                    ws_st_.alloc((size_t)lanes);
+                    ws_st_n_ = lanes;
+                }
+                inf_st = ws_st_.ptr;
+            }
             time_begin(stream, ev);
             if (!scene_.lights.empty()) {
                 hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream,
-                                   sc, rec, spp, seed, (int)total, ns_max, terms);
+                                   sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
                 hipLaunchKernelGGL(direct_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                                   sc, rec, (int)total, ns_max, (const DirectTerms *)terms);
+                                   sc, rec, (int)total, ns_max, (const DirectTerms *)terms, (const float4 *)inf_st);
             } else {
                 hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                                    sc, rec, (int)total);
@@ -367,6 +412,9 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                            ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
             hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
                                bp, (int)total);
+            if (sc.n_infinite > 0)
+                hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
+                                   (int)total);
         }
         for (size_t k = pi; k < pe; ++k) {
             const TileBatch &tb = pieces[k].tb;

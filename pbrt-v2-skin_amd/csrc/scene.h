@@ -1,5 +1,5 @@
 // scene.h -- the scene slice the multipole path needs (host side): triangle meshes in world
-// space, sphere area lights, perspective camera, the BVH over triangles, and the tessellated
+// space, sphere area lights and constant infinite lights, perspective camera, the BVH over triangles, and the tessellated
 // SurfacePoint set (reference: shapes/trianglemesh.{cpp,inl}, shapes/sphere.cpp,
 // lights/diffuse.cpp, cameras/perspective.cpp, accelerators/bvh.cpp,
 // renderers/surfacepoints.cpp:301-369).
@@ -21,9 +21,15 @@ struct Mesh {
     bool reverse_orientation = false, swaps_handedness = false;
 };
 
-struct SphereLight {  // AreaLightSource "area" on Shape "sphere" (translation-only placement)
+// scene->lights in declaration order. kind 0: AreaLightSource "area" on Shape "sphere"
+// (translation-only placement, lights/diffuse.cpp); kind 1: LightSource "infinite" with a
+// constant radiance map (lights/infinite.cpp:66-106, the 1x1 map of a light without "mapname").
+struct SceneLight {
+    int kind = 0;
     float center[3], radius;
-    float Lemit[NB];
+    float Lemit[NB];      // kind 0: DiffuseAreaLight::Lemit
+    float rgb[3];         // kind 1: the map's one texel, (L * scale).ToRGBSpectrum()
+    float l2w[9], w2l[9]; // kind 1: LightToWorld / WorldToLight (upper 3x3, row-major)
     int nsamples;
 };
 
@@ -55,7 +61,7 @@ struct alignas(16) TriRec {
 
 struct SceneData {
     std::vector<Mesh> meshes;
-    std::vector<SphereLight> lights;
+    std::vector<SceneLight> lights;
     Camera camera;
     // flattened (all meshes)
     std::vector<int32_t> tri_mesh, tri_local;  // global tri -> mesh, local index

@@ -23,4 +23,19 @@ inline float spectrum_y(const float *s) {
     return yy * (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
 }
 
+// SampledSpectrum::ToXYZ + XYZToRGB (spectrum.h:51-55, 370-393): ToRGBSpectrum's texel value
+inline void spectrum_to_rgb(const float *s, float rgb[3]) {
+    float xyz[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < NB; ++i) {
+        xyz[0] += MPSS_BAND_CIE_X[i] * s[i];
+        xyz[1] += MPSS_BAND_CIE_Y[i] * s[i];
+        xyz[2] += MPSS_BAND_CIE_Z[i] * s[i];
+    }
+    const float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
+    for (int k = 0; k < 3; ++k) xyz[k] *= scale;
+    rgb[0] = (3.240479f * xyz[0] - 1.537150f * xyz[1]) - 0.498535f * xyz[2];
+    rgb[1] = (-0.969256f * xyz[0] + 1.875991f * xyz[1]) + 0.041556f * xyz[2];
+    rgb[2] = (0.055648f * xyz[0] - 0.204043f * xyz[1]) + 1.057311f * xyz[2];
+}
+
 }  // namespace mpss

@@ -8,8 +8,8 @@ for the directives scenes/skin.pbrt and its relatives contain:
   Sampler (pixelsamples), SurfaceIntegrator "multipolesubsurface" (maxdepth, maxerror,
   minsampledistance, mix, showirradiancepoints, incenter), WorldBegin/WorldEnd,
   AttributeBegin/End, TransformBegin/End, Translate, Rotate, Scale, Identity,
-  Texture "constant", Material "layeredskin", AreaLightSource "area", Shape "sphere" (as an
-  area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
+  Texture "constant", Material "layeredskin", AreaLightSource "area", LightSource "infinite"
+  (constant L * scale, nsamples; no "mapname"), Shape "sphere" (as an area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
   package's stand-in for huge inline arrays, see tools/make_scene.py), Include.
 
 Transforms follow core/transform.cpp (Translate, Scale, Rotate, LookAt, Perspective) evaluated in
@@ -156,7 +156,7 @@ class Scene:
         self.integrator = {}
         self.materials = []  # list of layeredskin param dicts
         self.meshes = []     # dicts: P (world), N, S, uv, indices, o2w, w2o, reverse, material
-        self.lights = []     # dicts: center, radius, L (rgb), nsamples
+        self.lights = []     # dicts: center, radius, L (rgb), nsamples; or kind="infinite", L, scale, l2w, w2l
         self.base_dir = "."
         self.renderer = None  # ("mcprofile", ParamSet) when the file selects the MC profile renderer
 
@@ -261,7 +261,14 @@ def load(path, **override):
                 elif d == "AreaLightSource":
                     state["area"] = (ps.find("L", [1.0, 1.0, 1.0]), ps.one("nsamples", 1))
                 elif d == "LightSource":
-                    raise ValueError("LightSource %r is outside this path" % cls)
+                    if cls != "infinite":
+                        raise ValueError("LightSource %r is outside this path" % cls)
+                    if ps.find("mapname"):
+                        raise ValueError("infinite light maps (\"mapname\") are not supported; only a "
+                                         "constant L (DESIGN.md)")
+                    sc.lights.append(dict(kind="infinite", L=_rgb3(ps.find("L", [1.0])),
+                                          scale=_rgb3(ps.find("scale", [1.0])), nsamples=int(ps.one("nsamples", 1)),
+                                          l2w=ctm.astype(np.float32), w2l=np.linalg.inv(ctm).astype(np.float32)))
                 elif d == "Shape":
                     _shape(sc, cls, ps, ctm, state, base)
             else:
@@ -354,6 +361,13 @@ def integrator_config(sc, **kw):
     return cfg
 
 
+def infinite_L(li):
+    """CreateInfiniteLight's L * scale (lights/infinite.cpp:180-188): both "color" parameters are
+    Spectrum::FromRGB (reflectance, paramset.cpp:97-105), multiplied band by band."""
+    import mpss
+    return (mpss.host_from_rgb(li["L"]) * mpss.host_from_rgb(li["scale"])).astype(np.float32)
+
+
 def build_context(sc, **cfg_kw):
     """Create an mpss.Context holding the scene (materials, meshes, lights, camera)."""
     import mpss
@@ -369,7 +383,10 @@ def build_context(sc, **cfg_kw):
         ctx.add_mesh(me["P"], me["indices"], me["o2w"], me["w2o"], mids[me["material"]], N=me["N"], S=me["S"],
                      uv=me["uv"], reverse=me["reverse"])
     for li in sc.lights:
-        ctx.add_sphere_light(li["center"], li["radius"], mpss.host_from_rgb(li["L"]), li["nsamples"])
+        if li.get("kind") == "infinite":
+            ctx.add_infinite_light(infinite_L(li), li["nsamples"], li["l2w"], li["w2l"])
+        else:
+            ctx.add_sphere_light(li["center"], li["radius"], mpss.host_from_rgb(li["L"]), li["nsamples"])
     r2c, c2w = sc.raster_to_camera()
     ctx.set_camera(r2c, c2w, sc.xres, sc.yres)
     pf = sc.integrator.get("pointsfile")

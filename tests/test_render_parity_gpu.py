@@ -137,3 +137,40 @@ def test_image_parity_transmission_lobe(mpss, oracle, scene, kt):
     got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 21)
     ref = o.render_tile(sc.spp, 21, 0, sc.xres, 0, sc.yres)
     _check(got, ref)
+
+
+def _sky_light(deg, axis, L=(0.3, 0.35, 0.45), scale=(2, 2, 2), ns=4):
+    from mpss import pbrtscene
+    l2w = pbrtscene.rotate(deg, axis)
+    return dict(kind="infinite", L=list(L), scale=list(scale), nsamples=ns, l2w=l2w.astype(np.float32),
+                w2l=np.linalg.inv(l2w).astype(np.float32))
+
+
+@pytest.mark.parametrize("scene,lights", [("tissue_sky.pbrt", None), ("skin.pbrt", "sky+area"),
+                                          ("skin.pbrt", "sky")])
+def test_image_parity_infinite_light(mpss, oracle, scene, lights):
+    """LightSource "infinite" with a constant map (lights/infinite.cpp): Sample_L / Pdf for
+    irradiance and both MIS halves of EstimateDirect, Le for BSDF rays and camera rays that
+    escape; alone, and mixed with the sphere light in either order."""
+    import torch
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", scene), xres=48, yres=48, spp=4)
+    sc.integrator["minsampledistance"] = 0.008
+    for m in sc.materials:
+        m["desired_length"] = 128
+    if lights == "sky+area":
+        sc.lights = [sc.lights[0], _sky_light(40, [1, 1, 0], ns=2)]
+    elif lights == "sky":
+        sc.lights = [_sky_light(-70, [0, 1, 1], L=(0.8, 0.6, 0.5), ns=8)]
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=6)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    E = o.irradiance(pts, 6)
+    got_E = ctx.irradiance()
+    np.testing.assert_allclose(got_E, E, rtol=1e-5, atol=1e-6 * float(E.max()))
+    assert (got_E == E).mean() >= 0.99
+    o.set_octree(pts, E)
+    got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 17)
+    ref = o.render_tile(sc.spp, 17, 0, sc.xres, 0, sc.yres)
+    _check(got, ref)
