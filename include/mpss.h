@@ -131,6 +131,12 @@ int mpss_add_sphere_light(mpss_ctx *ctx, const float *center, float radius, cons
  * scene->lights in call order, mixed with sphere lights; at most 254 lights. */
 int mpss_add_infinite_light(mpss_ctx *ctx, const float *L, int nsamples, const float *light_to_world,
                             const float *world_to_light);
+/* LightSource "infinite" with "mapname": texels = the image ReadImage returns (width x height RGB
+ * triples, row-major, top row first), before the light multiplies them by L.ToRGBSpectrum(). The
+ * MIPMap (Lanczos resampling to powers of two) and the Distribution2D over img(u, v) * sin(theta)
+ * are built here (infinite.cpp:66-106, mipmap.h:147-220, montecarlo.h:54-175). */
+int mpss_add_infinite_light_map(mpss_ctx *ctx, const float *L, int nsamples, const float *light_to_world,
+                                const float *world_to_light, int width, int height, const float *texels);
 /* PerspectiveCamera (cameras/perspective.cpp): RasterToCamera and CameraToWorld, row-major 4x4. */
 int mpss_set_camera(mpss_ctx *ctx, const float *raster_to_camera, const float *camera_to_world, int xres, int yres);
 /* SurfacePoint records (44 B: p[3] n[3] u v materialId area rayEpsilon, renderers/surfacepoints.h:45-55),

@@ -106,7 +106,21 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T /* nullable:
 int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
                      const int32_t *idx, const float *o2w, const float *w2o, int flip, int material);
 int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *Le, int nsamples);
-int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l);
+/* texels: W x H RGB as ReadImage returns them, or NULL for a light without "mapname" */
+int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l, int W,
+                               int H, const float *texels);
+
+/* envmap.c: InfiniteAreaLight's radiance MIPMap level 0 and Distribution2D */
+typedef struct {
+    int tw, th, nu, nv;
+    float *tex, *func, *cdf, *rint, *mcdf;
+    float mint;
+} o_envmap;
+int o_envmap_build(int W, int H, const float *texels, o_envmap *m);
+void o_envmap_free(o_envmap *m);
+void o_envmap_lookup(const o_envmap *m, float s, float t, float out[3]);
+void o_envmap_sample(const o_envmap *m, float u0, float u1, float uv[2], float *pdf);
+float o_envmap_pdf(const o_envmap *m, float u, float v);
 long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_point *out, long cap);
 void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E);
 void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, const float *E, const float *area,

@@ -134,8 +134,8 @@ typedef struct {
     float r, phimax, thetamin, thetamax, area;
     float Le[O_NB];
     int ns_pow2;
-    float rgb[3], l2w[9], w2l[9]; /* kind 1: the texel, LightToWorld, WorldToLight */
-    float f;                      /* kind 1: Distribution2D's img[0] = texel.y() * sin(pi/2) */
+    float l2w[9], w2l[9]; /* kind 1: LightToWorld, WorldToLight */
+    o_envmap em;          /* kind 1: radiance map + Distribution2D */
 } o_light;
 
 typedef struct {
@@ -249,23 +249,34 @@ int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *L
     return s->nlights++;
 }
 
-/* CreateInfiniteLight + InfiniteAreaLight ctor without a map (lights/infinite.cpp:66-106, 180-188):
- * L is the 30-band L * scale; the map's one texel is L.ToRGBSpectrum() */
-int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l) {
+/* CreateInfiniteLight + InfiniteAreaLight ctor (lights/infinite.cpp:66-106, 180-188): L is the
+ * 30-band L * scale; texels are multiplied by L.ToRGBSpectrum(), or the map is that one texel */
+int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l, int W,
+                               int H, const float *texels) {
     s->lights = (o_light *)realloc(s->lights, (s->nlights + 1) * sizeof(o_light));
     o_light *l = &s->lights[s->nlights];
     memset(l, 0, sizeof(*l));
     l->kind = 1;
-    o_to_rgb(L, l->rgb);
+    float rgb[3];
+    o_to_rgb(L, rgb);
+    float *t;
+    if (texels) {
+        t = (float *)malloc((size_t)W * H * 3 * sizeof(float));
+        for (size_t i = 0; i < (size_t)W * H; ++i)
+            for (int k = 0; k < 3; ++k) t[3 * i + k] = texels[3 * i + k] * rgb[k];
+    } else {
+        W = H = 1;
+        t = (float *)malloc(3 * sizeof(float));
+        memcpy(t, rgb, sizeof(rgb));
+    }
+    int rc = o_envmap_build(W, H, t, &l->em);
+    free(t);
+    if (rc) return -1;
     for (int r = 0; r < 3; ++r)
         for (int k = 0; k < 3; ++k) {
             l->l2w[3 * r + k] = l2w[4 * r + k];
             l->w2l[3 * r + k] = w2l[4 * r + k];
         }
-    /* img[u + v*width] = radianceMap->Lookup(up, vp, filter).y() * sinTheta; filter 1 on a 1x1
-     * map is level 0's texel (mipmap.h:239-255); RGBSpectrum::y() */
-    float y = 0.212671f * l->rgb[0] + 0.715160f * l->rgb[1] + 0.072169f * l->rgb[2];
-    l->f = y * fsin(PI_F * (float)(0 + .5f) / (float)1);
     l->ns_pow2 = round_up_pow2(nsamples);
     return s->nlights++;
 }
@@ -492,18 +503,10 @@ static v3 xvec3(const float *m, v3 v) { /* Transform::operator()(Vector), transf
               m[6] * v.x + m[7] * v.y + m[8] * v.z);
 }
 
-/* Spectrum(radianceMap->Lookup(s, t), SPECTRUM_ILLUMINANT): MIPMap::Lookup with width 0 is
- * triangle(0, s, t) (mipmap.h:239-269) over TEXTURE_REPEAT copies of the one texel */
+/* Spectrum(radianceMap->Lookup(s, t), SPECTRUM_ILLUMINANT) */
 static void inf_le(const o_light *L, float s, float t, float out[O_NB]) {
-    s = s * (float)1u - 0.5f;
-    t = t * (float)1u - 0.5f;
-    int s0 = (int)floorf(s), t0 = (int)floorf(t);
-    float ds = s - s0, dt = t - t0;
     float rgb[3];
-    for (int k = 0; k < 3; ++k) {
-        float c = L->rgb[k];
-        rgb[k] = (1.f - ds) * (1.f - dt) * c + (1.f - ds) * dt * c + ds * (1.f - dt) * c + ds * dt * c;
-    }
+    o_envmap_lookup(&L->em, s, t, rgb);
     o_from_rgb(rgb, 1, out);
 }
 
@@ -523,19 +526,17 @@ static int black(const float *x) {
     return 1;
 }
 
-/* Distribution1D of one value f (montecarlo.h): SampleContinuous's pdf = func / funcInt */
-static float d1_pdf(float f) { return f / f; } /* 0 / 0 = NaN when funcInt == 0 */
-
-/* InfiniteAreaLight::Pdf (infinite.cpp:222-232) with Distribution2D::Pdf of the 1x1 map */
+/* InfiniteAreaLight::Pdf (infinite.cpp:222-232) */
 static float inf_pdf(const o_light *L, v3 w) {
     v3 wi = xvec3(L->w2l, w);
     float z = wi.z < -1.f ? -1.f : (wi.z > 1.f ? 1.f : wi.z);
     float theta = facos(z);
+    float phi = fatan2(wi.y, wi.x);
+    if (phi < 0.f) phi = phi + 2 * PI_F;
     float sintheta = fsin(theta);
     if (sintheta == 0.f) return 0.f;
-    float fi = L->f * L->f;
-    float dp = fi == 0.f ? 0.f : (L->f * L->f) / fi;
-    return dp / (2.f * PI_F * PI_F * sintheta);
+    float p = o_envmap_pdf(&L->em, phi * 0.15915494309189533577f, theta * INV_PI_F) / (2.f * PI_F * PI_F * sintheta);
+    return p;
 }
 
 /* Sample_L of either light kind: wi, pdf, shadow ray, radiance non-black flag, and for the
@@ -545,10 +546,11 @@ typedef struct { v3 wi, so, sd; float pdf, smint, smaxt; int nonblack; float Li[
 /* InfiniteAreaLight::Sample_L (infinite.cpp:195-218) + VisibilityTester::SetRay */
 static lsamp inf_sample(const o_light *L, v3 p, float peps, float u0, float u1) {
     lsamp r;
-    /* Distribution2D::SampleContinuous on 1x1: uv = (u0, u1) (du = (u - 0) / (1 - 0)) */
-    float uv0 = (0 + (u0 - 0.f) / (1.f - 0.f)) / 1, uv1 = (0 + (u1 - 0.f) / (1.f - 0.f)) / 1;
-    float mapPdf = d1_pdf(L->f) * d1_pdf(L->f);
-    float theta = uv1 * PI_F, phi = uv0 * 2.f * PI_F;
+    memset(&r, 0, sizeof(r));
+    float uv[2], mapPdf;
+    o_envmap_sample(&L->em, u0, u1, uv, &mapPdf);
+    if (mapPdf == 0.f) return r; /* "return 0.f": black, nothing contributes */
+    float theta = uv[1] * PI_F, phi = uv[0] * 2.f * PI_F;
     float costheta = fcos(theta), sintheta = fsin(theta);
     float sinphi = fsin(phi), cosphi = fcos(phi);
     r.wi = xvec3(L->l2w, mk(sintheta * cosphi, sintheta * sinphi, costheta));
@@ -558,7 +560,7 @@ static lsamp inf_sample(const o_light *L, v3 p, float peps, float u0, float u1) 
     r.sd = r.wi;
     r.smint = peps;
     r.smaxt = INFINITY;
-    inf_le(L, uv0, uv1, r.Li);
+    inf_le(L, uv[0], uv[1], r.Li);
     r.nonblack = !black(r.Li);
     return r;
 }
@@ -1327,6 +1329,8 @@ void o_scene_free(o_scene *s) {
         free(s->meshes[m].idx);
     }
     for (int m = 0; m < s->nmats; ++m) { free(s->mats[m].rho); free(s->mats[m].rd); }
+    for (int l = 0; l < s->nlights; ++l)
+        if (s->lights[l].kind) o_envmap_free(&s->lights[l].em);
     free(s->meshes); free(s->lights); free(s->mats);
     free(s->tri_mesh); free(s->tri_local); free(s->tp1); free(s->te1); free(s->te2);
     free(s->bvh); free(s->order);

@@ -45,7 +45,9 @@ public:
     void add_mesh(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
                   const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material);
     void add_sphere_light(const float *c, float r, const float *Lemit, int nsamples);
-    void add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l);
+    // texels: W x H RGB (nullable: no "mapname", the 1x1 map L.ToRGBSpectrum())
+    void add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l, int W = 0, int H = 0,
+                            const float *texels = nullptr);
     void set_camera(const float *r2c, const float *c2w, int xres, int yres);
     void set_surface_points(uint32_t n, const SurfacePoint *pts);
     void preprocess(uint32_t seed);
@@ -75,6 +77,8 @@ private:
     std::vector<std::unique_ptr<DevBuf<float>>> d_mesh_bufs_;
     DevBuf<struct RenderMesh> d_meshes_;
     DevBuf<struct RenderLight> d_lights_;
+    std::vector<std::unique_ptr<DevBuf<float>>> d_envmaps_;  // per infinite light (envmap.h layout)
+    DevBuf<float> d_zero_map_;                                // stand-in map of area lights
     DevBuf<struct RenderMaterial> d_materials_;
     // render workspace: per camera sample (flags, slot) and per surface hit (ld, Mo query, Mo)
     DevBuf<uint32_t> ws_flags_;

@@ -176,6 +176,14 @@ int mpss_add_infinite_light(mpss_ctx *c, const float *L, int ns, const float *l2
     });
 }
 
+int mpss_add_infinite_light_map(mpss_ctx *c, const float *L, int ns, const float *l2w, const float *w2l, int w, int h,
+                                const float *texels) {
+    return guarded([&] {
+        require(c && L && l2w && w2l && texels, "mpss_add_infinite_light_map: null argument");
+        reinterpret_cast<Context *>(c)->add_infinite_light(L, ns, l2w, w2l, w, h, texels);
+    });
+}
+
 int mpss_set_camera(mpss_ctx *c, const float *r2c, const float *c2w, int xres, int yres) {
     return guarded([&] {
         require(c && r2c && c2w, "mpss_set_camera: null argument");

@@ -21,12 +21,14 @@ struct RenderLight {
     float Lemit[NB];
     int nsamples_pow2;   // RoundUpPow2(nSamples): IrradianceTask (file line 196)
     int nsamples_round;  // LDSampler::RoundSize(nSamples): RequestSamples (file line 248)
-    // kind 1 (LightSource "infinite", constant map): the texel, LightToWorld / WorldToLight, and
-    // the 1x1 map's Distribution2D pdfs: SampleContinuous's mapPdf = (f/f)*(f/f) and Pdf()'s
-    // (f*f)/(f*f) (0 when f*f == 0), f = texel.y() * sin(pi/2) (infinite.cpp:92-101, montecarlo.h)
+    // kind 1 (LightSource "infinite"): LightToWorld / WorldToLight, level 0 of the radiance
+    // MIPMap (tw x th RGB texels) and the Distribution2D over the image (nu x nv): conditional
+    // func / cdf rows, their funcInts (= the marginal's func), the marginal cdf and funcInt
+    // (envmap.h). A light without "mapname" is the 1x1 map L.ToRGBSpectrum().
     int kind;
-    float map_pdf_sample, map_pdf_eval;
-    float rgb[3];
+    int tw, th, nu, nv;
+    const float *tex, *func, *cdf, *rint, *mcdf;
+    float mint;
     float l2w[9], w2l[9];
 };
 

@@ -152,6 +152,7 @@ struct LightSampleOut {
     bool nonblack;    // Ls = L(ps, ns, -wi) = Dot(ns, -wi) > 0 ? Lemit : 0
     V3 so, sd;        // shadow segment ray
     float smint, smaxt;
+    float ms, mt;     // infinite light: radiance-map coordinates of the sample
 };
 __device__ __forceinline__ LightSampleOut sample_light(const RenderLight &L, V3 p, float peps, float u0, float u1) {
     LightSampleOut r;
@@ -165,6 +166,7 @@ __device__ __forceinline__ LightSampleOut sample_light(const RenderLight &L, V3 
     r.smint = peps;
     r.smaxt = dist * (1.f - 1e-3f);
     r.nonblack = dot(ns, -r.wi) > 0.f;
+    r.ms = r.mt = 0.f;
     return r;
 }
 
@@ -174,17 +176,46 @@ __device__ __forceinline__ V3 xform3(const float *m, V3 v) {  // Transform::oper
               (m[6] * v.x + m[7] * v.y) + m[8] * v.z};
 }
 
-// MIPMap<RGBSpectrum>::Lookup(s, t) = triangle(0, s, t) (mipmap.h:239-269): four TEXTURE_REPEAT
-// copies of the one texel, weighted (1-ds)(1-dt), (1-ds)dt, ds(1-dt), ds dt and summed in order
+__device__ __forceinline__ int mod_pbrt(int a, int b) {  // Mod (pbrt.h:282-287)
+    const int n = a / b;
+    a -= n * b;
+    return a < 0 ? a + b : a;
+}
+
+// MIPMap<RGBSpectrum>::Lookup(s, t) = triangle(0, s, t) (mipmap.h:239-269) on level 0 with
+// TEXTURE_REPEAT: four texels weighted (1-ds)(1-dt), (1-ds)dt, ds(1-dt), ds dt, summed in order
 __device__ __forceinline__ void inf_lookup(const RenderLight &L, float s, float t, float rgb[3]) {
-    s = s - 0.5f;
-    t = t - 0.5f;
-    const float ds = s - (float)(int)floorf(s), dt = t - (float)(int)floorf(t);
+    s = s * (float)L.tw - 0.5f;
+    t = t * (float)L.th - 0.5f;
+    const int s0 = (int)floorf(s), t0 = (int)floorf(t);
+    const float ds = s - (float)s0, dt = t - (float)t0;
     const float w0 = (1.f - ds) * (1.f - dt), w1 = (1.f - ds) * dt, w2 = ds * (1.f - dt), w3 = ds * dt;
-    for (int k = 0; k < 3; ++k) {
-        const float c = L.rgb[k];
-        rgb[k] = ((c * w0 + c * w1) + c * w2) + c * w3;
+    const int sa = mod_pbrt(s0, L.tw), sb = mod_pbrt(s0 + 1, L.tw);
+    const int ta = mod_pbrt(t0, L.th) * L.tw, tb = mod_pbrt(t0 + 1, L.th) * L.tw;
+    const float *a = L.tex + 3 * (ta + sa), *b = L.tex + 3 * (tb + sa), *c = L.tex + 3 * (ta + sb),
+                *d = L.tex + 3 * (tb + sb);
+    for (int k = 0; k < 3; ++k) rgb[k] = ((a[k] * w0 + b[k] * w1) + c[k] * w2) + d[k] * w3;
+}
+
+// Distribution1D::SampleContinuous (montecarlo.h:81-98): std::upper_bound over cdf[0..count]
+__device__ __forceinline__ float d1_sample(const float *func, const float *cdf, float fint, int count, float u,
+                                           float &pdf, int &off) {
+    int lo = 0, len = count + 1;
+    while (len > 0) {
+        const int half = len >> 1;
+        if (!(u < cdf[lo + half])) {
+            lo += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
     }
+    int offset = lo - 1;
+    offset = offset < 0 ? 0 : (offset > count - 1 ? count - 1 : offset);
+    off = offset;
+    const float du = (u - cdf[offset]) / (cdf[offset + 1] - cdf[offset]);
+    pdf = func[offset] / fint;
+    return ((float)offset + du) / (float)count;
 }
 
 // band c of Spectrum(rgb, SPECTRUM_ILLUMINANT) = SampledSpectrum::FromRGB (spectrum.cpp:103-187)
@@ -241,31 +272,53 @@ __device__ __forceinline__ void inf_coords(const RenderLight &L, V3 d, float &s,
     t = m_acos(z) * kInvPiF;  // SphericalTheta * INV_PI
 }
 
-// InfiniteAreaLight::Sample_L (infinite.cpp:195-218): the 1x1 map's Distribution2D returns
-// uv = (u0, u1) with mapPdf = map_pdf_sample; VisibilityTester::SetRay (light.h:93-96)
+// InfiniteAreaLight::Sample_L (infinite.cpp:195-218): Distribution2D::SampleContinuous
+// (montecarlo.h:154-161) picks a row with the marginal, then a column in that row;
+// VisibilityTester::SetRay (light.h:93-96). (ms, mt) = uv, where Ls is looked up.
 __device__ __forceinline__ LightSampleOut sample_infinite(const RenderLight &L, V3 p, float peps, float u0, float u1) {
     LightSampleOut r;
-    const float theta = u1 * kPiF, phi = (u0 * 2.f) * kPiF;
+    float pdf0, pdf1;
+    int v, col;
+    const float uv1 = d1_sample(L.rint, L.mcdf, L.mint, L.nv, u1, pdf1, v);
+    const float uv0 = d1_sample(L.func + (size_t)v * L.nu, L.cdf + (size_t)v * (L.nu + 1), L.rint[v], L.nu, u0, pdf0, col);
+    const float mapPdf = pdf0 * pdf1;
+    r.ms = uv0;
+    r.mt = uv1;
+    r.so = p;
+    r.smint = peps;
+    r.smaxt = INFINITY;
+    if (mapPdf == 0.f) {  // "return 0.f": Ls black, nothing contributes
+        r.wi = r.sd = V3{0.f, 0.f, 0.f};
+        r.pdf = 0.f;
+        r.nonblack = false;
+        return r;
+    }
+    const float theta = uv1 * kPiF, phi = (uv0 * 2.f) * kPiF;
     const float costheta = m_cos(theta), sintheta = m_sin(theta);
     const float sinphi = m_sin(phi), cosphi = m_cos(phi);
     r.wi = xform3(L.l2w, V3{sintheta * cosphi, sintheta * sinphi, costheta});
-    r.pdf = L.map_pdf_sample / (((2.f * kPiF) * kPiF) * sintheta);
+    r.pdf = mapPdf / (((2.f * kPiF) * kPiF) * sintheta);
     if (sintheta == 0.f) r.pdf = 0.f;
-    r.so = p;
     r.sd = r.wi;
-    r.smint = peps;
-    r.smaxt = INFINITY;
-    r.nonblack = inf_nonblack(L, u0, u1);
+    r.nonblack = inf_nonblack(L, uv0, uv1);
     return r;
 }
 
-// InfiniteAreaLight::Pdf (infinite.cpp:222-232)
+// InfiniteAreaLight::Pdf (infinite.cpp:222-232) with Distribution2D::Pdf (montecarlo.h:162-170)
 __device__ __forceinline__ float infinite_pdf(const RenderLight &L, V3 w) {
     const V3 wi = xform3(L.w2l, w);
     const float z = wi.z < -1.f ? -1.f : (wi.z > 1.f ? 1.f : wi.z);
-    const float sintheta = m_sin(m_acos(z));
+    const float theta = m_acos(z);
+    float phi = m_atan2(wi.y, wi.x);
+    phi = phi < 0.f ? phi + 2.f * kPiF : phi;
+    const float sintheta = m_sin(theta);
     if (sintheta == 0.f) return 0.f;
-    return L.map_pdf_eval / (((2.f * kPiF) * kPiF) * sintheta);
+    int iu = (int)(phi * kInvTwoPiF * (float)L.nu), iv = (int)(theta * kInvPiF * (float)L.nv);
+    iu = iu < 0 ? 0 : (iu > L.nu - 1 ? L.nu - 1 : iu);
+    iv = iv < 0 ? 0 : (iv > L.nv - 1 ? L.nv - 1 : iv);
+    const float ri = L.rint[iv];
+    const float dp = ri * L.mint == 0.f ? 0.f : (L.func[(size_t)iv * L.nu + iu] * ri) / (ri * L.mint);
+    return dp / (((2.f * kPiF) * kPiF) * sintheta);
 }
 
 __device__ __forceinline__ float rho_lookup(const float *hd, int n, float ct) {  // multipole.cpp:458-463
@@ -313,9 +366,9 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
                 float ct = absdot(ls.wi, nrm);
                 ct = ct < 1.f ? ct : 1.f;
                 const float Ft = bss ? 1.f - rho_lookup(mat->rho, mat->n_rho, ct) : 1.f;
-                if (L.kind) {  // Li = Spectrum(map lookup at uv = (u0, u1), SPECTRUM_ILLUMINANT)
+                if (L.kind) {  // Li = Spectrum(map lookup at the sampled uv, SPECTRUM_ILLUMINANT)
                     float rgb[3];
-                    inf_lookup(L, u0, u1, rgb);
+                    inf_lookup(L, ls.ms, ls.mt, rgb);
                     for (int c = 0; c < NB; ++c) El[c] += Ft * illum_band(rgb, c) * ct / ls.pdf;
                 } else {
                     for (int c = 0; c < NB; ++c) El[c] += Ft * L.Lemit[c] * ct / ls.pdf;
@@ -519,7 +572,7 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     const float lu0 = van_der_corput(nidx, sl0), lu1 = sobol2(nidx, sl1);
     const LightSampleOut ls = L.kind ? sample_infinite(L, fr.p, reps, lu0, lu1) : sample_light(L, fr.p, reps, lu0, lu1);
     float lightPdf = ls.pdf;
-    float4 st = make_float4(lu0, lu1, 0.f, 0.f);
+    float4 st = make_float4(ls.ms, ls.mt, 0.f, 0.f);
     if (lightPdf > 0.f && ls.nonblack && ncomp > 0) {
         const V3 wi_l = to_local(fr, ls.wi);
         const Lobe f1 = bsdf_lobe(mat, dot(ls.wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);

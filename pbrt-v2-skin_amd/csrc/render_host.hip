@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "context.h"
+#include "envmap.h"
 #include "render.h"
 #include "spectral.h"
 
@@ -62,22 +63,36 @@ void Context::add_sphere_light(const float *c, float r, const float *Lemit, int 
 // CreateInfiniteLight + the InfiniteAreaLight ctor without a map (lights/infinite.cpp:66-90,
 // 180-188): texels[0] = L.ToRGBSpectrum(); Le and Sample_L convert map lookups back with
 // Spectrum(rgb, SPECTRUM_ILLUMINANT) on the device (render.hip).
-void Context::add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l) {
+void Context::add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l, int W, int H,
+                                 const float *texels) {
     if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_infinite_light: nsamples must be >= 1");
     if (scene_.lights.size() >= 254) throw Error(MPSS_ERR_INVALID, "add_infinite_light: at most 254 lights");
+    if (texels && (W < 1 || H < 1 || (int64_t)W * H > (int64_t)1 << 28))
+        throw Error(MPSS_ERR_INVALID, "add_infinite_light: bad map resolution");
     SceneLight l;
     l.kind = 1;
     l.center[0] = l.center[1] = l.center[2] = 0.f;
     l.radius = 0.f;
     memcpy(l.Lemit, L, sizeof(l.Lemit));
-    spectrum_to_rgb(L, l.rgb);
+    float rgb[3];
+    spectrum_to_rgb(L, rgb);  // L.ToRGBSpectrum()
+    if (texels) {             // texels[i] *= L.ToRGBSpectrum()
+        l.map_w = W;
+        l.map_h = H;
+        l.map.resize((size_t)W * H * 3);
+        for (size_t i = 0; i < (size_t)W * H; ++i)
+            for (int k = 0; k < 3; ++k) l.map[3 * i + k] = texels[3 * i + k] * rgb[k];
+    } else {
+        l.map_w = l.map_h = 1;
+        l.map.assign(rgb, rgb + 3);
+    }
     for (int r = 0; r < 3; ++r)
         for (int k = 0; k < 3; ++k) {
             l.l2w[3 * r + k] = l2w[4 * r + k];
             l.w2l[3 * r + k] = w2l[4 * r + k];
         }
     l.nsamples = cfg_.quick_render ? std::max(1, nsamples / 4) : nsamples;  // CreateInfiniteLight
-    scene_.lights.push_back(l);
+    scene_.lights.push_back(std::move(l));
     scene_dirty_ = true;
 }
 
@@ -133,6 +148,13 @@ void Context::upload_scene() {
     }
     d_meshes_.upload(rm.data(), rm.size());
     std::vector<RenderLight> rl;
+    d_envmaps_.clear();
+    // every light's map pointers address valid memory (a 1x1 zero map for area lights), so no
+    // load the compiler hoists out of a kind test can fault
+    if (!d_zero_map_.ptr) {
+        const float z[16] = {};
+        d_zero_map_.upload(z, 16);
+    }
     for (const SceneLight &l : scene_.lights) {
         RenderLight r{};
         r.s.c = V3{l.center[0], l.center[1], l.center[2]};
@@ -143,16 +165,36 @@ void Context::upload_scene() {
         r.s.area = r.s.phi_max * l.radius * (l.radius - -l.radius);  // Sphere::Area
         memcpy(r.Lemit, l.Lemit, sizeof(r.Lemit));
         r.kind = l.kind;
-        if (l.kind == 1) {
-            memcpy(r.rgb, l.rgb, sizeof(r.rgb));
+        r.tw = r.th = r.nu = r.nv = 1;
+        r.tex = r.func = r.cdf = r.rint = r.mcdf = d_zero_map_.ptr;
+        if (l.kind == 1) {  // radiance MIPMap level 0 + Distribution2D, one device block per light
             memcpy(r.l2w, l.l2w, sizeof(r.l2w));
             memcpy(r.w2l, l.w2l, sizeof(r.w2l));
-            // img[0] = radianceMap->Lookup(0, 0, 1).y() * sinf(M_PI * 0.5f): the texel's y() times 1
-            const float f = ((0.212671f * l.rgb[0] + 0.715160f * l.rgb[1]) + 0.072169f * l.rgb[2]) *
-                            m_sin(kPiF * (0.5f / 1.f));
-            r.map_pdf_sample = (f / f) * (f / f);
-            const float ff = f * f;
-            r.map_pdf_eval = ff == 0.f ? 0.f : ff / ff;
+            const EnvMap em = build_envmap(l.map_w, l.map_h, l.map.data());
+            std::vector<float> blk;
+            const size_t o_tex = blk.size();
+            blk.insert(blk.end(), em.tex.begin(), em.tex.end());
+            const size_t o_func = blk.size();
+            blk.insert(blk.end(), em.func.begin(), em.func.end());
+            const size_t o_cdf = blk.size();
+            blk.insert(blk.end(), em.cdf.begin(), em.cdf.end());
+            const size_t o_rint = blk.size();
+            blk.insert(blk.end(), em.row_int.begin(), em.row_int.end());
+            const size_t o_mcdf = blk.size();
+            blk.insert(blk.end(), em.mcdf.begin(), em.mcdf.end());
+            d_envmaps_.emplace_back(new DevBuf<float>());
+            DevBuf<float> &db = *d_envmaps_.back();
+            db.upload(blk.data(), blk.size());
+            r.tw = em.w0;
+            r.th = em.h0;
+            r.nu = em.nu;
+            r.nv = em.nv;
+            r.tex = db.ptr + o_tex;
+            r.func = db.ptr + o_func;
+            r.cdf = db.ptr + o_cdf;
+            r.rint = db.ptr + o_rint;
+            r.mcdf = db.ptr + o_mcdf;
+            r.mint = em.mint;
             r.s.r = 0.f;
         }
         r.nsamples_pow2 = round_up_pow2(l.nsamples);

@@ -28,8 +28,9 @@ struct SceneLight {
     int kind = 0;
     float center[3], radius;
     float Lemit[NB];      // kind 0: DiffuseAreaLight::Lemit
-    float rgb[3];         // kind 1: the map's one texel, (L * scale).ToRGBSpectrum()
     float l2w[9], w2l[9]; // kind 1: LightToWorld / WorldToLight (upper 3x3, row-major)
+    int map_w = 0, map_h = 0;
+    std::vector<float> map;  // kind 1: texels * (L * scale).ToRGBSpectrum(), or 1x1 without a map
     int nsamples;
 };
 

@@ -86,6 +86,7 @@ _sig("mpss_mo_batch", C.c_int, [vp, u32, u32, vp, vp, vp, vp])
 _sig("mpss_add_mesh", C.c_int, [vp, u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32])
 _sig("mpss_add_sphere_light", C.c_int, [vp, f32p, C.c_float, f32p, C.c_int])
 _sig("mpss_add_infinite_light", C.c_int, [vp, f32p, C.c_int, f32p, f32p])
+_sig("mpss_add_infinite_light_map", C.c_int, [vp, f32p, C.c_int, f32p, f32p, C.c_int, C.c_int, f32p])
 _sig("mpss_set_camera", C.c_int, [vp, f32p, f32p, C.c_int, C.c_int])
 _sig("mpss_set_surface_points", C.c_int, [vp, u32, vp])
 _sig("mpss_get_surface_points", C.c_int, [vp, vp, u32p])
@@ -292,13 +293,20 @@ class Context:
         check(_lib.mpss_add_sphere_light(self.h, np.ascontiguousarray(center, np.float32), radius,
                                          np.ascontiguousarray(Lemit, np.float32), nsamples))
 
-    def add_infinite_light(self, L, nsamples=1, light_to_world=None, world_to_light=None):
-        """LightSource "infinite" without a map; L = the 30-band L * scale (CreateInfiniteLight)."""
+    def add_infinite_light(self, L, nsamples=1, light_to_world=None, world_to_light=None, texels=None):
+        """LightSource "infinite"; L = the 30-band L * scale (CreateInfiniteLight); texels = the
+        map as an (H, W, 3) float array (ReadImage's RGB), or None for a constant light."""
         l2w = np.eye(4, dtype=np.float32) if light_to_world is None else light_to_world
         w2l = np.linalg.inv(np.asarray(l2w, np.float64)) if world_to_light is None else world_to_light
-        check(_lib.mpss_add_infinite_light(self.h, np.ascontiguousarray(L, np.float32), nsamples,
-                                           np.ascontiguousarray(l2w, np.float32),
-                                           np.ascontiguousarray(w2l, np.float32)))
+        args = (self.h, np.ascontiguousarray(L, np.float32), nsamples, np.ascontiguousarray(l2w, np.float32),
+                np.ascontiguousarray(w2l, np.float32))
+        if texels is None:
+            check(_lib.mpss_add_infinite_light(*args))
+        else:
+            tex = np.ascontiguousarray(texels, np.float32)
+            if tex.ndim != 3 or tex.shape[2] != 3:
+                raise ValueError("texels must be (height, width, 3)")
+            check(_lib.mpss_add_infinite_light_map(*args, tex.shape[1], tex.shape[0], tex))
 
     def set_camera(self, raster_to_camera, camera_to_world, xres, yres):
         check(_lib.mpss_set_camera(self.h, np.ascontiguousarray(raster_to_camera, np.float32),

@@ -9,7 +9,7 @@ for the directives scenes/skin.pbrt and its relatives contain:
   minsampledistance, mix, showirradiancepoints, incenter), WorldBegin/WorldEnd,
   AttributeBegin/End, TransformBegin/End, Translate, Rotate, Scale, Identity,
   Texture "constant", Material "layeredskin", AreaLightSource "area", LightSource "infinite"
-  (constant L * scale, nsamples; no "mapname"), Shape "sphere" (as an area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
+  (L, scale, nsamples, mapname: .exr / .pfm / .tga via mpss.imageio), Shape "sphere" (as an area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
   package's stand-in for huge inline arrays, see tools/make_scene.py), Include.
 
 Transforms follow core/transform.cpp (Translate, Scale, Rotate, LookAt, Perspective) evaluated in
@@ -263,10 +263,10 @@ def load(path, **override):
                 elif d == "LightSource":
                     if cls != "infinite":
                         raise ValueError("LightSource %r is outside this path" % cls)
-                    if ps.find("mapname"):
-                        raise ValueError("infinite light maps (\"mapname\") are not supported; only a "
-                                         "constant L (DESIGN.md)")
-                    sc.lights.append(dict(kind="infinite", L=_rgb3(ps.find("L", [1.0])),
+                    mapname = ps.one("mapname", "")
+                    if mapname:  # FindOneFilename: relative to the scene file's directory
+                        mapname = mapname if os.path.isabs(mapname) else os.path.join(base, mapname)
+                    sc.lights.append(dict(kind="infinite", L=_rgb3(ps.find("L", [1.0])), mapname=mapname or None,
                                           scale=_rgb3(ps.find("scale", [1.0])), nsamples=int(ps.one("nsamples", 1)),
                                           l2w=ctm.astype(np.float32), w2l=np.linalg.inv(ctm).astype(np.float32)))
                 elif d == "Shape":
@@ -368,6 +368,17 @@ def infinite_L(li):
     return (mpss.host_from_rgb(li["L"]) * mpss.host_from_rgb(li["scale"])).astype(np.float32)
 
 
+def infinite_texels(li):
+    """The light's map as ReadImage returns it (mpss.imageio), or None without "mapname";
+    "texels" in the dict (an (H, W, 3) array) overrides the file."""
+    if li.get("texels") is not None:
+        return np.ascontiguousarray(li["texels"], np.float32)
+    if not li.get("mapname"):
+        return None
+    from mpss import imageio
+    return imageio.read_image(li["mapname"])
+
+
 def build_context(sc, **cfg_kw):
     """Create an mpss.Context holding the scene (materials, meshes, lights, camera)."""
     import mpss
@@ -384,7 +395,7 @@ def build_context(sc, **cfg_kw):
                      uv=me["uv"], reverse=me["reverse"])
     for li in sc.lights:
         if li.get("kind") == "infinite":
-            ctx.add_infinite_light(infinite_L(li), li["nsamples"], li["l2w"], li["w2l"])
+            ctx.add_infinite_light(infinite_L(li), li["nsamples"], li["l2w"], li["w2l"], texels=infinite_texels(li))
         else:
             ctx.add_sphere_light(li["center"], li["radius"], mpss.host_from_rgb(li["L"]), li["nsamples"])
     r2c, c2w = sc.raster_to_camera()

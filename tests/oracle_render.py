@@ -34,7 +34,7 @@ def _lib():
     L.o_scene_add_sphere_light.restype = C.c_int
     L.o_scene_add_sphere_light.argtypes = [vp, f32p, C.c_float, f32p, C.c_int]
     L.o_scene_add_infinite_light.restype = C.c_int
-    L.o_scene_add_infinite_light.argtypes = [vp, f32p, C.c_int, f32p, f32p]
+    L.o_scene_add_infinite_light.argtypes = [vp, f32p, C.c_int, f32p, f32p, C.c_int, C.c_int, vp]
     L.o_tessellate.restype = C.c_long
     L.o_tessellate.argtypes = [vp, C.c_float, C.c_int, vp, C.c_long]
     L.o_irradiance.argtypes = [vp, C.c_int, vp, C.c_uint32, C.c_int, f32p]
@@ -103,8 +103,13 @@ class OracleScene:
             ns = li["nsamples"] if not cfg.quick_render else max(1, li["nsamples"] // 4)
             if li.get("kind") == "infinite":
                 Lsc = (oracle_lib.from_rgb(li["L"]) * oracle_lib.from_rgb(li["scale"])).astype(np.float32)
-                L.o_scene_add_infinite_light(self.h, Lsc, ns, np.ascontiguousarray(li["l2w"], np.float32),
-                                             np.ascontiguousarray(li["w2l"], np.float32))
+                from mpss import pbrtscene
+                tex = pbrtscene.infinite_texels(li)
+                H, W = (0, 0) if tex is None else tex.shape[:2]
+                rc = L.o_scene_add_infinite_light(self.h, Lsc, ns, np.ascontiguousarray(li["l2w"], np.float32),
+                                                  np.ascontiguousarray(li["w2l"], np.float32), W, H,
+                                                  None if tex is None else tex.ctypes.data)
+                assert rc >= 0
                 continue
             L.o_scene_add_sphere_light(self.h, np.ascontiguousarray(li["center"], np.float32), li["radius"],
                                        mpss.host_from_rgb(li["L"]), ns)

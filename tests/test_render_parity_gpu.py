@@ -147,11 +147,12 @@ def _sky_light(deg, axis, L=(0.3, 0.35, 0.45), scale=(2, 2, 2), ns=4):
 
 
 @pytest.mark.parametrize("scene,lights", [("tissue_sky.pbrt", None), ("skin.pbrt", "sky+area"),
-                                          ("skin.pbrt", "sky")])
+                                          ("skin.pbrt", "sky"), ("tissue.pbrt", "map+area"), ("skin.pbrt", "map")])
 def test_image_parity_infinite_light(mpss, oracle, scene, lights):
-    """LightSource "infinite" with a constant map (lights/infinite.cpp): Sample_L / Pdf for
-    irradiance and both MIS halves of EstimateDirect, Le for BSDF rays and camera rays that
-    escape; alone, and mixed with the sphere light in either order."""
+    """LightSource "infinite" (lights/infinite.cpp), constant or with a radiance map: Sample_L /
+    Pdf (Distribution2D) for irradiance and both MIS halves of EstimateDirect, Le (MIPMap
+    lookups) for BSDF rays and camera rays that escape; alone, and mixed with the sphere light
+    in either order."""
     import torch
     from mpss import pbrtscene
     sc = pbrtscene.load(os.path.join(ROOT, "scenes", scene), xres=48, yres=48, spp=4)
@@ -162,6 +163,16 @@ def test_image_parity_infinite_light(mpss, oracle, scene, lights):
         sc.lights = [sc.lights[0], _sky_light(40, [1, 1, 0], ns=2)]
     elif lights == "sky":
         sc.lights = [_sky_light(-70, [0, 1, 1], L=(0.8, 0.6, 0.5), ns=8)]
+    elif lights == "map+area":  # a non-power-of-two map (Lanczos-resampled MIPMap) with a sun
+        from test_infinite_light import envmap_texels
+        sky = _sky_light(100, [1, 0, 0], L=(1, 1, 1), scale=(3, 3, 3), ns=4)
+        sky["texels"] = envmap_texels(37, 21, seed=3)
+        sc.lights = [sc.lights[0], sky]
+    elif lights == "map":
+        from test_infinite_light import envmap_texels
+        sky = _sky_light(-60, [0, 1, 0], L=(1, 1, 1), ns=4)
+        sky["texels"] = envmap_texels(64, 32, seed=4)
+        sc.lights = [sky]
     ctx = pbrtscene.build_context(sc)
     ctx.preprocess(seed=6)
     o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
