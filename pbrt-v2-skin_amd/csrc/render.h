@@ -105,6 +105,7 @@ struct DirectTerms;
 __global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits, int ns_max,
                                     DirectTerms *terms, float4 *inf_st);
 __global__ void shade_nolight_kernel(RenderScene sc, SampleRecs rec, int max_hits);
+template <bool kInf>
 __global__ void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
                                       const DirectTerms *terms, const float4 *inf_st);
 // Li assembly per slot (L = Le + SSS + Ld, sample filter, ToXYZ), then the box-filtered film.

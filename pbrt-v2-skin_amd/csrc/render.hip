@@ -254,7 +254,7 @@ __device__ __forceinline__ float illum_band(const float rgb[3], int c) {
     return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
 }
 
-__device__ __forceinline__ bool inf_nonblack(const RenderLight &L, float s, float t) {  // !Le.IsBlack()
+__device__ __noinline__ bool inf_nonblack(const RenderLight &L, float s, float t) {  // !Le.IsBlack()
     float rgb[3];
     inf_lookup(L, s, t, rgb);
     for (int c = 0; c < NB; ++c)
@@ -263,7 +263,7 @@ __device__ __forceinline__ bool inf_nonblack(const RenderLight &L, float s, floa
 }
 
 // InfiniteAreaLight::Le (infinite.cpp:115-120): map coordinates of a world direction
-__device__ __forceinline__ void inf_coords(const RenderLight &L, V3 d, float &s, float &t) {
+__device__ __noinline__ void inf_coords(const RenderLight &L, V3 d, float &s, float &t) {
     const V3 wh = normalize(xform3(L.w2l, d));
     float ph = m_atan2(wh.y, wh.x);  // SphericalPhi
     ph = ph < 0.f ? ph + 2.f * kPiF : ph;
@@ -275,7 +275,7 @@ __device__ __forceinline__ void inf_coords(const RenderLight &L, V3 d, float &s,
 // InfiniteAreaLight::Sample_L (infinite.cpp:195-218): Distribution2D::SampleContinuous
 // (montecarlo.h:154-161) picks a row with the marginal, then a column in that row;
 // VisibilityTester::SetRay (light.h:93-96). (ms, mt) = uv, where Ls is looked up.
-__device__ __forceinline__ LightSampleOut sample_infinite(const RenderLight &L, V3 p, float peps, float u0, float u1) {
+__device__ __noinline__ LightSampleOut sample_infinite(const RenderLight &L, V3 p, float peps, float u0, float u1) {
     LightSampleOut r;
     float pdf0, pdf1;
     int v, col;
@@ -305,7 +305,7 @@ __device__ __forceinline__ LightSampleOut sample_infinite(const RenderLight &L, 
 }
 
 // InfiniteAreaLight::Pdf (infinite.cpp:222-232) with Distribution2D::Pdf (montecarlo.h:162-170)
-__device__ __forceinline__ float infinite_pdf(const RenderLight &L, V3 w) {
+__device__ __noinline__ float infinite_pdf(const RenderLight &L, V3 w) {
     const V3 wi = xform3(L.w2l, w);
     const float z = wi.z < -1.f ? -1.f : (wi.z > 1.f ? 1.f : wi.z);
     const float theta = m_acos(z);
@@ -464,6 +464,14 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
 // (Microfacet::f) with scalar D, G, F, den, so no lane carries a 30-band spectrum.
 // One lobe value of the layer-0 BSDF for a direction pair (BSDF::f, reflection.cpp:765-779):
 // kind 1 = Microfacet (R * D * G * F / den), kind 2 = MicrofacetTransmission (T * s * (1 - F)).
+// The transmission lobe and the infinite light run only for the materials / scenes that have
+// them; they are called out of line so the common path keeps its code small (I-cache).
+__device__ __noinline__ MtTerms mt_terms_ool(const Microfacet &m, V3 wo, V3 wi) { return mt_terms(m, wo, wi); }
+__device__ __noinline__ float mt_pdf_ool(const Microfacet &m, V3 wo, V3 wi) { return mt_pdf(m, wo, wi); }
+__device__ __noinline__ void mt_sample_ool(const Microfacet &m, V3 wo, float u1, float u2, V3 &wi, float &pdf) {
+    mt_sample(m, wo, u1, u2, wi, pdf);
+}
+
 struct Lobe {
     uint32_t kind;
     float a, b, c, d;
@@ -477,7 +485,7 @@ __device__ __forceinline__ Lobe bsdf_lobe(const RenderMaterial &mat, bool refl, 
             if (!t.zero) L = Lobe{1u, t.D, t.G, t.F, t.den};
         }
     } else if (mat.has_trans) {  // ... or BTDFs only
-        const MtTerms t = mt_terms(mat.mf, wo_l, wi_l);
+        const MtTerms t = mt_terms_ool(mat.mf, wo_l, wi_l);
         if (!t.zero) L = Lobe{2u, t.s, t.F, 0.f, 1.f};
     }
     return L;
@@ -500,7 +508,7 @@ __device__ __forceinline__ float bsdf_pdf(const RenderMaterial &mat, V3 wo_l, V3
     if (n == 0) return 0.f;
     float pdf = 0.f;
     if (mat.has_refl) pdf += microfacet_pdf(mat.mf, wo_l, wi_l);
-    if (mat.has_trans) pdf += mt_pdf(mat.mf, wo_l, wi_l);
+    if (mat.has_trans) pdf += mt_pdf_ool(mat.mf, wo_l, wi_l);
     return pdf / (float)n;
 }
 
@@ -591,13 +599,13 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
         V3 wi_l;
         float bsdfPdf;
         if (pick_t)
-            mt_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+            mt_sample_ool(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
         else
             beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
         if (bsdfPdf != 0.f) {
             const V3 wi = to_world(fr, wi_l);
             if (ncomp > 1) {
-                bsdfPdf += pick_t ? microfacet_pdf(mat.mf, wo_l, wi_l) : mt_pdf(mat.mf, wo_l, wi_l);
+                bsdfPdf += pick_t ? microfacet_pdf(mat.mf, wo_l, wi_l) : mt_pdf_ool(mat.mf, wo_l, wi_l);
                 bsdfPdf /= (float)ncomp;
             }
             const Lobe f2 = bsdf_lobe(mat, dot(wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
@@ -643,7 +651,11 @@ __global__ __launch_bounds__(256) void shade_nolight_kernel(RenderScene sc, Samp
 }
 
 // ld[c] = sum over lights of (sum over j of (0 + light term + BSDF term)) / ns, band by band in
-// the order UniformSampleAllLights accumulates (Ld += EstimateDirect; L += Ld / nSamples).
+// the order UniformSampleAllLights accumulates (Ld += EstimateDirect; L += Ld / nSamples). Each
+// light sample's record is read once and added to all 30 per-band accumulators (registers);
+// every band sees exactly the reference's sequence of float operations. kInf: the scene has
+// infinite lights, whose radiance depends on each term's direction (map coordinates in inf_st).
+template <bool kInf>
 __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
                                                              const DirectTerms *__restrict__ terms,
                                                              const float4 *__restrict__ inf_st) {
@@ -652,38 +664,48 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
     if (slot >= nhits || slot >= max_hits) return;
     if (rec.hit_s[slot] & 0x40000000u) return;
     const RenderMaterial &mat = sc.materials[(rec.hit_s[slot] >> REC_MAT_SHIFT) & 0xffu];
-    const DirectTerms *t = terms + (size_t)slot * sc.nlights * ns_max;
-    float *row = rec.ld + (size_t)slot * ROW;
-    for (int c = 0; c < NB; ++c) {
-        float ld = 0.f;
-        for (int l = 0; l < sc.nlights; ++l) {
-            const RenderLight &L = sc.lights[l];
-            const int ns = L.nsamples_round;
-            float Ld = 0.f;
-            for (int j = 0; j < ns; ++j) {
-                const DirectTerms &e = t[l * ns_max + j];
-                if (!e.l1.kind && !e.l2.kind) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
-                float Li1 = L.Lemit[c], Li2 = L.Lemit[c];
-                if (L.kind) {  // Spectrum(map lookup, SPECTRUM_ILLUMINANT) at each term's direction
-                    const float4 st = inf_st[(size_t)slot * sc.nlights * ns_max + l * ns_max + j];
-                    float rgb[3];
-                    inf_lookup(L, st.x, st.y, rgb);
-                    Li1 = illum_band(rgb, c);
-                    inf_lookup(L, st.z, st.w, rgb);
-                    Li2 = illum_band(rgb, c);
-                }
+    const size_t base = (size_t)slot * sc.nlights * ns_max;
+    float ld[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) ld[c] = 0.f;
+    for (int l = 0; l < sc.nlights; ++l) {
+        const RenderLight &L = sc.lights[l];
+        const int ns = L.nsamples_round;
+        float Ld[NB];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) Ld[c] = 0.f;
+        for (int j = 0; j < ns; ++j) {
+            const DirectTerms e = terms[base + l * ns_max + j];
+            if (!e.l1.kind && !e.l2.kind) continue;  // ed = 0 and Ld += 0 changes nothing (Ld is never -0)
+            float rgb1[3], rgb2[3];
+            const bool inf = kInf && L.kind;
+            if (inf) {  // Spectrum(map lookup, SPECTRUM_ILLUMINANT) at each term's direction
+                const float4 st = inf_st[base + l * ns_max + j];
+                inf_lookup(L, st.x, st.y, rgb1);
+                inf_lookup(L, st.z, st.w, rgb2);
+            }
+#pragma unroll
+            for (int c = 0; c < NB; ++c) {
+                const float Li1 = inf ? illum_band(rgb1, c) : L.Lemit[c];
+                const float Li2 = inf ? illum_band(rgb2, c) : L.Lemit[c];
                 float ed = 0.f;
                 if (e.l1.kind) ed += lobe_value(mat, e.l1, c) * Li1 * e.k1;
                 if (e.l2.kind) ed += lobe_value(mat, e.l2, c) * Li2 * e.adn * e.w2 / e.pdf2;
-                Ld += ed;
+                Ld[c] += ed;
             }
-            ld += Ld / (float)ns;
         }
-        row[c] = ld;
+#pragma unroll
+        for (int c = 0; c < NB; ++c) ld[c] += Ld[c] / (float)ns;
     }
-    row[30] = 0.f;
-    row[31] = 0.f;
+    float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) row[k] = make_float4(ld[4 * k], ld[4 * k + 1], ld[4 * k + 2], ld[4 * k + 3]);
+    row[7] = make_float4(ld[28], ld[29], 0.f, 0.f);
 }
+template __global__ void direct_combine_kernel<false>(RenderScene, SampleRecs, int, int, const DirectTerms *,
+                                                      const float4 *);
+template __global__ void direct_combine_kernel<true>(RenderScene, SampleRecs, int, int, const DirectTerms *,
+                                                     const float4 *);
 
 // ------------------------------------------------------------------ film
 // Li of one camera sample with radiance (MultipoleSubsurfaceIntegrator::Li,

@@ -429,8 +429,14 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             if (!scene_.lights.empty()) {
                 hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream,
                                    sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
-                hipLaunchKernelGGL(direct_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                                   sc, rec, (int)total, ns_max, (const DirectTerms *)terms, (const float4 *)inf_st);
+                if (sc.n_infinite > 0)
+                    hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                                       stream, sc, rec, (int)total, ns_max, (const DirectTerms *)terms,
+                                       (const float4 *)inf_st);
+                else
+                    hipLaunchKernelGGL(direct_combine_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                                       0, stream, sc, rec, (int)total, ns_max, (const DirectTerms *)terms,
+                                       (const float4 *)nullptr);
             } else {
                 hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                                    sc, rec, (int)total);
