@@ -185,11 +185,12 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         const bool any_open = __builtin_amdgcn_ballot_w64(open) != 0;
         if (h.leaf_first >= 0) {
             if (any_open) {
+                // the leaf's non-black points only (DeviceOctree::upload puts them first, h.pad)
                 float lacc[4] = {0.f, 0.f, 0.f, 0.f};
-                for (int i = 0; i < h.leaf_count; ++i) {
+                const int live = (int)h.pad;
+                for (int i = 0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
                     const float4 ph = a.pt_hdr[kp];
-                    if (__builtin_signbit(ph.w)) continue;  // E is black
                     if (!open) continue;
                     if (COUNT) ++k_pts;
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;

@@ -307,11 +307,32 @@ void launch_t(const MoArgs &a, bool count, hipStream_t s) {
 
 }  // namespace
 
+// The device copy moves each leaf's black points (E == 0: every kernel skips them, they add
+// nothing) behind its other points, keeping the others' order, and records the count of the
+// rest in NodeHdr::pad, so the sharded gather's leaf loop needs no per-point test.
 void DeviceOctree::upload(const FlatOctree &t) {
-    nodes.upload(t.hdr.data(), t.hdr.size());
+    std::vector<NodeHdr> hdr = t.hdr;
+    std::vector<float> ph(t.pt_hdr.size()), pe(t.pt_e.size());
+    for (NodeHdr &h : hdr) {
+        h.pad = 0;
+        if (h.leaf_first < 0) continue;
+        int o = h.leaf_first;
+        for (int pass = 0; pass < 2; ++pass)
+            for (int i = 0; i < h.leaf_count; ++i) {
+                const size_t k = (size_t)h.leaf_first + i;
+                const bool blk = std::signbit(t.pt_hdr[4 * k + 3]);
+                if (blk != (pass == 1)) continue;
+                memcpy(&ph[4 * (size_t)o], &t.pt_hdr[4 * k], 4 * sizeof(float));
+                memcpy(&pe[(size_t)o * ROW], &t.pt_e[k * ROW], ROW * sizeof(float));
+                ++o;
+                if (pass == 0) ++h.pad;
+            }
+    }
+    nodes.upload(hdr.data(), hdr.size());
     node_et.upload(t.node_et.data(), t.node_et.size());
-    pt_hdr.upload(reinterpret_cast<const float4 *>(t.pt_hdr.data()), t.pt_hdr.size() / 4);
-    pt_e.upload(t.pt_e.data(), t.pt_e.size());
+    pt_hdr.upload(reinterpret_cast<const float4 *>(ph.data()), ph.size() / 4);
+    pt_e.upload(pe.data(), pe.size());
+    band_valid = false;
     n_nodes = (int)t.hdr.size();
     n_points = (int)t.pt_index.size();
     max_depth = t.max_depth;
