@@ -5,12 +5,14 @@ MultipoleSubsurfaceIntegrator + LayeredSkin; SamplerRenderer::Render's task loop
 samplerrenderer.cpp:177-236): every camera sample is traced, shaded (direct lighting + the
 Mo() octree gather) and splatted into the film. Frames are cut into 128x128 tiles dealt to
 ranks round-robin; rank 0 collects every rank's film tiles with one RCCL gather per step.
-Weak scaling: at N GPUs a step renders N frames (different sampler seeds).
+Weak scaling: at N GPUs a step renders N frames (different sampler seeds). --config c3 / c5
+run BASELINE.json's 8-GPU configs instead (one frame per step split over the GPUs: strong
+scaling); they are reference points, the driver's bench line is C2.
 
 Preprocess (tessellation, irradiance kernel, octree build) runs once before timing and is
 reported separately, as SURVEY.md §8d prescribes.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -31,14 +33,30 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 REC_HDR_BYTES = 16
 
 
+# BASELINE.json configs this bench runs: (label, resolution, spp, default scaling, mesh subdivision
+# levels). C5's "synthetic 4M-triangle head mesh + 2M irradiance SurfacePoints": head.pbrt
+# subdivided 1:4 four times (4.06 M triangles, the same surface) lit and shaded as skin.pbrt,
+# with the 2.2 M points of the original mesh's tessellation handed over as a pointsfile would be.
+CONFIGS = {
+    "c2": ("C2: skin.pbrt 1024x1024 64 spp", 1024, 64, "weak", 0),
+    "c3": ("C3: skin.pbrt 2048x2048 256 spp", 2048, 256, "strong", 0),
+    "c5": ("C5: synthetic 4M-triangle head + 2.2M SurfacePoints, 4096x4096 512 spp", 4096, 512, "strong", 4),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
+                    help="BASELINE.json config: c2 (default; the metric's), c3 or c5 (8-GPU configs, strong scaling)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="weak: one frame per GPU per step; strong: one frame per step split over the GPUs "
+                         "(default: the config's)")
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"))
-    ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--tile", type=int, default=128)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
@@ -68,17 +86,27 @@ def main():
     import mpss
     from mpss import pbrtscene, tiles as tl
 
-    sc = pbrtscene.load(a.scene, xres=a.res, yres=a.res, spp=a.spp)
+    label, res, spp, scaling, subdiv = CONFIGS[a.config]
+    res = a.res or res
+    spp = a.spp or spp
+    scaling = a.scaling or scaling
+    sc = pbrtscene.load(a.scene, xres=res, yres=res, spp=spp)
+    pts = None
+    if subdiv:
+        pts = pbrtscene.mesh_points(sc)
+        sc.meshes = [pbrtscene.subdivide_mesh(me, subdiv) for me in sc.meshes]
     t0 = time.perf_counter()
     ctx = pbrtscene.build_context(sc, device=local)
     t_materials = time.perf_counter() - t0
+    if pts is not None:
+        ctx.set_surface_points(pts)
     t0 = time.perf_counter()
     ctx.preprocess(seed=1)
     torch.cuda.synchronize()
     t_pre = time.perf_counter() - t0
     n_points = ctx.octree_info()["n_points"] if ctx.surface_points().size else 0
 
-    frames = world                     # weak scaling: one frame's worth of work per GPU
+    frames = world if scaling == "weak" else 1  # weak: one frame's worth of work per GPU
     T = a.tile
     tiles = tl.tile_grid(sc.xres, sc.yres, T)
     items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
@@ -143,7 +171,8 @@ def main():
                 "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
                 "dominant_kernel": dom,
                 "kernel_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in kern.items()}}
-    pt = pmc_traffic(a.pmc_json, shade_launch_ms)
+    # the committed PMC summaries are of the C2 command; other configs report traffic only with --pmc-json
+    pt = pmc_traffic(a.pmc_json, shade_launch_ms) if (a.config == "c2" or a.pmc_json) else None
     if pt:
         roofline["traffic"] = pt["traffic"]
         roofline["traffic_source"] = pt["source"] + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"
@@ -155,12 +184,16 @@ def main():
         cpu = cpu_baseline(sc, ctx, a)
 
     if rank == 0:
-        line = {"metric": "Msamples/s (skin.pbrt C2 pixel loop) + Mo()-gather HBM GB/s", "value": round(value, 3),
+        line = {"metric": "Msamples/s (%s pixel loop) + Mo()-gather HBM GB/s" % ("skin.pbrt C2" if a.config == "c2"
+                                                                                   else a.config.upper()),
+                "value": round(value, 3),
                 "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-                "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-                "vs_baseline": None, "dtype": "f32", "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh)",
-                "config": {"workload": "skin.pbrt %dx%d %d spp per GPU (C2), %dx%d tiles, RCCL film gather"
-                           % (sc.xres, sc.yres, sc.spp, T, T), "frames_per_step": frames,
+                "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
+                "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh%s)" % (", subdivided" if subdiv else ""),
+                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles, RCCL film gather"
+                           % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T),
+                           "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3),
                            "mo_gbs": round(mo_gbs, 1), "mo_sss_samples": cnt["sss_samples"],
@@ -218,7 +251,7 @@ def cpu_baseline(sc, ctx, a):
         import oracle_render
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "Msamples/s", "cores": None, "kind": "port", "sample": "unavailable: %s" % e}
-    return oracle_render.time_cpu_baseline(sc, ctx, a.spp, a.seed, a.cpu_baseline_seconds)
+    return oracle_render.time_cpu_baseline(sc, ctx, sc.spp, a.seed, a.cpu_baseline_seconds)
 
 
 if __name__ == "__main__":

@@ -350,6 +350,55 @@ def _shape(sc, cls, ps, ctm, state, base):
                           reverse=state["reverse"], material=sc.materials.index(mat)))
 
 
+def subdivide_mesh(me, levels):
+    """Midpoint (1:4) subdivision of a loaded trianglemesh dict, `levels` times: the same surface
+    with 4^levels as many triangles (BASELINE.json config C5's synthetic dense head). N and S are
+    interpolated and renormalised, uv interpolated; winding is kept."""
+    P = np.asarray(me["P"], np.float64)
+    idx = np.asarray(me["indices"], np.int64)
+    att = {k: (None if me.get(k) is None else np.asarray(me[k], np.float64)) for k in ("N", "S", "uv")}
+    for _ in range(levels):
+        a, b, c = idx[:, 0], idx[:, 1], idx[:, 2]
+        e = np.concatenate([np.stack([a, b], 1), np.stack([b, c], 1), np.stack([c, a], 1)])
+        key = np.sort(e, 1)
+        uniq, inv = np.unique(key, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+        base = len(P)
+        P = np.concatenate([P, 0.5 * (P[uniq[:, 0]] + P[uniq[:, 1]])])
+        for k, v in att.items():
+            if v is None:
+                continue
+            m = 0.5 * (v[uniq[:, 0]] + v[uniq[:, 1]])
+            if k in ("N", "S"):
+                m /= np.maximum(np.linalg.norm(m, axis=1, keepdims=True), 1e-20)
+            att[k] = np.concatenate([v, m])
+        nt = len(idx)
+        ab, bc, ca = base + inv[:nt], base + inv[nt:2 * nt], base + inv[2 * nt:]
+        idx = np.concatenate([np.stack([a, ab, ca], 1), np.stack([ab, b, bc], 1), np.stack([ca, bc, c], 1),
+                              np.stack([ab, bc, ca], 1)])
+    out = dict(me)
+    out["P"] = P.astype(np.float32)
+    out["indices"] = idx.astype(np.int32)
+    for k, v in att.items():
+        out[k] = None if v is None else v.astype(np.float32)
+    return out
+
+
+def mesh_points(sc, min_dist=None):
+    """SurfacePoints of a scene's meshes by the product's host tessellator (the pointsfile a
+    TessellateSurfacePointsRenderer pass would write), e.g. to pair a subdivided mesh with the
+    points of the original surface."""
+    import mpss
+    md = float(sc.integrator.get("minsampledistance", 0.25)) if min_dist is None else min_dist
+    parts = []
+    for me in sc.meshes:
+        det = np.linalg.det(np.asarray(me["o2w"], np.float64)[:3, :3])
+        parts.append(mpss.host_tessellate(me["P"], me["indices"], me["o2w"], me["w2o"], md, N=me["N"], S=me["S"],
+                                          uv=me["uv"], flip=bool(me["reverse"]) ^ bool(det < 0),
+                                          material=me["material"]))
+    return np.concatenate(parts)
+
+
 def integrator_config(sc, **kw):
     """mpss_config from the SurfaceIntegrator line (CreateMultipoleSubsurfaceIntegrator)."""
     it = sc.integrator
