@@ -67,6 +67,8 @@ typedef struct {
     int64_t max_batch_samples; /* camera samples per render batch; the workspace is sized for the
                                   worst case (every sample a hit): ~280 B/sample, 4.7 GB at the
                                   default 1 << 24 */
+    int use_poisson_point_finder; /* "usepoissonpointfinder" = false: SurfacePoints by random-walk
+                                  dart throwing (FindPoissonPointDistribution) instead of tessellation */
 } mpss_config;
 
 void mpss_config_defaults(mpss_config *cfg);

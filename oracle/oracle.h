@@ -110,6 +110,10 @@ int o_scene_add_sphere_light(o_scene *s, const float *c, float r, const float *L
 int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const float *l2w, const float *w2l, int W,
                                int H, const float *texels);
 
+/* FindPoissonPointDistribution with one task (replay-mode random numbers); returns the number of
+ * points written to out (<= cap), -1 if cap is too small, -2 if no BSSRDF surface was found */
+long o_poisson_points(o_scene *s, float min_dist, int quick, uint32_t seed, o_surface_point *out, long cap);
+
 /* envmap.c: InfiniteAreaLight's radiance MIPMap level 0 and Distribution2D */
 typedef struct {
     int tw, th, nu, nv;

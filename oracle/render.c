@@ -1337,3 +1337,163 @@ void o_scene_free(o_scene *s) {
     if (s->octree) o_octree_free(s->octree);
     free(s);
 }
+
+/* ------------------------------------------------------------------ Poisson point finder
+ * FindPoissonPointDistribution -> SurfacePointsRenderer::Render (renderers/surfacepoints.cpp:
+ * 115-150) with one SurfacePointTask (:175-284). Paths are traced one after another and their
+ * candidates tested in path order (the reference tests a batch's candidates after tracing it;
+ * tracing never depends on the test, so the order of tests is the same), the give-up test
+ * after every 20000 paths. Random numbers: counter-based per (seed, path, draw), replay mode. */
+static float pu01(uint32_t seed, uint32_t path, uint32_t k) { return (float)(hash3(seed, path, k) >> 8) * 0x1p-24f; }
+static v3 ffwd(v3 n, v3 v) { return dot(n, v) < 0.f ? neg(n) : n; }
+static v3 sph_point(const o_light *L, v3 o, v3 d, float t) {
+    v3 ph = add(sub(o, L->c), mul(d, t));
+    if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * L->r;
+    return add(ph, L->c);
+}
+
+typedef struct { int64_t key; int first; } pcell;
+typedef struct {
+    pcell *tab; size_t mask; int *next; float md;
+} pgrid;
+static uint64_t pkey(int64_t x, int64_t y, int64_t z) {
+    return ((uint64_t)(x & 0x1fffff) << 42) | ((uint64_t)(y & 0x1fffff) << 21) | (uint64_t)(z & 0x1fffff);
+}
+static pcell *pfind(pgrid *g, uint64_t k, int insert) {
+    size_t h = (size_t)(mix32((uint32_t)k ^ mix32((uint32_t)(k >> 32)))) & g->mask;
+    for (;;) {
+        pcell *c = &g->tab[h];
+        if (c->first < 0) {
+            if (!insert) return NULL;
+            c->key = (int64_t)k;
+            return c;
+        }
+        if ((uint64_t)c->key == k) return c;
+        h = (h + 1) & g->mask;
+    }
+}
+
+long o_poisson_points(o_scene *s, float min_dist, int quick, uint32_t seed, o_surface_point *out, long cap) {
+    scene_prepare(s);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int mi = 0; mi < s->nmeshes; ++mi) {
+        const o_mesh *m = &s->meshes[mi];
+        for (int t = 0; t < 3 * m->nt; ++t)
+            for (int k = 0; k < 3; ++k) {
+                float v = m->P[3 * m->idx[t] + k];
+                lo[k] = fminf(lo[k], v);
+                hi[k] = fmaxf(hi[k], v);
+            }
+    }
+    for (int l = 0; l < s->nlights; ++l) {
+        const o_light *L = &s->lights[l];
+        if (L->kind) continue;
+        float c[3] = {L->c.x, L->c.y, L->c.z};
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fminf(lo[k], c[k] + -L->r);
+            hi[k] = fmaxf(hi[k], c[k] + L->r);
+        }
+    }
+    /* BBox::BoundingSphere, and the ReverseOrientation sphere there */
+    o_light bound;
+    memset(&bound, 0, sizeof(bound));
+    bound.c = mk(.5f * lo[0] + .5f * hi[0], .5f * lo[1] + .5f * hi[1], .5f * lo[2] + .5f * hi[2]);
+    int inside = bound.c.x >= lo[0] && bound.c.x <= hi[0] && bound.c.y >= lo[1] && bound.c.y <= hi[1] &&
+                 bound.c.z >= lo[2] && bound.c.z <= hi[2];
+    bound.r = inside ? len(sub(bound.c, mk(hi[0], hi[1], hi[2]))) : 0.f;
+    bound.phimax = (PI_F / 180.f) * 360.f;
+    bound.thetamin = facos(-1.f);
+    bound.thetamax = facos(1.f);
+    bound.area = bound.phimax * bound.r * (bound.r - -bound.r);
+    const v3 origin = xpoint(s->c2w, mk(0.f, 0.f, 0.f));
+    const uint32_t sd = mix32(seed * 37u + 0x5eed1u);
+    const int max_fails = quick ? (200 > 10 ? 200 : 10) : 2000;
+    const float md2 = min_dist * min_dist;
+    const float area = PI_F * (min_dist / 2.f) * (min_dist / 2.f);
+    pgrid g;
+    size_t tsz = 1;
+    while (tsz < 2 * (size_t)(cap > 0 ? cap : 1)) tsz <<= 1;
+    g.tab = (pcell *)malloc(tsz * sizeof(pcell));
+    for (size_t i = 0; i < tsz; ++i) g.tab[i].first = -1;
+    g.mask = tsz - 1;
+    g.next = (int *)malloc((size_t)(cap > 0 ? cap : 1) * sizeof(int));
+    long n = 0;
+    int fails = 0, done = 0;
+    for (uint32_t path = 0; !done; ++path) {
+        uint32_t k = 0;
+        float u1 = pu01(sd, path, k++), u2 = pu01(sd, path, k++);
+        v3 o = origin, d = sample_sphere_uniform(u1, u2);
+        float mint = 0.f;
+        for (int depth = 0; depth < 30 && !done; ++depth) {
+            hit_t h = intersect(s, o, d, mint, INFINITY);
+            v3 p, nn;
+            float eps;
+            int cand = 0;
+            o_surface_point sp;
+            if (h.tri == NO_HIT) {
+                float t;
+                v3 snn;
+                if (!sphere_hit(&bound, o, d, mint, INFINITY, &t, &snn)) break;
+                p = sph_point(&bound, o, d, t);
+                nn = ffwd(snn, neg(d));
+                eps = 5e-4f * t;
+            } else if (h.tri < 0) {
+                p = sph_point(&s->lights[-1 - h.tri], o, d, h.t);
+                nn = ffwd(h.lnn, neg(d));
+                eps = 5e-4f * h.t;
+            } else {
+                const int mi = s->tri_mesh[h.tri], lt = s->tri_local[h.tri];
+                const o_mesh *mesh = &s->meshes[mi];
+                p = add(o, mul(d, h.t));
+                frame_t fr = tri_frame(mesh, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
+                nn = ffwd(fr.ng, neg(d));
+                eps = 1e-3f * h.t;
+                if (depth >= 3) { /* every material on this path is LayeredSkin: GetBSSRDF != NULL */
+                    v3 sn = (!mesh->N && !mesh->S) ? nn : fr.nn;
+                    sp.p[0] = p.x; sp.p[1] = p.y; sp.p[2] = p.z;
+                    sp.n[0] = sn.x; sp.n[1] = sn.y; sp.n[2] = sn.z;
+                    sp.u = fr.u; sp.v = fr.v;
+                    sp.material = (uint32_t)mesh->material;
+                    sp.area = area;
+                    sp.ray_eps = eps;
+                    cand = 1;
+                }
+            }
+            if (cand) { /* PoissonCheck against every accepted point within a cell of p */
+                int64_t cx = (int64_t)floor((double)sp.p[0] / (double)min_dist);
+                int64_t cy = (int64_t)floor((double)sp.p[1] / (double)min_dist);
+                int64_t cz = (int64_t)floor((double)sp.p[2] / (double)min_dist);
+                int fail = 0;
+                for (int dz = -1; dz <= 1 && !fail; ++dz)
+                    for (int dy = -1; dy <= 1 && !fail; ++dy)
+                        for (int dx = -1; dx <= 1 && !fail; ++dx) {
+                            pcell *c = pfind(&g, pkey(cx + dx, cy + dy, cz + dz), 0);
+                            for (int q = c ? c->first : -1; q >= 0; q = g.next[q]) {
+                                float ex = out[q].p[0] - sp.p[0], ey = out[q].p[1] - sp.p[1], ez = out[q].p[2] - sp.p[2];
+                                if (ex * ex + ey * ey + ez * ez < md2) { fail = 1; break; }
+                            }
+                        }
+                if (fail) {
+                    if (++fails >= max_fails) done = 1;
+                } else {
+                    if (n >= cap) { free(g.tab); free(g.next); return -1; }
+                    fails = 0;
+                    pcell *c = pfind(&g, pkey(cx, cy, cz), 1);
+                    g.next[n] = c->first;
+                    c->first = (int)n;
+                    out[n++] = sp;
+                }
+            }
+            if (done) break;
+            u1 = pu01(sd, path, k++);
+            u2 = pu01(sd, path, k++);
+            d = ffwd(sample_sphere_uniform(u1, u2), nn);
+            o = p;
+            mint = eps;
+        }
+        if (!done && (path + 1) % 20000 == 0 && (long)(path + 1) > 50000 && n == 0) { done = 1; n = -2; }
+    }
+    free(g.tab);
+    free(g.next);
+    return n;
+}

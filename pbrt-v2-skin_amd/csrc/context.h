@@ -51,6 +51,8 @@ public:
     void set_camera(const float *r2c, const float *c2w, int xres, int yres);
     void set_surface_points(uint32_t n, const SurfacePoint *pts);
     void preprocess(uint32_t seed);
+    // FindPoissonPointDistribution (usepoissonpointfinder): fills points_ (render_host.hip)
+    void find_poisson_points(uint32_t seed);
     void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);
     const std::vector<SurfacePoint> &surface_points() const { return points_; }
     const std::vector<float> &irradiance() const { return irradiance_; }

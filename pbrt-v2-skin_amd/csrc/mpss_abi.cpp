@@ -41,7 +41,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 1; }
+int mpss_abi_version(void) { return 2; }  // 2: mpss_config.use_poisson_point_finder, infinite lights
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -59,6 +59,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->count_traversal = 0;
     c->profile_on_host = 0;
     c->max_batch_samples = (int64_t)1 << 24;
+    c->use_poisson_point_finder = 0;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {

@@ -92,6 +92,17 @@ struct SampleRecs {
     float4 *xyz;     // [hits] the sample's filtered XYZ (assemble_kernel)
 };
 
+// SurfacePointTask's random-walk paths (usepoissonpointfinder): one lane per path, candidates of
+// path i at out[i * kPoissonCand ...], their count in count[i] (render.hip).
+constexpr int kPoissonDepth = 30, kPoissonCand = kPoissonDepth - 3;
+struct PoissonWalk {
+    V3 origin;        // pCamera
+    SphereView bound; // the scene's bounding sphere (ReverseOrientation sphere at its centre)
+    uint32_t seed, path0;
+    int npaths;
+};
+__global__ void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint *out, int *count);
+
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, int n, uint32_t seed, float *E_out);
 struct BandPos {

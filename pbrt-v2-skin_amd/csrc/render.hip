@@ -382,6 +382,86 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
     for (int c = 0; c < NB; ++c) E_out[(size_t)i * NB + c] = E[c];
 }
 
+// ------------------------------------------------------------------ Poisson point finder
+// SurfacePointTask::Run's paths (renderers/surfacepoints.cpp:181-215): from pCamera in a
+// uniformly random direction, up to 30 rays; a ray that leaves the scene bounces off the inside
+// of the bounding sphere; hits of rays of depth >= 3 on a surface whose material has a BSSRDF
+// become candidate SurfacePoints (p, shading normal, u, v, material, area, rayEpsilon); each
+// next direction is a uniform sphere sample turned to the faceforwarded normal. Random numbers
+// are counter-based per (seed, path, draw) -- replay mode, like the render sampler.
+__device__ __forceinline__ float poisson_u01(uint32_t seed, uint32_t path, uint32_t k) {
+    return (float)(hash3(seed, path, k) >> 8) * 0x1p-24f;
+}
+__device__ __forceinline__ V3 sphere_hit_point(const SphereView &s, V3 o, V3 d, float t) {
+    V3 ph = (o - s.c) + d * t;  // object-space Ray::operator() of the translated sphere
+    if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * s.r;
+    return ph + s.c;
+}
+__device__ __forceinline__ V3 faceforward(V3 n, V3 v) { return dot(n, v) < 0.f ? -n : n; }
+
+__global__ __launch_bounds__(256) void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint *out,
+                                                           int *count) {
+    __shared__ int stk_all[kStack * 256];
+    int *stk = stk_all + threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= w.npaths) return;
+    const uint32_t path = w.path0 + (uint32_t)i;
+    uint32_t k = 0;
+    float u1 = poisson_u01(w.seed, path, k++), u2 = poisson_u01(w.seed, path, k++);
+    V3 o = w.origin, d = uniform_sample_sphere(u1, u2);
+    float mint = 0.f;
+    int n = 0;
+    SurfacePoint *mine = out + (size_t)i * kPoissonCand;
+    for (int depth = 0; depth < kPoissonDepth; ++depth) {
+        const Hit h = trace_closest(sc, o, d, mint, INFINITY, stk, 256);
+        V3 p, nn;
+        float eps;
+        if (h.tri == INT_MIN) {  // sphere.Intersect(ray, &isect): the bounding sphere
+            float t;
+            V3 snn;
+            if (!sphere_intersect(w.bound, o, d, mint, INFINITY, t, &snn)) break;
+            p = sphere_hit_point(w.bound, o, d, t);
+            nn = snn;
+            eps = 5e-4f * t;
+            nn = faceforward(nn, -d);
+        } else if (h.tri < 0) {  // an area light's sphere (its material has no BSSRDF)
+            p = sphere_hit_point(sc.lights[-1 - h.tri].s, o, d, h.t);
+            nn = faceforward(h.lnn, -d);
+            eps = 5e-4f * h.t;
+        } else {
+            const int mi = sc.tri_mesh[h.tri], lt = sc.tri_local[h.tri];
+            const RenderMesh &mesh = sc.meshes[mi];
+            p = o + d * h.t;
+            const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
+            nn = faceforward(fr.ng, -d);
+            eps = 1e-3f * h.t;
+            if (depth >= 3 && mesh.material < (uint32_t)sc.nmaterials && sc.materials[mesh.material].has_bssrdf) {
+                // dgs = dgShading (no bump map); without N and S the shading geometry is dg itself
+                const V3 sn = (!mesh.view.N && !mesh.view.S) ? nn : fr.nn;
+                SurfacePoint sp;
+                sp.p[0] = p.x;
+                sp.p[1] = p.y;
+                sp.p[2] = p.z;
+                sp.n[0] = sn.x;
+                sp.n[1] = sn.y;
+                sp.n[2] = sn.z;
+                sp.u = fr.u;
+                sp.v = fr.v;
+                sp.material = mesh.material;
+                sp.area = 0.f;  // pi (minDist / 2)^2, set by the host
+                sp.ray_eps = eps;
+                mine[n++] = sp;
+            }
+        }
+        u1 = poisson_u01(w.seed, path, k++);
+        u2 = poisson_u01(w.seed, path, k++);
+        d = faceforward(uniform_sample_sphere(u1, u2), nn);
+        o = p;
+        mint = eps;
+    }
+    count[i] = n;
+}
+
 // ------------------------------------------------------------------ camera rays (primary)
 // SamplerRendererTask::Run's per-sample head: image sample -> PerspectiveCamera::GenerateRay ->
 // Scene::Intersect. Surface hits are compacted (one atomic per wave, sample order kept inside

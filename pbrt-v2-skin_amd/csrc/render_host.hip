@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <unordered_map>
 
 #include "context.h"
 #include "envmap.h"
@@ -265,7 +266,12 @@ void Context::preprocess(uint32_t seed) {
         irradiance_.clear();
         return;
     }
-    if (!have_points_) tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_);
+    if (!have_points_) {
+        if (cfg_.use_poisson_point_finder)
+            find_poisson_points(seed);
+        else
+            tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_);
+    }
     const int n = (int)points_.size();
     if (n == 0) throw Error(MPSS_ERR_INTERNAL, "tessellation produced no surface points");
     std::vector<float> p(3 * (size_t)n), nr(3 * (size_t)n), eps(n);
@@ -305,6 +311,105 @@ void Context::preprocess(uint32_t seed) {
     std::vector<float> area(n);
     for (int i = 0; i < n; ++i) area[i] = points_[i].area;
     set_irradiance_points(n, p.data(), nr.data(), irradiance_.data(), area.data());
+}
+
+// FindPoissonPointDistribution -> SurfacePointsRenderer::Render (renderers/surfacepoints.cpp:115-150)
+// with ONE SurfacePointTask (:175-284; the reference runs one per core and its result depends on
+// their interleaving): batches of 20000 paths from pCamera are traced on the GPU, 16 batches per
+// launch; on the host each batch's candidates are taken in path order and accepted unless an
+// accepted point lies within minDist (PoissonCheck: DistanceSquared < minDist^2; the reference's
+// octree lookup finds exactly those), until maxFails candidates in a row fail.
+void Context::find_poisson_points(uint32_t seed) {
+    if (scene_dirty_) upload_scene();
+    activate();
+    // scene->WorldBound(): every triangle and every area-light sphere
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = scene_.bvh[0].bmin[k];
+        hi[k] = scene_.bvh[0].bmax[k];
+    }
+    for (const SceneLight &l : scene_.lights) {
+        if (l.kind != 0) continue;
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], l.center[k] + -l.radius);
+            hi[k] = std::max(hi[k], l.center[k] + l.radius);
+        }
+    }
+    PoissonWalk w{};
+    const V3 c = V3{.5f * lo[0] + .5f * hi[0], .5f * lo[1] + .5f * hi[1], .5f * lo[2] + .5f * hi[2]};
+    const bool inside = c.x >= lo[0] && c.x <= hi[0] && c.y >= lo[1] && c.y <= hi[1] && c.z >= lo[2] && c.z <= hi[2];
+    const float rad = inside ? length(c - V3{hi[0], hi[1], hi[2]}) : 0.f;  // BBox::BoundingSphere
+    w.bound.c = c;
+    w.bound.r = rad;
+    w.bound.phi_max = (kPiF / 180.f) * 360.f;
+    w.bound.theta_min = m_acos(-1.f);
+    w.bound.theta_max = m_acos(1.f);
+    w.bound.area = w.bound.phi_max * rad * (rad - -rad);
+    w.origin = xform_point(scene_.camera.camera_to_world, V3{0.f, 0.f, 0.f});
+    w.seed = mix32(seed * 37u + 0x5eed1u);  // RNG rng(37 * taskNum), replay mode
+    const int max_fails = cfg_.quick_render ? std::max(10, 2000 / 10) : 2000;
+    const float md = min_dist_, md2 = md * md;
+    const float area = kPiF * (md / 2.f) * (md / 2.f);
+    constexpr int kBatch = 20000, kBatchesPerLaunch = 16;
+    DevBuf<SurfacePoint> dcand;
+    DevBuf<int> dcount;
+    dcand.alloc((size_t)kBatch * kBatchesPerLaunch * kPoissonCand);
+    dcount.alloc((size_t)kBatch * kBatchesPerLaunch);
+    std::vector<SurfacePoint> cand((size_t)kBatch * kBatchesPerLaunch * kPoissonCand);
+    std::vector<int> cnt((size_t)kBatch * kBatchesPerLaunch);
+    // accepted points, bucketed by minDist cells
+    std::unordered_map<uint64_t, std::vector<uint32_t>> grid;
+    auto cell = [&](float x) { return (int64_t)std::floor((double)x / (double)md); };
+    auto key = [](int64_t x, int64_t y, int64_t z) {
+        return ((uint64_t)(x & 0x1fffff) << 42) | ((uint64_t)(y & 0x1fffff) << 21) | (uint64_t)(z & 0x1fffff);
+    };
+    points_.clear();
+    const RenderScene sc = render_scene();
+    int repeated_fails = 0;
+    int64_t total_paths = 0;
+    bool done = false;
+    for (uint32_t launch = 0; !done; ++launch) {
+        w.path0 = launch * (uint32_t)(kBatch * kBatchesPerLaunch);
+        w.npaths = kBatch * kBatchesPerLaunch;
+        hipLaunchKernelGGL(poisson_walk_kernel, dim3((unsigned)((w.npaths + 255) / 256)), dim3(256), 0, 0, sc, w,
+                           dcand.ptr, dcount.ptr);
+        MPSS_HIP(hipGetLastError());
+        MPSS_HIP(hipMemcpy(cnt.data(), dcount.ptr, sizeof(int) * cnt.size(), hipMemcpyDeviceToHost));
+        MPSS_HIP(hipMemcpy(cand.data(), dcand.ptr, sizeof(SurfacePoint) * cand.size(), hipMemcpyDeviceToHost));
+        for (int b = 0; b < kBatchesPerLaunch && !done; ++b) {
+            total_paths += kBatch;
+            for (int i = b * kBatch; i < (b + 1) * kBatch && !done; ++i)
+                for (int j = 0; j < cnt[i] && !done; ++j) {
+                    SurfacePoint sp = cand[(size_t)i * kPoissonCand + j];
+                    const int64_t cx = cell(sp.p[0]), cy = cell(sp.p[1]), cz = cell(sp.p[2]);
+                    bool fail = false;
+                    for (int dz = -1; dz <= 1 && !fail; ++dz)
+                        for (int dy = -1; dy <= 1 && !fail; ++dy)
+                            for (int dx = -1; dx <= 1 && !fail; ++dx) {
+                                auto it = grid.find(key(cx + dx, cy + dy, cz + dz));
+                                if (it == grid.end()) continue;
+                                for (uint32_t q : it->second) {
+                                    const SurfacePoint &o = points_[q];
+                                    const float ex = o.p[0] - sp.p[0], ey = o.p[1] - sp.p[1], ez = o.p[2] - sp.p[2];
+                                    if (ex * ex + ey * ey + ez * ez < md2) {
+                                        fail = true;
+                                        break;
+                                    }
+                                }
+                            }
+                    if (fail) {
+                        if (++repeated_fails >= max_fails) done = true;
+                    } else {
+                        repeated_fails = 0;
+                        sp.area = area;
+                        grid[key(cx, cy, cz)].push_back((uint32_t)points_.size());
+                        points_.push_back(sp);
+                    }
+                }
+            if (!done && total_paths > 50000 && points_.empty())
+                throw Error(MPSS_ERR_INVALID, "Poisson point finder: no objects with BSSRDFs in the scene");
+        }
+    }
 }
 
 // SamplerRenderer::Render restricted to pixel rectangles. Each rectangle is cut into row

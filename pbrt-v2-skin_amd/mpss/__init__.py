@@ -41,7 +41,7 @@ class Config(C.Structure):
                 ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
                 ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
-                ("max_batch_samples", C.c_int64)]
+                ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int)]
 
 
 class RenderStats(C.Structure):

@@ -405,7 +405,8 @@ def integrator_config(sc, **kw):
     cfg = dict(max_depth=int(it.get("maxdepth", 5)), max_error=float(it.get("maxerror", 0.05)),
                min_sample_distance=float(it.get("minsampledistance", 0.25)), mix=float(it.get("mix", 0.5)),
                show_irradiance_points=int(it.get("showirradiancepoints", "false") == "true"),
-               incenter=int(it.get("incenter", "false") == "true"))
+               incenter=int(it.get("incenter", "false") == "true"),
+               use_poisson_point_finder=int(it.get("usepoissonpointfinder", "false") in ("true", True, 1)))
     cfg.update(kw)
     return cfg
 

@@ -35,6 +35,8 @@ def _lib():
     L.o_scene_add_sphere_light.argtypes = [vp, f32p, C.c_float, f32p, C.c_int]
     L.o_scene_add_infinite_light.restype = C.c_int
     L.o_scene_add_infinite_light.argtypes = [vp, f32p, C.c_int, f32p, f32p, C.c_int, C.c_int, vp]
+    L.o_poisson_points.restype = C.c_long
+    L.o_poisson_points.argtypes = [vp, C.c_float, C.c_int, C.c_uint32, vp, C.c_long]
     L.o_tessellate.restype = C.c_long
     L.o_tessellate.argtypes = [vp, C.c_float, C.c_int, vp, C.c_long]
     L.o_irradiance.argtypes = [vp, C.c_int, vp, C.c_uint32, C.c_int, f32p]
@@ -115,6 +117,7 @@ class OracleScene:
                                        mpss.host_from_rgb(li["L"]), ns)
         self.max_error = cfg.max_error * (4 if cfg.quick_render else 1)
         self.min_dist = cfg.min_sample_distance * (4 if cfg.quick_render else 1)
+        self.quick = bool(cfg.quick_render)
 
     def close(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -130,6 +133,15 @@ class OracleScene:
         out = np.zeros(n, SURFACE_POINT)
         L.o_tessellate(self.h, self.min_dist, int(incenter), out.ctypes.data, n)
         return out
+
+    def poisson_points(self, seed, cap=1 << 22, min_dist=None):
+        """FindPoissonPointDistribution (one task, replay-mode random numbers)."""
+        out = np.zeros(cap, SURFACE_POINT)
+        md = self.min_dist if min_dist is None else min_dist
+        n = _lib().o_poisson_points(self.h, md, int(self.quick), seed, out.ctypes.data, cap)
+        if n < 0:
+            raise RuntimeError("o_poisson_points failed (%d)" % n)
+        return out[:n]
 
     def irradiance(self, pts, seed, nthreads=None):
         pts = np.ascontiguousarray(pts, SURFACE_POINT)
