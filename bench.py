@@ -223,7 +223,7 @@ def pmc_traffic(path, launch_ms):
     the L2 request rate (TCC_HIT + TCC_MISS per launch / launch time)."""
     import glob
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
-                                       key=os.path.getmtime, reverse=True)
+                                       reverse=True)  # newest round tag first (r01j > r01i > ... > r01)
     for f in cands:
         try:
             d = json.load(open(f))
