@@ -105,6 +105,32 @@ int mpss_set_material_tables(mpss_ctx *ctx, const float *rd_table, uint32_t leng
 int mpss_get_material_tables(mpss_ctx *ctx, uint32_t material_id, float *rd_table, uint32_t *length, float *rcp,
                              float *rho_hd, uint32_t *n_rho, float *total_reflectance);
 
+/* Texture "imagemap" (CreateImageSpectrumTexture / CreateImageFloatTexture, textures/imagemap.cpp:
+ * 110-180) with the default "uv" mapping (UVMapping2D, core/texture.cpp:88-98). texels = the image
+ * ReadImage returns (width x height RGB triples, row-major, row t = 0 first); they pass through
+ * convertIn (RGB: scale * (pow(c, gamma) + shift); float: scale * (pow(y(c), gamma) + shift)) and
+ * build the MIPMap (Lanczos resampling to powers of two, box-filtered levels; core/mipmap.h).
+ * width = 0 or texels = NULL: the file could not be read; the reference then uses a one-valued
+ * 1x1 map of powf(scale * (1 + shift), gamma) (imagemap.cpp:76-81). Lookups filter with EWA
+ * (mipmap.h:272-363), or trilinearly with "trilinear". */
+typedef struct {
+    int width, height;
+    const float *texels;
+    int is_float;          /* 1: a "float" texture (bumpmap), 0: "color"/"spectrum" (albedo) */
+    float shift, scale, gamma;   /* "shift" = 0, "scale" = 1, "gamma" = 1 (this fork's convertIn) */
+    int wrap;              /* "wrap": 0 repeat (default), 1 black, 2 clamp */
+    int trilinear;         /* "trilinear" = false */
+    float max_anisotropy;  /* "maxanisotropy" = 8 */
+    float uscale, vscale, udelta, vdelta;  /* "uscale" = "vscale" = 1, "udelta" = "vdelta" = 0 */
+} mpss_imagemap;
+void mpss_imagemap_defaults(mpss_imagemap *t);
+int mpss_add_imagemap(mpss_ctx *ctx, const mpss_imagemap *t, uint32_t *texture_id);
+/* LayeredSkin's texture parameters (CreateLayeredSkinMaterial, layeredskin.cpp:246-249): "albedo"
+ * (a spectrum imagemap; the constant albedo[] of mpss_layeredskin applies when -1) and "bumpmap"
+ * (a float imagemap, Material::Bump on the shading geometry; -1: none). The albedo texture is
+ * evaluated per irradiance point (no differentials) and per camera hit (ray differentials). */
+int mpss_set_material_textures(mpss_ctx *ctx, uint32_t material_id, int32_t albedo_texture, int32_t bump_texture);
+
 /* Irradiance points (IrradiancePoint p, n, E, area; irradiancepoint.h:36-45) -> device octree. */
 int mpss_set_irradiance_points(mpss_ctx *ctx, uint32_t n, const float *p, const float *nrm, const float *E,
                                const float *area);
@@ -205,6 +231,15 @@ int mpss_host_from_rgb(const float *rgb, int illuminant, float *out);
 int mpss_host_tessellate(uint32_t nverts, const float *P, const float *N, const float *S, const float *uv,
                          uint32_t ntris, const int32_t *indices, const float *obj_to_world, const float *world_to_obj,
                          int flip, uint32_t material_id, float min_dist, int incenter, void *records, uint32_t *n);
+/* The same with a "bumpmap" float imagemap applied to every point's normal (BumpMapping::Bump,
+ * trianglemesh.cpp:240-245); bump NULL = mpss_host_tessellate. */
+int mpss_host_tessellate_bumped(uint32_t nverts, const float *P, const float *N, const float *S, const float *uv,
+                                uint32_t ntris, const int32_t *indices, const float *obj_to_world,
+                                const float *world_to_obj, int flip, uint32_t material_id, float min_dist,
+                                int incenter, const mpss_imagemap *bump, void *records, uint32_t *n);
+/* ImageTexture::Evaluate of an imagemap at n points: uvd[6 i ..] = u, v, dudx, dvdx, dudy, dvdy;
+ * out[3 i ..] = the MIPMap value (RGB; a float texture fills out[3 i] and zeroes the rest). */
+int mpss_host_imagemap_lookup(const mpss_imagemap *t, uint32_t n, const float *uvd, float *out);
 /* LayeredSkin -> per-layer 30-band mua/musp [2][30], thickness[2], eta[2] (layeredskin.cpp:47-89). */
 int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, float *thickness, float *eta);
 /* Multipole profile from layer params; rd_table: [30][*length] (query *length with rd_table NULL). */

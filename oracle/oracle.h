@@ -99,6 +99,21 @@ typedef struct {  /* SurfacePoint, renderers/surfacepoints.h:45-55 (44-byte reco
     float area, ray_eps;
 } o_surface_point;
 typedef struct o_scene o_scene;
+/* ImageTexture with UVMapping2D (texture.c): MIPMap levels of the converted texels */
+typedef struct {
+    int nch, nlevels, wrap, trilinear; /* wrap: 0 repeat, 1 black, 2 clamp */
+    float max_aniso, su, sv, du, dv;
+    int w[16], h[16];
+    float *lv[16];
+} o_tex;
+int o_tex_build(o_tex *t, int W, int H, const float *texels, int is_float, float shift, float scale, float gamma,
+                int wrap, int trilinear, float max_aniso, float su, float sv, float du, float dv);
+void o_tex_free(o_tex *t);
+void o_tex_eval(const o_tex *t, float u, float v, float dudx, float dvdx, float dudy, float dvdy, float out[3]);
+int o_imagemap_lookup(int W, int H, const float *texels, int is_float, float shift, float scale, float gamma,
+                      int wrap, int trilinear, float max_aniso, float su, float sv, float du, float dv, int n,
+                      const float *uvd, float *out);
+
 o_scene *o_scene_create(int xres, int yres, const float *raster_to_camera, const float *camera_to_world);
 int o_scene_add_material(o_scene *s, const float *R, const float *T /* nullable: black */, const float *albedo,
                          float mix, float roughness, float eta, int fixed_fresnel, const float *rho, int n_rho,
@@ -131,6 +146,10 @@ void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, con
                         float max_error);
 void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw);
 void o_scene_free(o_scene *s);
+/* LayeredSkin "albedo" (which = 0, a spectrum imagemap) or "bumpmap" (which = 1, a float imagemap) */
+int o_scene_set_material_texture(o_scene *s, int material, int which, int W, int H, const float *texels,
+                                 float shift, float scale, float gamma, int wrap, int trilinear, float max_aniso,
+                                 float su, float sv, float du, float dv);
 
 /* ---- Monte-Carlo layered profile (mc.c; src/renderers/mcprofile.cpp:120-341,443-498) ---- */
 typedef struct { float mua, musp, ior, thickness; } o_mc_layer;

@@ -140,6 +140,9 @@ typedef struct {
 
 typedef struct {
     float R[O_NB], T[O_NB], alb_mix[O_NB], alb_1mmix[O_NB];
+    float mix;
+    int has_alb, has_bump; /* ImageTexture "albedo" / "bumpmap" */
+    o_tex alb, bump;
     float rough2, eta;
     int fixed_fresnel, is_mc, has_refl, has_trans;
     float *rho;
@@ -198,6 +201,7 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T, const float
         if (m->T[c] != 0.f) m->has_trans = 1;
         m->alb_mix[c] = fpowf_(albedo[c], mix);          /* Pow(albedo, mix): IrradianceTask */
         m->alb_1mmix[c] = fpowf_(albedo[c], 1.f - mix);  /* Pow(albedo, 1 - mix): Li */
+        m->mix = mix;
         m->rcp[c] = rcp[c];
     }
     float r = roughness < 1e-3f ? 1e-3f : roughness;    /* Beckmann ctor clamps */
@@ -210,6 +214,19 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T, const float
     m->rd = dupf(rd, (size_t)O_NB * L);
     m->L = L;
     return s->nmats++;
+}
+
+int o_scene_set_material_texture(o_scene *s, int material, int which, int W, int H, const float *texels,
+                                 float shift, float scale, float gamma, int wrap, int trilinear, float max_aniso,
+                                 float su, float sv, float du, float dv) {
+    if (material < 0 || material >= s->nmats) return -1;
+    o_mat *m = &s->mats[material];
+    o_tex *t = which ? &m->bump : &m->alb;
+    if (which ? m->has_bump : m->has_alb) o_tex_free(t);
+    o_tex_build(t, W, H, texels, which, shift, scale, gamma, wrap, trilinear, max_aniso, su, sv, du, dv);
+    if (which) m->has_bump = 1;
+    else m->has_alb = 1;
+    return 0;
 }
 
 int o_scene_add_mesh(o_scene *s, int nv, const float *P, const float *N, const float *S, const float *uv, int nt,
@@ -282,7 +299,12 @@ int o_scene_add_infinite_light(o_scene *s, const float *L, int nsamples, const f
 }
 
 /* ------------------------------------------------------------------ triangle geometry */
-typedef struct { v3 p, ng, nn, sn, tn; float u, v; } frame_t;
+typedef struct {
+    v3 p, ng, nn, sn, tn;
+    float u, v;
+    v3 dpdu, dpdv;          /* dgGeom */
+    v3 ss, ts, dndu, dndv;  /* dgShading's dpdu, dpdv, dndu, dndv */
+} frame_t;
 
 static void tri_uvs(const o_mesh *m, int t, float uv[3][2]) { /* TriangleBase::GetUVs */
     if (m->uv) {
@@ -322,9 +344,14 @@ static frame_t tri_frame(const o_mesh *m, int t, v3 p, float b0, float b1, float
     if (m->flip) ng = mul(ng, -1.f);
     f.ng = ng;
     v3 ss, ts;
+    f.dpdu = dpdu;
+    f.dpdv = dpdv;
+    f.dndu = f.dndv = mk(0.f, 0.f, 0.f);
     if (!m->N && !m->S) {
         f.nn = ng;
         ss = dpdu;
+        f.ss = dpdu;
+        f.ts = dpdv;
     } else {
         /* GetShadingGeometry: barycentrics of (u, v) via SolveLinearSystem2x2 */
         float b[3];
@@ -362,10 +389,95 @@ static frame_t tri_frame(const o_mesh *m, int t, v3 p, float b0, float b1, float
         v3 nn = nrm(crs(ss, ts));
         if (m->flip) nn = mul(nn, -1.f);
         f.nn = nn;
+        f.ss = ss;
+        f.ts = ts;
+        if (m->N && det != 0.f) { /* trianglemesh.inl:269-295, then ObjectToWorld(Normal) */
+            v3 n0 = ld(m->N, m->idx[3 * t]), n1 = ld(m->N, m->idx[3 * t + 1]), n2 = ld(m->N, m->idx[3 * t + 2]);
+            v3 dn1 = sub(n0, n2), dn2 = sub(n1, n2);
+            float invdet = 1.f / det;
+            f.dndu = xnormal(m->w2o, mul(sub(mul(dn1, dv2), mul(dn2, dv1)), invdet));
+            f.dndv = xnormal(m->w2o, mul(add(mul(dn1, -du2), mul(dn2, du1)), invdet));
+        }
     }
     f.sn = nrm(ss);
     f.tn = crs(f.nn, f.sn);
     return f;
+}
+
+/* ------------------------------------------------------------------ textures on the surface */
+/* DifferentialGeometry::ComputeDifferentials (diffgeom.cpp:58-111) for the offset rays
+ * (rxOrigin = ryOrigin = o, directions rxd, ryd): dudx, dvdx, dudy, dvdy into g[2..5] */
+static int solve22(const float A[2][2], const float B[2], float *x0, float *x1) { /* SolveLinearSystem2x2 */
+    float det = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+    if (fabsf(det) < 1e-10f) return 0;
+    *x0 = (A[1][1] * B[0] - A[0][1] * B[1]) / det;
+    *x1 = (A[0][0] * B[1] - A[1][0] * B[0]) / det;
+    if (isnan(*x0) || isnan(*x1)) return 0;
+    return 1;
+}
+static float comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+static void differentials(v3 p, v3 nn, v3 dpdu, v3 dpdv, v3 o, v3 rxd, v3 ryd, float g[6]) {
+    g[2] = g[3] = g[4] = g[5] = 0.f;
+    float d = -dot(nn, p);
+    float tx = -(dot(nn, o) + d) / dot(nn, rxd);
+    if (isnan(tx)) return;
+    v3 px = add(o, mul(rxd, tx));
+    float ty = -(dot(nn, o) + d) / dot(nn, ryd);
+    if (isnan(ty)) return;
+    v3 py = add(o, mul(ryd, ty));
+    int a0, a1;
+    if (fabsf(nn.x) > fabsf(nn.y) && fabsf(nn.x) > fabsf(nn.z)) { a0 = 1; a1 = 2; }
+    else if (fabsf(nn.y) > fabsf(nn.z)) { a0 = 0; a1 = 2; }
+    else { a0 = 0; a1 = 1; }
+    float A[2][2] = {{comp(dpdu, a0), comp(dpdv, a0)}, {comp(dpdu, a1), comp(dpdv, a1)}};
+    float Bx[2] = {comp(px, a0) - comp(p, a0), comp(px, a1) - comp(p, a1)};
+    float By[2] = {comp(py, a0) - comp(p, a0), comp(py, a1) - comp(p, a1)};
+    if (!solve22(A, Bx, &g[2], &g[3])) g[2] = g[3] = 0.f;
+    if (!solve22(A, By, &g[4], &g[5])) g[4] = g[5] = 0.f;
+}
+
+static float tex1(const o_tex *t, const float g[6]) {
+    float x[3];
+    o_tex_eval(t, g[0], g[1], g[2], g[3], g[4], g[5], x);
+    return x[0];
+}
+
+/* Material::Bump (material.cpp:47-104, this fork's central differences); g = u, v, dudx, dvdx,
+ * dudy, dvdy of dgs; returns the bumped dpdu and (faceforwarded to ng) nn */
+static void bump(const o_tex *t, const float g[6], const frame_t *f, v3 nn_s, v3 ng, int flip, v3 *dpdu_b,
+                 v3 *nn_b) {
+    float e[6];
+    memcpy(e, g, sizeof(e));
+    float du = fabsf(g[2]) + fabsf(g[4]);
+    if (du == 0.f) du = .01f;
+    e[0] = g[0] + du;
+    float upD = tex1(t, e);
+    float dv = fabsf(g[3]) + fabsf(g[5]);
+    if (dv == 0.f) dv = .01f;
+    e[0] = g[0];
+    e[1] = g[1] + dv;
+    float vpD = tex1(t, e);
+    float disp = tex1(t, g);
+    du = -du;
+    e[0] = g[0] + du; /* e[1] stays v + dv, as dgEval.v does */
+    float unD = tex1(t, e);
+    dv = -dv;
+    e[0] = g[0];
+    e[1] = g[1] + dv;
+    float vnD = tex1(t, e);
+    *dpdu_b = add(add(f->ss, mul(nn_s, (upD - unD) / (2 * du))), mul(f->dndu, disp));
+    v3 dpdv_b = add(add(f->ts, mul(nn_s, (vpD - vnD) / (2 * dv))), mul(f->dndv, disp));
+    v3 n = nrm(crs(*dpdu_b, dpdv_b));
+    if (flip) n = mul(n, -1.f);
+    *nn_b = dot(n, ng) < 0.f ? neg(n) : n;
+}
+
+/* Pow(FromRGB(albedo lookup), e) */
+static void albedo_pow(const o_tex *t, const float g[6], float e, float out[O_NB]) {
+    float rgb[3], spec[O_NB];
+    o_tex_eval(t, g[0], g[1], g[2], g[3], g[4], g[5], rgb);
+    o_from_rgb(rgb, 0, spec);
+    for (int c = 0; c < O_NB; ++c) out[c] = fpowf_(spec[c], e);
 }
 
 /* Triangle::Intersect ray test */
@@ -940,6 +1052,7 @@ typedef struct {
     v3 v0, v1, v2;
     o_surface_point *out;
     long n, cap;
+    const o_tex *bump; /* the mesh material's bumpmap, or NULL */
 } tess_ctx;
 
 static void domain(tess_ctx *c, bary a, bary b, bary d) {
@@ -955,8 +1068,14 @@ static void domain(tess_ctx *c, bary a, bary b, bary d) {
         o_surface_point *sp = &c->out[c->n];
         v3 p = bpoint(bc, c->v0, c->v1, c->v2);
         frame_t fr = tri_frame(c->m, c->t, p, bc.b0, bc.b1, bc.b2);
+        v3 n = fr.nn;
+        if (c->bump) { /* BumpMapping::Bump with dgs from GetDifferentialGeometries (no differentials) */
+            float g[6] = {fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
+            v3 dpdu_b;
+            bump(c->bump, g, &fr, fr.nn, fr.ng, c->m->flip, &dpdu_b, &n);
+        }
         sp->p[0] = p.x; sp->p[1] = p.y; sp->p[2] = p.z;
-        sp->n[0] = fr.nn.x; sp->n[1] = fr.nn.y; sp->n[2] = fr.nn.z;
+        sp->n[0] = n.x; sp->n[1] = n.y; sp->n[2] = n.z;
         sp->u = fr.u;
         sp->v = fr.v;
         sp->material = (uint32_t)c->m->material;
@@ -1030,6 +1149,8 @@ long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_poin
     for (int mi = 0; mi < s->nmeshes; ++mi) {
         const o_mesh *m = &s->meshes[mi];
         c.m = m;
+        c.bump = (m->material >= 0 && m->material < s->nmats && s->mats[m->material].has_bump)
+                     ? &s->mats[m->material].bump : NULL;
         for (int t = 0; t < m->nt; ++t) {
             c.t = t;
             c.v0 = ld(m->P, m->idx[3 * t]);
@@ -1085,8 +1206,13 @@ static void *irr_worker(void *arg) {
             }
             for (int c = 0; c < O_NB; ++c) E[c] += El[c] / (float)ns;
         }
-        if (mat)
+        if (mat && mat->has_alb) { /* albedo->Evaluate(dgs): (u, v) of the point, no differentials */
+            float g[6] = {sp->u, sp->v, 0.f, 0.f, 0.f, 0.f}, a[O_NB];
+            albedo_pow(&mat->alb, g, mat->mix, a);
+            for (int c = 0; c < O_NB; ++c) E[c] *= a[c];
+        } else if (mat) {
             for (int c = 0; c < O_NB; ++c) E[c] *= mat->alb_mix[c];
+        }
         memcpy(&j->E[(size_t)i * O_NB], E, sizeof(E));
     }
     return NULL;
@@ -1171,6 +1297,27 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
     float reps = 1e-3f * h.t;
     frame_t fr = tri_frame(mesh, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
     v3 wo = neg(d);
+    float alb1[O_NB];
+    if (mat->has_alb || mat->has_bump) {
+        /* GenerateRayDifferential (perspective.cpp:81-113) + ScaleDifferentials(1 / sqrtf(spp)),
+         * then dg.ComputeDifferentials: dgShading's (u, v) and differentials */
+        v3 c0 = xpoint(s->r2c, mk(0.f, 0.f, 0.f));
+        v3 dxc = sub(xpoint(s->r2c, mk(1.f, 0.f, 0.f)), c0), dyc = sub(xpoint(s->r2c, mk(0.f, 1.f, 0.f)), c0);
+        v3 rxw = xvector(s->c2w, nrm(add(pcam, dxc))), ryw = xvector(s->c2w, nrm(add(pcam, dyc)));
+        float k = 1.f / sqrtf((float)spp);
+        v3 rxd = add(d, mul(sub(rxw, d), k)), ryd = add(d, mul(sub(ryw, d), k));
+        float g[6] = {fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
+        differentials(p, fr.ng, fr.dpdu, fr.dpdv, o, rxd, ryd, g);
+        if (mat->has_alb) albedo_pow(&mat->alb, g, 1.f - mat->mix, alb1);
+        if (mat->has_bump) { /* BSDF on the bumped dgs */
+            v3 dpdu_b, nn_b;
+            bump(&mat->bump, g, &fr, fr.nn, fr.ng, mesh->flip, &dpdu_b, &nn_b);
+            fr.nn = nn_b;
+            fr.sn = nrm(dpdu_b);
+            fr.tn = crs(fr.nn, fr.sn);
+        }
+    }
+    if (!mat->has_alb) memcpy(alb1, mat->alb_1mmix, sizeof(alb1));
     /* Mo() term (multipolesubsurface.cpp:268-290) */
     if (s->octree) {
         float q[3] = {fr.p.x, fr.p.y, fr.p.z}, mo[O_NB];
@@ -1179,7 +1326,7 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
         ct = ct < 1.f ? ct : 1.f;
         float Ft = mat->is_mc ? 1.f : 1.f - rho_at(mat, ct);
         for (int c = 0; c < O_NB; ++c) {
-            float t = ((INV_PI_F * Ft) * mo[c]) * mat->alb_1mmix[c];
+            float t = ((INV_PI_F * Ft) * mo[c]) * alb1[c];
             L[c] += t < 0.f ? 0.f : t;
         }
     }
@@ -1328,7 +1475,12 @@ void o_scene_free(o_scene *s) {
         free(s->meshes[m].P); free(s->meshes[m].N); free(s->meshes[m].S); free(s->meshes[m].uv);
         free(s->meshes[m].idx);
     }
-    for (int m = 0; m < s->nmats; ++m) { free(s->mats[m].rho); free(s->mats[m].rd); }
+    for (int m = 0; m < s->nmats; ++m) {
+        free(s->mats[m].rho);
+        free(s->mats[m].rd);
+        if (s->mats[m].has_alb) o_tex_free(&s->mats[m].alb);
+        if (s->mats[m].has_bump) o_tex_free(&s->mats[m].bump);
+    }
     for (int l = 0; l < s->nlights; ++l)
         if (s->lights[l].kind) o_envmap_free(&s->lights[l].em);
     free(s->meshes); free(s->lights); free(s->mats);
@@ -1450,6 +1602,12 @@ long o_poisson_points(o_scene *s, float min_dist, int quick, uint32_t seed, o_su
                 eps = 1e-3f * h.t;
                 if (depth >= 3) { /* every material on this path is LayeredSkin: GetBSSRDF != NULL */
                     v3 sn = (!mesh->N && !mesh->S) ? nn : fr.nn;
+                    const o_mat *mt = &s->mats[mesh->material];
+                    if (mt->has_bump) { /* Bump(hitGeometry, dgShading) without differentials */
+                        float g[6] = {fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
+                        v3 dpdu_b;
+                        bump(&mt->bump, g, &fr, sn, nn, mesh->flip, &dpdu_b, &sn);
+                    }
                     sp.p[0] = p.x; sp.p[1] = p.y; sp.p[2] = p.z;
                     sp.n[0] = sn.x; sp.n[1] = sn.y; sp.n[2] = sn.z;
                     sp.u = fr.u; sp.v = fr.v;

@@ -90,6 +90,77 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
     return (uint32_t)materials_.size() - 1;
 }
 
+std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m) {
+    auto t = std::make_unique<ImageTexture>();
+    const int nch = m.is_float ? 1 : 3;
+    if (m.width <= 0 || m.height <= 0 || !m.texels) {
+        // the image could not be read: a one-valued MIPMap(1, 1, oneVal) with the MIPMap defaults
+        // (no trilinear, maxAniso 8, TEXTURE_REPEAT), oneVal = powf(scale * (1 + shift), gamma)
+        const float one = m_pow(m.scale * (1 + m.shift), m.gamma);
+        const float v[3] = {one, one, one};
+        t->py = build_pyramid(1, 1, nch, v, TEX_REPEAT);
+        t->trilinear = 0;
+        t->max_aniso = 8.f;
+    } else {
+        if ((int64_t)m.width * m.height > (int64_t)1 << 28) throw Error(MPSS_ERR_INVALID, "imagemap: image too large");
+        const size_t n = (size_t)m.width * m.height;
+        std::vector<float> conv(n * nch);
+        for (size_t i = 0; i < n; ++i) {
+            const float *x = m.texels + 3 * i;
+            if (nch == 3) {  // convertIn(RGBSpectrum): scale * (Pow(from, gamma) + shift)
+                for (int k = 0; k < 3; ++k) conv[3 * i + k] = m.scale * (m_pow(x[k], m.gamma) + m.shift);
+            } else {         // convertIn(float): scale * (powf(from.y(), gamma) + shift)
+                const float y = (0.212671f * x[0] + 0.715160f * x[1]) + 0.072169f * x[2];
+                conv[i] = m.scale * (m_pow(y, m.gamma) + m.shift);
+            }
+        }
+        if (m.wrap < TEX_REPEAT || m.wrap > TEX_CLAMP) throw Error(MPSS_ERR_INVALID, "imagemap: bad wrap mode");
+        t->py = build_pyramid(m.width, m.height, nch, conv.data(), m.wrap);
+        t->trilinear = m.trilinear != 0;
+        t->max_aniso = m.max_anisotropy;
+    }
+    t->su = m.uscale;
+    t->sv = m.vscale;
+    t->du = m.udelta;
+    t->dv = m.vdelta;
+    t->host = t->py.view(t->trilinear, t->max_aniso);
+    t->host.su = t->su;
+    t->host.sv = t->sv;
+    t->host.du = t->du;
+    t->host.dv = t->dv;
+    return t;
+}
+
+uint32_t Context::add_imagemap(const mpss_imagemap &m) {
+    textures_.push_back(build_imagemap(m));
+    scene_dirty_ = true;
+    return (uint32_t)textures_.size() - 1;
+}
+
+void Context::set_material_textures(uint32_t material, int albedo, int bump) {
+    if (material >= materials_.size()) throw Error(MPSS_ERR_INVALID, "set_material_textures: unknown material id");
+    auto check = [&](int id, bool want_float, const char *what) {
+        if (id < 0) return;
+        if (id >= (int)textures_.size())
+            throw Error(MPSS_ERR_INVALID, std::string("set_material_textures: unknown texture id for ") + what);
+        if ((textures_[id]->py.nch == 1) != want_float)
+            throw Error(MPSS_ERR_INVALID, std::string("set_material_textures: ") + what +
+                                              (want_float ? " needs a float texture" : " needs a spectrum texture"));
+    };
+    check(albedo, false, "albedo");
+    check(bump, true, "bumpmap");
+    materials_[material]->albedo_tex = albedo;
+    materials_[material]->bump_tex = bump;
+    scene_dirty_ = true;
+}
+
+std::vector<const TexView *> Context::host_bump_views() const {
+    std::vector<const TexView *> v(materials_.size(), nullptr);
+    for (size_t i = 0; i < materials_.size(); ++i)
+        if (materials_[i]->bump_tex >= 0) v[i] = &textures_[materials_[i]->bump_tex]->host;
+    return v;
+}
+
 const Material &Context::material(uint32_t id) const {
     if (id >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(id));
     return *materials_[id];

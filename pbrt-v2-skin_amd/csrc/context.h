@@ -10,6 +10,7 @@
 #include "mo_kernel.h"
 #include "octree.h"
 #include "scene.h"
+#include "texture_build.h"
 
 namespace mpss {
 
@@ -26,7 +27,27 @@ struct Material {
     bool is_monte_carlo = false;
     DeviceProfile dev_profile;
     DevBuf<float> dev_rho;  // [n_rho]
+    int albedo_tex = -1, bump_tex = -1;  // ImageTexture ids ("texture albedo" / "texture bumpmap")
 };
+
+// ImageTexture<RGBSpectrum, Spectrum> / ImageTexture<float, float> (textures/imagemap.{h,cpp})
+// with its UVMapping2D: the converted texels' MIPMap, on the host and (after upload) the device.
+struct ImageTexture {
+    HostPyramid py;
+    int trilinear = 0;
+    float max_aniso = 8.f, su = 1.f, sv = 1.f, du = 0.f, dv = 0.f;
+    TexView host;  // over py.data
+    DevBuf<float> dev;
+    TexView device_view(const float *lut) const {
+        TexView v = host;
+        v.data = dev.ptr;
+        v.lut = lut;
+        return v;
+    }
+};
+// ImageTexture::GetTexture's conversion + MIPMap (imagemap.cpp:55-84): texels through convertIn,
+// or the one-valued map when the image could not be read (width == 0)
+std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m);
 
 class Context {
 public:
@@ -38,6 +59,9 @@ public:
     const Material &material(uint32_t id) const;
     void set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area);
     const DeviceOctree &octree() const;
+    uint32_t add_imagemap(const mpss_imagemap &m);
+    void set_material_textures(uint32_t material, int albedo, int bump);
+    std::vector<const TexView *> host_bump_views() const;
     float max_error() const { return max_error_; }
     const mpss_config &config() const { return cfg_; }
 
@@ -82,6 +106,10 @@ private:
     std::vector<std::unique_ptr<DevBuf<float>>> d_envmaps_;  // per infinite light (envmap.h layout)
     DevBuf<float> d_zero_map_;                                // stand-in map of area lights
     DevBuf<struct RenderMaterial> d_materials_;
+    std::vector<std::unique_ptr<ImageTexture>> textures_;
+    DevBuf<float> d_lut_;  // EWA weight table
+    DevBuf<float4> ws_alb_, ws_frame_;  // per hit: albedo lookup, bumped frame (textured scenes)
+    int64_t ws_tex_hits_ = 0;
     // render workspace: per camera sample (flags, slot) and per surface hit (ld, Mo query, Mo)
     DevBuf<uint32_t> ws_flags_;
     DevBuf<int32_t> ws_slot_;

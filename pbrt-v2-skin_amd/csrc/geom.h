@@ -48,6 +48,8 @@ MPSS_HD void tri_uvs(const MeshView &m, int t, float uv[3][2]) {
 struct ShadingFrame {
     V3 p, ng, nn, sn, tn;  // geometric normal, shading normal, BSDF tangent frame (reflection.cpp:754-762)
     float u, v;
+    V3 dpdu, dpdv;         // dgGeom's partial derivatives (ComputeDifferentials)
+    V3 ss, ts, dndu, dndv; // dgShading's dpdu, dpdv, dndu, dndv (world space; Bump)
 };
 
 // Geometry + shading geometry at barycentrics (b0, b1, b2) with point p:
@@ -78,9 +80,14 @@ MPSS_HD ShadingFrame tri_shading(const MeshView &m, int t, V3 p, float b0, float
     if (m.flip) ng = ng * -1.f;
     f.ng = ng;
     V3 ss, ts;
+    f.dpdu = dpdu;
+    f.dpdv = dpdv;
+    f.dndu = f.dndv = V3{0.f, 0.f, 0.f};
     if (!m.N && !m.S) {
         f.nn = ng;
         ss = dpdu;
+        f.ss = dpdu;
+        f.ts = dpdv;
     } else {
         float bb[3];
         const float A00 = uv[1][0] - uv[0][0], A01 = uv[2][0] - uv[0][0];
@@ -120,6 +127,15 @@ MPSS_HD ShadingFrame tri_shading(const MeshView &m, int t, V3 p, float b0, float
         V3 nn = normalize(cross(ss, ts));
         if (m.flip) nn = nn * -1.f;
         f.nn = nn;
+        f.ss = ss;
+        f.ts = ts;
+        if (m.N && det != 0.f) {  // dndu, dndv from the vertex normals (trianglemesh.inl:269-295)
+            const V3 n0 = ldv3(m.N, m.idx[3 * t]), n1 = ldv3(m.N, m.idx[3 * t + 1]), n2 = ldv3(m.N, m.idx[3 * t + 2]);
+            const V3 dn1 = n0 - n2, dn2 = n1 - n2;
+            const float invdet = 1.f / det;
+            f.dndu = xform_normal(m.w2o, (dn1 * dv2 - dn2 * dv1) * invdet);
+            f.dndv = xform_normal(m.w2o, (dn1 * -du2 + dn2 * du1) * invdet);
+        }
     }
     f.sn = normalize(ss);        // BSDF: sn = Normalize(dgShading.dpdu)
     f.tn = cross(f.nn, f.sn);    //       tn = Cross(nn, sn)

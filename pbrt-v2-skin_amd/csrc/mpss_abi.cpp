@@ -41,7 +41,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 2; }  // 2: mpss_config.use_poisson_point_finder, infinite lights
+int mpss_abi_version(void) { return 3; }  // 2: poisson point finder, infinite lights; 3: imagemap textures
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -99,6 +99,29 @@ int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {
         require(m->desired_length >= 2 && m->desired_length <= 4096, "desiredlength out of range [2, 4096]");
         require(m->nmperunit > 0.f, "nmperunit must be positive");
         *id = reinterpret_cast<Context *>(c)->add_layeredskin(*m);
+    });
+}
+
+void mpss_imagemap_defaults(mpss_imagemap *t) {
+    if (!t) return;
+    memset(t, 0, sizeof(*t));
+    t->scale = 1.f;
+    t->gamma = 1.f;
+    t->max_anisotropy = 8.f;
+    t->uscale = t->vscale = 1.f;
+}
+
+int mpss_add_imagemap(mpss_ctx *c, const mpss_imagemap *t, uint32_t *id) {
+    return guarded([&] {
+        require(c && t && id, "mpss_add_imagemap: null argument");
+        *id = reinterpret_cast<Context *>(c)->add_imagemap(*t);
+    });
+}
+
+int mpss_set_material_textures(mpss_ctx *c, uint32_t mid, int32_t albedo, int32_t bump) {
+    return guarded([&] {
+        require(c != nullptr, "mpss_set_material_textures: null context");
+        reinterpret_cast<Context *>(c)->set_material_textures(mid, albedo, bump);
     });
 }
 
@@ -311,6 +334,26 @@ int mpss_mc_profile(mpss_ctx *c, const mpss_layer *layers, int n, float mfp_rang
 int mpss_host_tessellate(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
                          const int32_t *idx, const float *o2w, const float *w2o, int flip, uint32_t mat,
                          float min_dist, int incenter, void *rec, uint32_t *n) {
+    return mpss_host_tessellate_bumped(nv, P, N, S, uv, nt, idx, o2w, w2o, flip, mat, min_dist, incenter, nullptr, rec,
+                                       n);
+}
+
+int mpss_host_imagemap_lookup(const mpss_imagemap *t, uint32_t n, const float *uvd, float *out) {
+    return guarded([&] {
+        require(t && (n == 0 || (uvd && out)), "mpss_host_imagemap_lookup: null argument");
+        const std::unique_ptr<ImageTexture> tex = build_imagemap(*t);
+        for (uint32_t i = 0; i < n; ++i) {
+            const float *a = uvd + 6 * (size_t)i;
+            const UVDiff g{a[0], a[1], a[2], a[3], a[4], a[5]};
+            tex_eval(tex->host, g, out + 3 * (size_t)i);
+        }
+    });
+}
+
+int mpss_host_tessellate_bumped(uint32_t nv, const float *P, const float *N, const float *S, const float *uv,
+                                uint32_t nt, const int32_t *idx, const float *o2w, const float *w2o, int flip,
+                                uint32_t mat, float min_dist, int incenter, const mpss_imagemap *bump, void *rec,
+                                uint32_t *n) {
     return guarded([&] {
         require(P && idx && o2w && w2o && n && nv > 0 && min_dist > 0.f, "mpss_host_tessellate: bad argument");
         SceneData sd;
@@ -328,7 +371,15 @@ int mpss_host_tessellate(uint32_t nv, const float *P, const float *N, const floa
         m.material = mat;
         sd.meshes.push_back(std::move(m));
         std::vector<SurfacePoint> pts;
-        tessellate_surface_points(sd, min_dist, incenter != 0, pts);
+        std::unique_ptr<ImageTexture> bt;
+        std::vector<const TexView *> bv;
+        if (bump) {
+            require(bump->is_float != 0, "mpss_host_tessellate_bumped: the bumpmap is a float texture");
+            bt = build_imagemap(*bump);
+            bv.assign((size_t)mat + 1, nullptr);
+            bv[mat] = &bt->host;
+        }
+        tessellate_surface_points(sd, min_dist, incenter != 0, pts, 0, bump ? bv.data() : nullptr);
         if (rec) {
             require(*n >= pts.size(), "mpss_host_tessellate: records buffer too small");
             memcpy(rec, pts.data(), pts.size() * sizeof(SurfacePoint));

@@ -8,6 +8,7 @@
 #include "mo_kernel.h"
 #include "mo_band.h"
 #include "scene.h"
+#include "texture.h"
 
 namespace mpss {
 
@@ -40,6 +41,11 @@ struct RenderMaterial {
     Microfacet mf;
     const float *rho;     // device rho_hd table
     int n_rho, has_bssrdf, has_refl, has_trans, is_mc;
+    // ImageTexture "albedo" (replaces alb_mix / alb_1mmix: Pow(FromRGB(lookup), mix) per point)
+    // and "bumpmap" (Material::Bump of the shading geometry), textures/imagemap.cpp
+    int has_alb_tex, has_bump;
+    float mix;
+    TexView alb_tex, bump_tex;
 };
 
 struct RenderScene {
@@ -52,7 +58,9 @@ struct RenderScene {
     int nlights, nmaterials, xres, yres;
     int have_octree;  // Preprocess built an octree: BSSRDF hits evaluate Mo()
     int n_infinite;   // lights of kind 1: camera rays that miss everything see their Le
+    int any_tex;      // some material has an albedo texture or a bump map: shade_tex_kernel runs
     float raster_to_camera[16], camera_to_world[16];
+    float dx_camera[3], dy_camera[3];  // PerspectiveCamera dxCamera / dyCamera (perspective.cpp:47-48)
 };
 
 // A tile [x0,x1) x [y0,y1) extended by one pixel on every side that exists (origin ex0, ey0;
@@ -90,6 +98,8 @@ struct SampleRecs {
     int *hit_count;  // device counter of hit slots (shared by every tile of a batch)
     float4 *mo4;     // [hits][kGroups] Mo() per band group (mo_band.h layout)
     float4 *xyz;     // [hits] the sample's filtered XYZ (assemble_kernel)
+    float4 *hit_alb; // [hits] albedo texture lookup (RGB) of a textured BSSRDF hit (shade_tex_kernel)
+    float4 *hit_frame; // [hits][2] bump-mapped shading normal nn and dpdu direction sn (shade_tex_kernel)
 };
 
 // SurfacePointTask's random-walk paths (usepoissonpointfinder): one lane per path, candidates of
@@ -104,7 +114,7 @@ struct PoissonWalk {
 __global__ void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint *out, int *count);
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
-                                  const uint32_t *sp_mat, int n, uint32_t seed, float *E_out);
+                                  const uint32_t *sp_mat, const float *sp_uv, int n, uint32_t seed, float *E_out);
 struct BandPos {
     int pos[NB];  // band c's float offset inside a sample's mo4 row (BandGroups::pos)
 };
@@ -115,6 +125,10 @@ struct DirectTerms;
 // of the light-sampled and the BSDF-sampled direction of an infinite light's EstimateDirect
 __global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits, int ns_max,
                                     DirectTerms *terms, float4 *inf_st);
+// Per surface hit of a material with textures: the camera ray's differentials (scaled by
+// 1/sqrt(spp)), ComputeDifferentials, the albedo lookup (-> hit_alb) and the bumped shading frame
+// (-> hit_frame), before shade_direct_kernel reads them.
+__global__ void shade_tex_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits);
 __global__ void shade_nolight_kernel(RenderScene sc, SampleRecs rec, int max_hits);
 template <bool kInf>
 __global__ void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,

@@ -29,6 +29,12 @@ __constant__ float kIllum[7][NB] = {MPSS_BAND_RGBILLUM2SPECTWHITE_INIT,  MPSS_BA
                                     MPSS_BAND_RGBILLUM2SPECTRED_INIT,     MPSS_BAND_RGBILLUM2SPECTGREEN_INIT,
                                     MPSS_BAND_RGBILLUM2SPECTBLUE_INIT};
 
+// rgbRefl2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue} (spectrum.cpp:316-370)
+__constant__ float kRefl[7][NB] = {MPSS_BAND_RGBREFL2SPECTWHITE_INIT,  MPSS_BAND_RGBREFL2SPECTCYAN_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTMAGENTA_INIT, MPSS_BAND_RGBREFL2SPECTYELLOW_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTRED_INIT,     MPSS_BAND_RGBREFL2SPECTGREEN_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTBLUE_INIT};
+
 namespace {
 
 constexpr int kStack = 48;  // BVH traversal stack depth (host checks the tree depth)
@@ -254,6 +260,45 @@ __device__ __forceinline__ float illum_band(const float rgb[3], int c) {
     return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
 }
 
+// band c of Spectrum::FromRGB(rgb) (reflectance; spectrum.cpp:103-187): ImageTexture's convertOut
+__device__ __forceinline__ float refl_band(const float rgb[3], int c) {
+    const float R = rgb[0], G = rgb[1], B = rgb[2];
+    float r = 0.f;
+    if (R <= G && R <= B) {
+        r += kRefl[0][c] * R;
+        if (G <= B) {
+            r += kRefl[1][c] * (G - R);
+            r += kRefl[6][c] * (B - G);
+        } else {
+            r += kRefl[1][c] * (B - R);
+            r += kRefl[5][c] * (G - B);
+        }
+    } else if (G <= R && G <= B) {
+        r += kRefl[0][c] * G;
+        if (R <= B) {
+            r += kRefl[2][c] * (R - G);
+            r += kRefl[6][c] * (B - R);
+        } else {
+            r += kRefl[2][c] * (B - G);
+            r += kRefl[4][c] * (R - B);
+        }
+    } else {
+        r += kRefl[0][c] * B;
+        if (R <= G) {
+            r += kRefl[3][c] * (R - B);
+            r += kRefl[5][c] * (G - R);
+        } else {
+            r += kRefl[3][c] * (G - B);
+            r += kRefl[4][c] * (R - G);
+        }
+    }
+    const float v = r * .94f;
+    return v < 0.f ? 0.f : v;
+}
+
+// Pow(albedo, e) band c for a textured albedo: the ImageTexture value at the point, FromRGB
+__device__ __noinline__ float tex_albedo_pow(const float rgb[3], int c, float e) { return m_pow(refl_band(rgb, c), e); }
+
 __device__ __noinline__ bool inf_nonblack(const RenderLight &L, float s, float t) {  // !Le.IsBlack()
     float rgb[3];
     inf_lookup(L, s, t, rgb);
@@ -335,7 +380,8 @@ __device__ __forceinline__ float rho_lookup(const float *hd, int n, float ct) { 
 __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const float *__restrict__ sp_p,
                                                          const float *__restrict__ sp_n,
                                                          const float *__restrict__ sp_eps,
-                                                         const uint32_t *__restrict__ sp_mat, int n, uint32_t seed,
+                                                         const uint32_t *__restrict__ sp_mat,
+                                                         const float *__restrict__ sp_uv, int n, uint32_t seed,
                                                          float *__restrict__ E_out) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
@@ -377,8 +423,14 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
         }
         for (int c = 0; c < NB; ++c) E[c] += El[c] / (float)ns;
     }
-    if (bss)
+    if (bss && mat->has_alb_tex) {  // albedo->Evaluate(dgs): dgs has no differentials -> triangle(0, s, t)
+        const UVDiff g{sp_uv[2 * i], sp_uv[2 * i + 1], 0.f, 0.f, 0.f, 0.f};
+        float rgb[3];
+        tex_eval(mat->alb_tex, g, rgb);
+        for (int c = 0; c < NB; ++c) E[c] *= tex_albedo_pow(rgb, c, mat->mix);
+    } else if (bss) {
         for (int c = 0; c < NB; ++c) E[c] *= mat->alb_mix[c];
+    }
     for (int c = 0; c < NB; ++c) E_out[(size_t)i * NB + c] = E[c];
 }
 
@@ -436,8 +488,15 @@ __global__ __launch_bounds__(256) void poisson_walk_kernel(RenderScene sc, Poiss
             nn = faceforward(fr.ng, -d);
             eps = 1e-3f * h.t;
             if (depth >= 3 && mesh.material < (uint32_t)sc.nmaterials && sc.materials[mesh.material].has_bssrdf) {
-                // dgs = dgShading (no bump map); without N and S the shading geometry is dg itself
-                const V3 sn = (!mesh.view.N && !mesh.view.S) ? nn : fr.nn;
+                // dgs = Bump(hitGeometry, dgShading); without N and S the shading geometry is dg itself
+                // (its nn already faceforwarded); no ray differentials (GetBSSRDF(RayDifferential(ray)))
+                V3 sn = (!mesh.view.N && !mesh.view.S) ? nn : fr.nn;
+                const RenderMaterial &mt = sc.materials[mesh.material];
+                if (mt.has_bump) {
+                    const UVDiff g{fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
+                    V3 dpdu_b;
+                    bump_frame(mt.bump_tex, g, fr.ss, fr.ts, fr.dndu, fr.dndv, sn, nn, mesh.view.flip, dpdu_b, sn);
+                }
                 SurfacePoint sp;
                 sp.p[0] = p.x;
                 sp.p[1] = p.y;
@@ -639,9 +698,15 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     const RenderMesh &mesh = sc.meshes[mi];
     const V3 p = o + d * ha.x;  // Ray::operator()
     const float reps = 1e-3f * ha.x;
-    const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - ha.y - ha.z, ha.y, ha.z);
+    ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - ha.y - ha.z, ha.y, ha.z);
     const V3 wo = -d;
     const RenderMaterial &mat = sc.materials[mid];
+    if (mat.has_bump) {  // BSDF on the bumped dgs: nn, sn = Normalize(dpdu), tn = Cross(nn, sn)
+        const float4 a = rec.hit_frame[2 * (size_t)slot], b = rec.hit_frame[2 * (size_t)slot + 1];
+        fr.nn = V3{a.x, a.y, a.z};
+        fr.sn = V3{b.x, b.y, b.z};
+        fr.tn = cross(fr.nn, fr.sn);
+    }
     if (lj == 0) {
         float ct = absdot(wo, fr.nn);
         ct = ct < 1.f ? ct : 1.f;
@@ -718,6 +783,58 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     }
     terms[gid] = out;
     if (L.kind) inf_st[gid] = st;
+}
+
+// ------------------------------------------------------------------ textures
+// Li's GetBSDF / GetMultipoleBSSRDF for materials with an albedo texture or a bump map: the
+// camera RayDifferential (PerspectiveCamera::GenerateRayDifferential, perspective.cpp:81-113,
+// ScaleDifferentials(1 / sqrtf(spp)), samplerrenderer.cpp:90-91), dg.ComputeDifferentials, then
+// albedo->Evaluate(dgShading) (layeredskin.cpp:180-185) and Bump (layeredskin.cpp:143-146).
+__global__ __launch_bounds__(256) void shade_tex_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
+                                                        int max_hits) {
+    const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int nhits = *rec.hit_count;
+    if (slot >= nhits || slot >= max_hits) return;
+    const uint32_t hs = rec.hit_s[slot];
+    if (hs & 0x40000000u) return;
+    const RenderMaterial &mat = sc.materials[(hs >> REC_MAT_SHIFT) & 0xffu];
+    const bool want_alb = (hs >> 31) && mat.has_alb_tex;
+    if (!want_alb && !mat.has_bump) return;
+    const float4 ha = rec.hit_a[slot], hb = rec.hit_b[slot];
+    const int s = (int)(hs & 0xffffu), tri = __float_as_int(ha.w);
+    const uint32_t pix = __float_as_uint(hb.w);
+    const V3 d = V3{hb.x, hb.y, hb.z};
+    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
+    const RenderMesh &mesh = sc.meshes[sc.tri_mesh[tri]];
+    const V3 p = o + d * ha.x;
+    const ShadingFrame fr = tri_shading(mesh.view, sc.tri_local[tri], p, 1.f - ha.y - ha.z, ha.y, ha.z);
+    // the sample's image position (as primary_kernel) and its offset rays
+    const int px = (int)(pix % (uint32_t)sc.xres), py = (int)(pix / (uint32_t)sc.xres);
+    const float X = (float)px + van_der_corput((uint32_t)s, hash3(seed, pix, DIM_IMAGE));
+    const float Y = (float)py + sobol2((uint32_t)s, hash3(seed, pix, DIM_IMAGE + 1));
+    const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
+    const V3 dxc = V3{sc.dx_camera[0], sc.dx_camera[1], sc.dx_camera[2]};
+    const V3 dyc = V3{sc.dy_camera[0], sc.dy_camera[1], sc.dy_camera[2]};
+    const V3 rxw = xform_vector(sc.camera_to_world, normalize(pcam + dxc));
+    const V3 ryw = xform_vector(sc.camera_to_world, normalize(pcam + dyc));
+    const float k = 1.f / sqrtf((float)spp);
+    const V3 rxd = d + (rxw - d) * k, ryd = d + (ryw - d) * k;
+    UVDiff g;
+    g.u = fr.u;
+    g.v = fr.v;
+    compute_differentials(p, fr.ng, fr.dpdu, fr.dpdv, o, rxd, ryd, g);
+    if (want_alb) {
+        float rgb[3];
+        tex_eval(mat.alb_tex, g, rgb);
+        rec.hit_alb[slot] = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
+    }
+    if (mat.has_bump) {
+        V3 dpdu_b, nn_b;
+        bump_frame(mat.bump_tex, g, fr.ss, fr.ts, fr.dndu, fr.dndv, fr.nn, fr.ng, mesh.view.flip, dpdu_b, nn_b);
+        const V3 sn = normalize(dpdu_b);  // BSDF: sn = Normalize(dgs.dpdu)
+        rec.hit_frame[2 * (size_t)slot] = make_float4(nn_b.x, nn_b.y, nn_b.z, 0.f);
+        rec.hit_frame[2 * (size_t)slot + 1] = make_float4(sn.x, sn.y, sn.z, 0.f);
+    }
 }
 
 // A scene without lights: no direct light and (Preprocess returned early) no octree.
@@ -799,7 +916,8 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
     const uint32_t hs = rec.hit_s[slot];
     const float *le = nullptr, *mo = nullptr, *ld = nullptr;
     const RenderMaterial *mat = nullptr;
-    float kss = 0.f;
+    float kss = 0.f, arg[3] = {0.f, 0.f, 0.f};
+    bool alb = false;
     if ((hs & 0x40000000u) && ((hs >> REC_MAT_SHIFT) & 0xffu) == 0xffu) return;  // escaped: sky_kernel
     if (hs & 0x40000000u) {
         le = sc.lights[(hs >> REC_MAT_SHIFT) & 0xffu].Lemit;
@@ -811,6 +929,13 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
             const float Ft = mat->is_mc ? 1.f : 1.f - rho_lookup(mat->rho, mat->n_rho, q.w);
             kss = kInvPiF * Ft;
             mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
+            if (mat->has_alb_tex) {
+                const float4 a = rec.hit_alb[slot];
+                arg[0] = a.x;
+                arg[1] = a.y;
+                arg[2] = a.z;
+                alb = true;
+            }
         }
     }
     float X = 0.f, Y = 0.f, Z = 0.f;
@@ -819,7 +944,8 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
         float L = 0.f;
         if (le) L += le[c];
         if (mo) {
-            float t = (kss * mo[bp.pos[c]]) * mat->alb_1mmix[c];
+            const float ab = alb ? tex_albedo_pow(arg, c, 1.f - mat->mix) : mat->alb_1mmix[c];
+            float t = (kss * mo[bp.pos[c]]) * ab;
             t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
             L += t;
         }

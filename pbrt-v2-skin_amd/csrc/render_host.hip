@@ -9,6 +9,7 @@
 #include "envmap.h"
 #include "render.h"
 #include "spectral.h"
+#include "texture_build.h"
 
 namespace mpss {
 
@@ -204,6 +205,9 @@ void Context::upload_scene() {
     }
     d_lights_.upload(rl.data(), rl.size());
     std::vector<RenderMaterial> rmat;
+    if (!d_lut_.ptr) d_lut_.upload(ewa_weight_lut(), kEwaLut);
+    for (auto &t : textures_)
+        if (!t->dev.ptr) t->dev.upload(t->py.data.data(), t->py.data.size());
     for (const auto &mp : materials_) {
         const Material &m = *mp;
         RenderMaterial r{};
@@ -228,6 +232,15 @@ void Context::upload_scene() {
         r.n_rho = (int)m.rho.hd.size();
         r.has_bssrdf = 1;
         r.is_mc = m.is_monte_carlo ? 1 : 0;
+        r.mix = cfg_.mix;
+        if (m.albedo_tex >= 0) {
+            r.has_alb_tex = 1;
+            r.alb_tex = textures_[m.albedo_tex]->device_view(d_lut_.ptr);
+        }
+        if (m.bump_tex >= 0) {
+            r.has_bump = 1;
+            r.bump_tex = textures_[m.bump_tex]->device_view(d_lut_.ptr);
+        }
         rmat.push_back(r);
     }
     d_materials_.upload(rmat.data(), rmat.size());
@@ -250,6 +263,17 @@ RenderScene Context::render_scene() const {
     sc.yres = scene_.camera.yres;
     memcpy(sc.raster_to_camera, scene_.camera.raster_to_camera, sizeof(sc.raster_to_camera));
     memcpy(sc.camera_to_world, scene_.camera.camera_to_world, sizeof(sc.camera_to_world));
+    // dxCamera = RasterToCamera(Point(1,0,0)) - RasterToCamera(Point(0,0,0)) (perspective.cpp:47-48)
+    const V3 c0 = xform_point(sc.raster_to_camera, V3{0.f, 0.f, 0.f});
+    const V3 dx = xform_point(sc.raster_to_camera, V3{1.f, 0.f, 0.f}) - c0;
+    const V3 dy = xform_point(sc.raster_to_camera, V3{0.f, 1.f, 0.f}) - c0;
+    sc.dx_camera[0] = dx.x;
+    sc.dx_camera[1] = dx.y;
+    sc.dx_camera[2] = dx.z;
+    sc.dy_camera[0] = dy.x;
+    sc.dy_camera[1] = dy.y;
+    sc.dy_camera[2] = dy.z;
+    for (const auto &m : materials_) sc.any_tex |= (m->albedo_tex >= 0 || m->bump_tex >= 0);
     return sc;
 }
 
@@ -270,13 +294,16 @@ void Context::preprocess(uint32_t seed) {
         if (cfg_.use_poisson_point_finder)
             find_poisson_points(seed);
         else
-            tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_);
+            tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_, 0, host_bump_views().data());
     }
     const int n = (int)points_.size();
     if (n == 0) throw Error(MPSS_ERR_INTERNAL, "tessellation produced no surface points");
     std::vector<float> p(3 * (size_t)n), nr(3 * (size_t)n), eps(n);
     std::vector<uint32_t> mat(n);
+    std::vector<float> uv(2 * (size_t)n);
     for (int i = 0; i < n; ++i) {
+        uv[2 * (size_t)i] = points_[i].u;
+        uv[2 * (size_t)i + 1] = points_[i].v;
         for (int k = 0; k < 3; ++k) {
             p[3 * (size_t)i + k] = points_[i].p[k];
             nr[3 * (size_t)i + k] = points_[i].n[k];
@@ -284,8 +311,9 @@ void Context::preprocess(uint32_t seed) {
         eps[i] = points_[i].ray_eps;
         mat[i] = points_[i].material;
     }
-    DevBuf<float> dp, dn, de, dE;
+    DevBuf<float> dp, dn, de, dE, duv;
     DevBuf<uint32_t> dm;
+    duv.upload(uv.data(), uv.size());
     dp.upload(p.data(), p.size());
     dn.upload(nr.data(), nr.size());
     de.upload(eps.data(), eps.size());
@@ -302,7 +330,7 @@ void Context::preprocess(uint32_t seed) {
         hipEvent_t ev{};
         time_begin(0, ev);
         hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sc, dp.ptr, dn.ptr, de.ptr,
-                           dm.ptr, n, seed, dE.ptr);
+                           dm.ptr, duv.ptr, n, seed, dE.ptr);
         MPSS_HIP(hipGetLastError());
         time_end(0, ev, 0);
         irradiance_.resize((size_t)n * NB);
@@ -493,6 +521,11 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             ws_xyz_.alloc(total);
             ws_hits_ = total;
         }
+        if (sc.any_tex && ws_tex_hits_ < total) {
+            ws_alb_.alloc(total);
+            ws_frame_.alloc(2 * total);
+            ws_tex_hits_ = total;
+        }
         if (ws_px_ < total / spp) {
             ws_spill_.alloc(total / spp);
             ws_px_ = total / spp;
@@ -505,7 +538,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         for (size_t k = pi; k < pe; ++k) {
             const TileBatch &tb = pieces[k].tb;
             SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
-                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
             hipLaunchKernelGGL(primary_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0,
                                stream, sc, tb, rec);
             off += tb.nsamples;
@@ -513,7 +546,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         time_end(stream, ev, 1);
         {
             SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
-                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
             int ns_max = 1;
             for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
             const int64_t lanes = total * std::max<int64_t>(1, (int64_t)scene_.lights.size()) * ns_max;
@@ -531,6 +564,9 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 inf_st = ws_st_.ptr;
             }
             time_begin(stream, ev);
+            if (sc.any_tex)
+                hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
+                                   rec, spp, seed, (int)total);
             if (!scene_.lights.empty()) {
                 hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream,
                                    sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
@@ -562,7 +598,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         time_begin(stream, ev);
         {
             SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
-                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
             hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
                                bp, (int)total);
             if (sc.n_infinite > 0)
@@ -572,7 +608,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         for (size_t k = pi; k < pe; ++k) {
             const TileBatch &tb = pieces[k].tb;
             SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
-                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr};
+                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
             const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
             hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec,
                                pieces[k].out, tw);

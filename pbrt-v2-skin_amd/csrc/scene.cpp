@@ -3,6 +3,7 @@
 #include "scene.h"
 
 #include "geom.h"
+#include "texture.h"
 
 #include <algorithm>
 #include <atomic>
@@ -267,7 +268,7 @@ MeshView mesh_view(const Mesh &m) {
 }
 
 void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter, std::vector<SurfacePoint> &out,
-                               int nthreads) {
+                               int nthreads, const TexView *const *bump) {
     out.clear();
     struct Job {
         int mesh, t0, t1;
@@ -306,11 +307,19 @@ void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter
                     SurfacePoint sp;
                     const V3 p = bc_point(bc, v0, v1, v2);
                     sp.p[0] = p.x; sp.p[1] = p.y; sp.p[2] = p.z;
-                    // GetDifferentialGeometries(bc) -> dgShading; Bump with no map copies it (material.cpp:107-114)
+                    // GetDifferentialGeometries(bc) -> dgGeom, dgShading (no differentials); Bump with
+                    // no map copies dgShading (material.cpp:107-114)
                     const ShadingFrame fr = tri_shading(mv, t, p, bc.b0, bc.b1, bc.b2);
                     sp.u = fr.u;
                     sp.v = fr.v;
-                    sp.n[0] = fr.nn.x; sp.n[1] = fr.nn.y; sp.n[2] = fr.nn.z;
+                    V3 n = fr.nn;
+                    const TexView *bt = bump ? bump[m.material] : nullptr;
+                    if (bt) {
+                        const UVDiff g{fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
+                        V3 dpdu_b;
+                        bump_frame(*bt, g, fr.ss, fr.ts, fr.dndu, fr.dndv, fr.nn, fr.ng, mv.flip, dpdu_b, n);
+                    }
+                    sp.n[0] = n.x; sp.n[1] = n.y; sp.n[2] = n.z;
                     sp.material = m.material;
                     sp.area = .5f * length(cross(s1 - s0, s2 - s0));
                     sp.ray_eps = min_dist / 10.f;

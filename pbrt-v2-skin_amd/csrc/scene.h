@@ -82,7 +82,10 @@ static_assert(sizeof(SurfacePoint) == 44, "SurfacePoint matches the reference's 
 
 // TriangleMesh::TessellateSurfacePoints over every mesh in order (trianglemesh.cpp:187-257,
 // tessellator 265-318, matching 321-351; driver surfacepoints.cpp:301-333).
+// bump (nullable): per material id, its "bumpmap" ImageTexture (host view) or null; a bumped
+// material's points carry the bump-mapped normal (BumpMapping::Bump, trianglemesh.cpp:240-245).
+struct TexView;
 void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter, std::vector<SurfacePoint> &out,
-                               int nthreads = 0);
+                               int nthreads = 0, const TexView *const *bump = nullptr);
 
 }  // namespace mpss

@@ -64,6 +64,14 @@ class LayeredSkin(C.Structure):
                 ("double_ref_sslf", C.c_int)]
 
 
+class Imagemap(C.Structure):
+    """mpss_imagemap (Texture "imagemap" params, textures/imagemap.cpp:110-180)."""
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("texels", vp), ("is_float", C.c_int),
+                ("shift", C.c_float), ("scale", C.c_float), ("gamma", C.c_float), ("wrap", C.c_int),
+                ("trilinear", C.c_int), ("max_anisotropy", C.c_float), ("uscale", C.c_float), ("vscale", C.c_float),
+                ("udelta", C.c_float), ("vdelta", C.c_float)]
+
+
 def _sig(name, res, args):
     f = getattr(_lib, name)
     f.restype = res
@@ -104,6 +112,12 @@ _sig("mpss_mc_profile", C.c_int, [vp, f32p, C.c_int, C.c_float, C.c_int, C.c_uin
                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64), vp])
 _sig("mpss_host_tessellate", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32,
                                        C.c_float, C.c_int, vp, u32p])
+_sig("mpss_imagemap_defaults", None, [C.POINTER(Imagemap)])
+_sig("mpss_add_imagemap", C.c_int, [vp, C.POINTER(Imagemap), u32p])
+_sig("mpss_set_material_textures", C.c_int, [vp, u32, C.c_int32, C.c_int32])
+_sig("mpss_host_tessellate_bumped", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int,
+                                              u32, C.c_float, C.c_int, vp, vp, u32p])
+_sig("mpss_host_imagemap_lookup", C.c_int, [C.POINTER(Imagemap), u32, f32p, f32p])
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
@@ -152,6 +166,45 @@ def default_skin(**kw):
     return m
 
 
+_WRAP = {"repeat": 0, "black": 1, "clamp": 2}
+
+
+def imagemap(texels=None, is_float=False, shift=0.0, scale=1.0, gamma=1.0, wrap="repeat", trilinear=False,
+             maxanisotropy=8.0, uscale=1.0, vscale=1.0, udelta=0.0, vdelta=0.0):
+    """An mpss_imagemap for an (H, W, 3) texel array (ReadImage's RGB, mpss.imageio), or for an
+    image that could not be read (texels None: the reference's one-valued map). Returns (struct,
+    the array it points at -- keep it alive while the struct is used)."""
+    t = Imagemap()
+    _lib.mpss_imagemap_defaults(C.byref(t))
+    arr = None
+    if texels is not None:
+        arr = np.ascontiguousarray(texels, np.float32)
+        if arr.ndim != 3 or arr.shape[2] != 3:
+            raise ValueError("texels must be (height, width, 3)")
+        t.height, t.width = arr.shape[:2]
+        t.texels = arr.ctypes.data
+    t.is_float = int(bool(is_float))
+    t.shift, t.scale, t.gamma = float(shift), float(scale), float(gamma)
+    if wrap not in _WRAP:
+        raise ValueError("wrap mode %r" % wrap)
+    t.wrap = _WRAP[wrap]
+    t.trilinear = int(bool(trilinear))
+    t.max_anisotropy = float(maxanisotropy)
+    t.uscale, t.vscale, t.udelta, t.vdelta = float(uscale), float(vscale), float(udelta), float(vdelta)
+    return t, arr
+
+
+def host_imagemap_lookup(tex, uvd):
+    """ImageTexture::Evaluate of the product's host code: tex = imagemap(...) kwargs dict;
+    uvd (n, 6) = u, v, dudx, dvdx, dudy, dvdy -> (n, 3) MIPMap values."""
+    t, keep = imagemap(**tex)
+    uvd = np.ascontiguousarray(uvd, np.float32).reshape(-1, 6)
+    out = np.zeros((len(uvd), 3), np.float32)
+    check(_lib.mpss_host_imagemap_lookup(C.byref(t), len(uvd), uvd, out))
+    del keep
+    return out
+
+
 # SurfacePoint record, the "pointsfile" format (renderers/surfacepoints.h:45-55), 44 B.
 SURFACE_POINT = np.dtype([("p", "<f4", 3), ("n", "<f4", 3), ("u", "<f4"), ("v", "<f4"), ("material", "<u4"),
                           ("area", "<f4"), ("ray_eps", "<f4")])
@@ -165,17 +218,23 @@ def host_from_rgb(rgb, illuminant=False):
     return out
 
 
-def host_tessellate(P, idx, o2w, w2o, min_dist, N=None, S=None, uv=None, flip=False, material=0, incenter=False):
+def host_tessellate(P, idx, o2w, w2o, min_dist, N=None, S=None, uv=None, flip=False, material=0, incenter=False,
+                    bump=None):
+    """TessellateSurfacePoints of one mesh by the product's host code; bump: imagemap(...) kwargs
+    dict of a float "bumpmap" texture, or None."""
     P = np.ascontiguousarray(P, np.float32).reshape(-1, 3)
     idx = np.ascontiguousarray(idx, np.int32).reshape(-1, 3)
     opt = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (N, S, uv)]
     args = [len(P), P] + [None if a is None else a.ctypes.data for a in opt] + \
         [len(idx), idx.ctypes.data_as(C.POINTER(C.c_int32)), np.ascontiguousarray(o2w, np.float32),
          np.ascontiguousarray(w2o, np.float32), int(flip), material, min_dist, int(incenter)]
+    bt, keep = imagemap(**bump) if bump is not None else (None, None)
+    args.append(C.byref(bt) if bt is not None else None)
     n = C.c_uint32(0)
-    check(_lib.mpss_host_tessellate(*args, None, C.byref(n)))
+    check(_lib.mpss_host_tessellate_bumped(*args, None, C.byref(n)))
     out = np.zeros(n.value, SURFACE_POINT)
-    check(_lib.mpss_host_tessellate(*args, out.ctypes.data, C.byref(n)))
+    check(_lib.mpss_host_tessellate_bumped(*args, out.ctypes.data, C.byref(n)))
+    del keep
     return out
 
 
@@ -288,6 +347,17 @@ class Context:
                                  len(idx), idx.ctypes.data_as(C.POINTER(C.c_int32)),
                                  np.ascontiguousarray(o2w, np.float32), np.ascontiguousarray(w2o, np.float32),
                                  int(reverse), material))
+
+    def add_imagemap(self, **tex):
+        """Texture "imagemap" (see mpss.imagemap for the keywords); returns its texture id."""
+        t, keep = imagemap(**tex)
+        tid = C.c_uint32(0)
+        check(_lib.mpss_add_imagemap(self.h, C.byref(t), C.byref(tid)))
+        del keep
+        return tid.value
+
+    def set_material_textures(self, material, albedo=-1, bump=-1):
+        check(_lib.mpss_set_material_textures(self.h, material, albedo, bump))
 
     def add_sphere_light(self, center, radius, Lemit, nsamples=1):
         check(_lib.mpss_add_sphere_light(self.h, np.ascontiguousarray(center, np.float32), radius,

@@ -8,7 +8,7 @@ for the directives scenes/skin.pbrt and its relatives contain:
   Sampler (pixelsamples), SurfaceIntegrator "multipolesubsurface" (maxdepth, maxerror,
   minsampledistance, mix, showirradiancepoints, incenter), WorldBegin/WorldEnd,
   AttributeBegin/End, TransformBegin/End, Translate, Rotate, Scale, Identity,
-  Texture "constant", Material "layeredskin", AreaLightSource "area", LightSource "infinite"
+  Texture "constant" / "imagemap" (albedo, bumpmap), Material "layeredskin", AreaLightSource "area", LightSource "infinite"
   (L, scale, nsamples, mapname: .exr / .pfm / .tga via mpss.imageio), Shape "sphere" (as an area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
   package's stand-in for huge inline arrays, see tools/make_scene.py), Include.
 
@@ -250,9 +250,7 @@ def load(path, **override):
                     if cls != "box" or ps.one("xwidth", 0.5) != 0.5 or ps.one("ywidth", 0.5) != 0.5:
                         raise ValueError("only the default 0.5-wide box filter is supported")
                 elif d == "Texture":
-                    if cls != "constant":
-                        raise ValueError("texture %r: only constant textures are available (DESIGN.md)" % cls)
-                    textures[name] = ps.find("value", [1.0])
+                    textures[name] = _texture(cls, _kind, ps, base)
                 elif d == "Material":
                     if cls != "layeredskin":
                         state["material"] = ("other", cls)
@@ -286,6 +284,38 @@ def _rgb3(v):
     return v * 3 if len(v) == 1 else v
 
 
+def _texture(cls, typ, ps, base):
+    """Texture "name" "color"|"spectrum"|"float" "constant"|"imagemap" (api.cpp pbrtTexture ->
+    CreateConstant*Texture / CreateImage*Texture, textures/imagemap.cpp:110-180). An imagemap keeps
+    the mpss.imagemap keywords; its file is read with mpss.imageio (FindFilename: relative to the
+    scene file); a file that cannot be read gives the reference's one-valued map (texels None)."""
+    if typ not in ("color", "spectrum", "float"):
+        raise ValueError("texture type %r" % typ)
+    if cls == "constant":
+        return dict(cls="constant", type=typ, value=ps.find("value", [1.0]))
+    if cls != "imagemap":
+        raise ValueError("texture %r: only constant and imagemap textures are on this path (DESIGN.md)" % cls)
+    mapping = ps.one("mapping", "uv")
+    if mapping != "uv":
+        raise ValueError("imagemap mapping %r: only the default uv mapping is on this path" % mapping)
+    fn = ps.one("filename", "")
+    path = fn if os.path.isabs(fn) else os.path.join(base, fn)
+    texels = None
+    if fn and os.path.exists(path):
+        from mpss import imageio
+        texels = imageio.read_image(path)
+    else:
+        import warnings
+        warnings.warn("imagemap %r could not be read: one-valued texture (imagemap.cpp:76-81)" % fn)
+    tex = dict(texels=texels, is_float=typ == "float", shift=float(ps.one("shift", 0.0)),
+               scale=float(ps.one("scale", 1.0)), gamma=float(ps.one("gamma", 1.0)), wrap=ps.one("wrap", "repeat"),
+               trilinear=ps.one("trilinear", "false") in ("true", True, 1),
+               maxanisotropy=float(ps.one("maxanisotropy", 8.0)), uscale=float(ps.one("uscale", 1.0)),
+               vscale=float(ps.one("vscale", 1.0)), udelta=float(ps.one("udelta", 0.0)),
+               vdelta=float(ps.one("vdelta", 0.0)))
+    return dict(cls="imagemap", type=typ, tex=tex, filename=fn)
+
+
 def _skin_params(ps, textures):
     p = {}
     for k in _SKIN_FLOATS:
@@ -300,9 +330,24 @@ def _skin_params(ps, textures):
             typ, vals = ps[k]
             if typ == "texture":
                 if vals[0] not in textures:
-                    raise ValueError("texture %r is not a constant texture" % vals[0])
-                vals = textures[vals[0]]
+                    raise ValueError("texture %r is not defined" % vals[0])
+                t = textures[vals[0]]
+                if t["type"] == "float":
+                    raise ValueError("%s needs a spectrum texture, %r is a float texture" % (k, vals[0]))
+                if t["cls"] == "imagemap":
+                    if k != "albedo":
+                        raise ValueError("an imagemap %s is outside this path (DESIGN.md); albedo and bumpmap "
+                                         "take image textures" % k)
+                    p["albedo_tex"] = t["tex"]
+                    continue
+                vals = t["value"]
             p[k] = _rgb3(vals)
+    if "bumpmap" in ps:
+        typ, vals = ps["bumpmap"]
+        t = textures.get(vals[0]) if typ == "texture" else None
+        if t is None or t["cls"] != "imagemap" or t["type"] != "float":
+            raise ValueError("bumpmap: only a float imagemap texture is on this path")
+        p["bump_tex"] = t["tex"]
     for k in ("desiredlength",):
         if k in ps:
             p["desired_length"] = int(ps.one(k))
@@ -339,7 +384,7 @@ def _shape(sc, cls, ps, ctm, state, base):
     if state["material"] is None or state["material"][0] != "layeredskin":
         raise ValueError("meshes need a layeredskin material on this path")
     mat = state["material"][1]
-    if mat not in sc.materials:
+    if not any(x is mat for x in sc.materials):  # one material per Material directive
         sc.materials.append(mat)
     o2w = ctm
     P = np.asarray(arr["P"], np.float32).reshape(-1, 3).astype(np.float64)
@@ -347,7 +392,8 @@ def _shape(sc, cls, ps, ctm, state, base):
     sc.meshes.append(dict(P=Pw, N=arr.get("N"), S=arr.get("S"), uv=arr.get("uv"),
                           indices=np.asarray(arr["indices"], np.int32).reshape(-1, 3),
                           o2w=o2w.astype(np.float32), w2o=np.linalg.inv(o2w).astype(np.float32),
-                          reverse=state["reverse"], material=sc.materials.index(mat)))
+                          reverse=state["reverse"],
+                          material=next(i for i, x in enumerate(sc.materials) if x is mat)))
 
 
 def subdivide_mesh(me, levels):
@@ -435,11 +481,16 @@ def build_context(sc, **cfg_kw):
     ctx = mpss.Context(**integrator_config(sc, **cfg_kw))
     mids = []
     for m in sc.materials:
-        kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
+        kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo", "albedo_tex", "bump_tex")}
         for k in ("Kr", "Kt", "albedo"):
             if k in m:
                 kw[k] = mpss.host_from_rgb(m[k])
         mids.append(ctx.add_layeredskin(mpss.default_skin(**kw)))
+    for m, mid in zip(sc.materials, mids):
+        if m.get("albedo_tex") is not None or m.get("bump_tex") is not None:
+            alb = ctx.add_imagemap(**m["albedo_tex"]) if m.get("albedo_tex") is not None else -1
+            bump = ctx.add_imagemap(**m["bump_tex"]) if m.get("bump_tex") is not None else -1
+            ctx.set_material_textures(mid, alb, bump)
     for me in sc.meshes:
         ctx.add_mesh(me["P"], me["indices"], me["o2w"], me["w2o"], mids[me["material"]], N=me["N"], S=me["S"],
                      uv=me["uv"], reverse=me["reverse"])

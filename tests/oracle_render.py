@@ -43,8 +43,42 @@ def _lib():
     L.o_scene_set_octree.argtypes = [vp, C.c_int, f32p, f32p, f32p, f32p, C.c_float]
     L.o_render_tile.argtypes = [vp, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p]
     L.o_scene_free.argtypes = [vp]
+    L.o_scene_set_material_texture.restype = C.c_int
+    L.o_scene_set_material_texture.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_float, C.c_float,
+                                               C.c_float, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float,
+                                               C.c_float, C.c_float]
+    L.o_imagemap_lookup.restype = C.c_int
+    L.o_imagemap_lookup.argtypes = [C.c_int, C.c_int, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
+                                    C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, f32p, f32p]
     L._render_sigs = True
     return L
+
+
+_WRAP = {"repeat": 0, "black": 1, "clamp": 2}
+
+
+def _tex_args(tex):
+    """(W, H, texels, keep-alive array, params after texels) of an mpss.imagemap kwargs dict."""
+    arr = None if tex.get("texels") is None else np.ascontiguousarray(tex["texels"], np.float32)
+    H, W = (0, 0) if arr is None else arr.shape[:2]
+    rest = [float(tex.get("shift", 0.0)), float(tex.get("scale", 1.0)), float(tex.get("gamma", 1.0)),
+            _WRAP[tex.get("wrap", "repeat")], int(bool(tex.get("trilinear", False))),
+            float(tex.get("maxanisotropy", 8.0)), float(tex.get("uscale", 1.0)), float(tex.get("vscale", 1.0)),
+            float(tex.get("udelta", 0.0)), float(tex.get("vdelta", 0.0))]
+    return W, H, (None if arr is None else arr.ctypes.data), arr, rest
+
+
+def imagemap_lookup(tex, uvd):
+    """The oracle's ImageTexture::Evaluate (oracle/texture.c) at uvd (n, 6) = u, v, dudx, dvdx,
+    dudy, dvdy; tex = mpss.imagemap kwargs dict."""
+    W, H, ptr, arr, rest = _tex_args(tex)
+    uvd = np.ascontiguousarray(uvd, np.float32).reshape(-1, 6)
+    out = np.zeros((len(uvd), 3), np.float32)
+    _lib().o_imagemap_lookup(W, H, ptr, int(bool(tex.get("is_float", False))), *rest, len(uvd), uvd, out)
+    return out
+
+
+_TEXKEYS = ("Kr", "Kt", "albedo", "albedo_tex", "bump_tex")
 
 
 def _opt(a):
@@ -59,7 +93,7 @@ def tables_from_host(sc, mpss):
     """Material tables from the product's host builders (CPU only; no device needed)."""
     out = []
     for m in sc.materials:
-        kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
+        kw = {k: v for k, v in m.items() if k not in _TEXKEYS}
         skin = mpss.default_skin(**kw)
         tab, rcp, _ = mpss.host_build_profile(*mpss.host_skin_layers(skin), desired_length=skin.desired_length,
                                               lerp=bool(skin.lerp_on_thin_slab))
@@ -82,7 +116,7 @@ class OracleScene:
                                   np.ascontiguousarray(c2w, np.float32))
         self._keep = []
         for mid, m in enumerate(sc.materials):
-            kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo")}
+            kw = {k: v for k, v in m.items() if k not in _TEXKEYS}
             skin = mpss.default_skin(**kw)
             Kr = mpss.host_from_rgb(m["Kr"]) if "Kr" in m else np.ones(NB, np.float32)
             Kt = mpss.host_from_rgb(m["Kt"]) if "Kt" in m else np.ones(NB, np.float32)
@@ -91,6 +125,10 @@ class OracleScene:
             L.o_scene_add_material(self.h, Kr, Kt, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
                                    int(skin.double_ref_sslf), rho, len(rho), 0,
                                    np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
+            for which, key in ((0, "albedo_tex"), (1, "bump_tex")):
+                if m.get(key) is not None:
+                    W, H, ptr, arr, rest = _tex_args(m[key])
+                    assert L.o_scene_set_material_texture(self.h, mid, which, W, H, ptr, *rest) == 0
         for me in sc.meshes:
             N, S, uv = _opt(me["N"]), _opt(me["S"]), _opt(me["uv"])
             self._keep += [N, S, uv]

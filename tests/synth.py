@@ -54,3 +54,26 @@ def morton3(p, bits=10):
         for a in range(3):
             code |= ((q[:, a] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + a)
     return code
+
+
+def texture_texels(w, h, seed=3, lo=0.05, hi=1.0):
+    """A (h, w, 3) RGB image like a skin diffuse map: smooth colour bands plus per-texel noise,
+    values in [lo, hi) (ReadImage's float texels)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    base = np.stack([0.5 + 0.4 * np.sin(x / max(w, 1) * 6.3 + k + y / max(h, 1) * 2.1) for k in range(3)], -1)
+    img = lo + (hi - lo) * np.clip(0.8 * base + 0.2 * rng.random((h, w, 3)), 0, 0.999)
+    return img.astype(np.float32)
+
+
+def random_uvd(n, seed=5, scale=0.02, outside=0.1):
+    """(n, 6) lookup points u, v, dudx, dvdx, dudy, dvdy: u, v partly outside [0, 1) (wrap
+    modes), differentials log-uniform over ~4 decades of `scale`, a share of them zero
+    (the irradiance / tessellation lookups) and a share strongly anisotropic."""
+    rng = np.random.default_rng(seed)
+    uv = rng.uniform(-outside, 1 + outside, (n, 2))
+    d = rng.standard_normal((n, 4)) * scale * np.exp(rng.uniform(-4.5, 4.5, (n, 1)))
+    d[rng.random(n) < 0.15] = 0.0
+    an = rng.random(n) < 0.15
+    d[an, 2:] *= 1e-3
+    return np.concatenate([uv, d], 1).astype(np.float32)

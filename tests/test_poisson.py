@@ -63,9 +63,13 @@ def test_oracle_poisson_properties(mpss, oracle, quick):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,md", [("tissue.pbrt", 0.02), ("skin.pbrt", 0.02)])
-def test_poisson_points_gpu_vs_oracle(mpss, oracle, scene, md):
+@pytest.mark.parametrize("scene,md,bump", [("tissue.pbrt", 0.02, False), ("skin.pbrt", 0.02, False),
+                                           ("skin.pbrt", 0.02, True)])
+def test_poisson_points_gpu_vs_oracle(mpss, oracle, scene, md, bump):
+    """bump: a "bumpmap" float imagemap -- candidates carry Bump(hitGeometry, dgShading).nn
+    (surfacepoints.cpp:203-211)."""
     import torch
+    import synth
     from mpss import pbrtscene
     assert torch.cuda.is_available()
     sc = pbrtscene.load(os.path.join(ROOT, "scenes", scene), xres=32, yres=32, spp=1)
@@ -73,6 +77,8 @@ def test_poisson_points_gpu_vs_oracle(mpss, oracle, scene, md):
     sc.integrator["usepoissonpointfinder"] = "true"
     for m in sc.materials:
         m["desired_length"] = 64
+        if bump:
+            m["bump_tex"] = dict(texels=synth.texture_texels(40, 30, seed=12), is_float=True, scale=0.05)
     ctx = pbrtscene.build_context(sc)
     ctx.preprocess(seed=5)
     got = ctx.surface_points()
