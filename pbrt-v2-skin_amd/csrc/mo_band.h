@@ -26,7 +26,8 @@ namespace mpss {
 
 constexpr int kGroups = 8;
 constexpr int kBandBlock = 1024;  // queries per workgroup (16 waves of one band group)
-constexpr int kLdsRd = 4096;      // leading Rd entries of each of the group's 4 bands kept in LDS (64 KB)
+constexpr int kLdsRd = 4096;      // leading Rd entries per band kept in LDS (64 KB: two workgroups per CU)
+constexpr int kLdsRdBig = 10224;  // the same filling one CU's 160 KB (one workgroup per CU)
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -70,7 +71,7 @@ struct BandTree {
     const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
     const float4 *__restrict__ pt_hdr;   // [n_points] {p, area (sign bit: E black)}
     const float4 *__restrict__ band_e;   // [kGroups][n_points]
-    const float *__restrict__ table;     // [NB][L]
+    const float *__restrict__ table;     // [NB][L] + 2 trailing zeros (DeviceProfile::upload)
     const float *__restrict__ rcp;       // [NB]
     BandGroups groups;
     int L, n_nodes, n_points;
@@ -83,42 +84,63 @@ struct BandTree {
 struct __attribute__((aligned(4))) RdPair {
     float a, b;
 };
+typedef float f2v __attribute__((ext_vector_type(2)));  // v_pk_{add,mul}_f32 operands
+typedef __attribute__((address_space(3))) const float lds_float;  // ds_read, never a flat load
 
-// Rd lookups of one record for the lane's 4 bands, straight-line: the 4 pair loads are issued
-// back to back (lanes past a band's profile read a clamped, valid entry and are masked), then
-// consumed -- one memory round trip per record and no divergent branches for the compiler to
-// serialize. t = fract(f) equals f - (float)(uint)f exactly for 0 <= f < 2^24.
-// acc[j] += Rd_j(d2) * e[j] (* w) exactly as sampleProfile + the Mo() product
-// (multipole.cpp:60-73; diffusionutil.h:185,197).
-// The first kLdsRd entries of each band (the near field: leaf points and close clusters, about
-// 40 % of the red bands' lookups) come from the workgroup's LDS copy, the rest from L2.
-template <bool POINT>
-__device__ __forceinline__ void band_rd_accumulate(const float *const tb[4], const float rcp[4], float lm1,
-                                                   uint32_t smax, float d2, const float e[4], float w,
-                                                   float acc[4], const float (*lt)[kLdsRd]) {
+// The lane's view of its group's 4 bands.
+struct BandLane {
+    const float *tb[4];  // band tables (an empty slot reads band 0's with rcp 0; its sum is unused)
+    float rcp[4];
+    uint32_t zero[4];    // tb[j] + zero[j] = the table's trailing zero pair
+    float lm1;           // L - 1: sampleProfile's range end
+    float klim;          // min(KLDS, L) - 1: f < klim <=> the lerp pair is in LDS and in range
+};
+
+// Rd lookups of one record for the lane's 4 bands, accumulated:
+// acc[j] += Rd_j(d2) * e[j] (* w), as sampleProfile + the Mo() product (multipole.cpp:60-73;
+// diffusionutil.h:185,197) -- the same IEEE operations in the same order as the scalar code.
+// lt: the workgroup's LDS copy of the first KLDS entries of each band, rows of KLDS + 2 floats
+// (the last two zero). Per band one wave-uniform choice: if every active lane's pair is in the
+// LDS copy (or the lane is past the profile end), all read LDS; otherwise all read the table
+// (L2). A lane past the profile end reads a zero pair, so its term is (0 * e) * w = +-0 and the
+// running sum (which starts at +0 and is never -0) is unchanged: no masking instruction. The
+// pairs of all 4 bands are requested before any is consumed (one memory round trip per
+// record); the lerp and the products run as packed f32 (two values per instruction).
+template <bool POINT, int KLDS, bool FLAT>
+__device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
+                                                   const float *lt) {
     float f[4];
-    bool ok[4];
     RdPair v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        f[j] = d2 * rcp[j];
-        ok[j] = f[j] < lm1;
-        const uint32_t s = ok[j] ? (uint32_t)f[j] : smax;
-        // two unconditional loads and a select (a branch here makes the compiler merge both
-        // paths into flat loads): lanes served by LDS point their L2 load at one shared line
-        const bool in_lds = s + 1 < (uint32_t)kLdsRd;
-        const uint32_t sl = in_lds ? s : 0u, sg = in_lds ? smax : s;
-        const float la = lt[j][sl], lb = lt[j][sl + 1];
-        const RdPair g = *reinterpret_cast<const RdPair *>(tb[j] + sg);
-        v[j].a = in_lds ? la : g.a;
-        v[j].b = in_lds ? lb : g.b;
+        f[j] = d2 * b.rcp[j];
+        const uint32_t s = (uint32_t)f[j];  // fSegId (the double product is exact: multipole.cpp:63-65)
+        const bool ok = f[j] < b.lm1;
+        const bool in_lds = f[j] < b.klim;  // implies ok
+        if (FLAT) {  // per lane: one flat load whose address is in LDS or in the table
+            const float *src = in_lds ? lt + j * (KLDS + 2) + s : b.tb[j] + (ok ? s : b.zero[j]);
+            v[j] = *reinterpret_cast<const RdPair *>(src);
+        } else if (__builtin_amdgcn_ballot_w64(ok && !in_lds) == 0) {
+            const lds_float *row =
+                (const lds_float *)lt + j * (KLDS + 2) + (in_lds ? s : (uint32_t)KLDS);
+            v[j].a = row[0];
+            v[j].b = row[1];
+        } else {
+            v[j] = *reinterpret_cast<const RdPair *>(b.tb[j] + (ok ? s : b.zero[j]));
+        }
     }
+    float rd[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float t = __builtin_amdgcn_fractf(f[j]);
-        const float rd = (1.f - t) * v[j].a + t * v[j].b;
-        const float val = POINT ? rd * e[j] * w : rd * e[j];
-        acc[j] += ok[j] ? val : 0.f;  // == the masked add: acc starts at +0 and never becomes -0
+        const float t = __builtin_amdgcn_fractf(f[j]);  // == f - (float)(uint)f for 0 <= f < 2^24
+        const f2v p = f2v{1.f - t, t} * f2v{v[j].a, v[j].b};
+        rd[j] = p.x + p.y;  // (1 - t) * T[s] + t * T[s + 1]
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f2v val = f2v{rd[2 * h], rd[2 * h + 1]} * f2v{e[2 * h], e[2 * h + 1]};
+        if (POINT) val = val * f2v{w, w};
+        acc[h] += val;
     }
 }
 
@@ -135,23 +157,24 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
     return below;
 }
 
-template <bool COUNT>
+template <bool COUNT, int KLDS, bool FLAT>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
-                                                 float acc[4], int &k_nodes, int &k_pts, const float (*lt)[kLdsRd]) {
-    float rcp[4];
-    const float *tb[4];
+                                                 float out[4], int &k_nodes, int &k_pts, const float *lt) {
+    BandLane b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = a.groups.band[grp][j];
-        rcp[j] = c >= 0 ? a.rcp[c] : INFINITY;
-        tb[j] = a.table + (size_t)(c >= 0 ? c : 0) * a.L;
-        acc[j] = 0.f;
+        const int cc = c >= 0 ? c : 0;
+        b.rcp[j] = c >= 0 ? a.rcp[c] : 0.f;
+        b.tb[j] = a.table + (size_t)cc * a.L;
+        b.zero[j] = (uint32_t)(NB - cc) * (uint32_t)a.L;
     }
+    b.lm1 = (float)(a.L - 1);
+    b.klim = (float)((a.L < KLDS ? a.L : KLDS) - 1);
+    f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     const float rcp_min = a.groups.rcp_min[grp];
     const float4 *__restrict__ et_g = a.band_et + (size_t)grp * a.n_nodes;
     const float4 *__restrict__ e_g = a.band_e + (size_t)grp * a.n_points;
-    const float lm1 = (float)(a.L - 1);
-    const uint32_t smax = (uint32_t)(a.L - 2);  // clamped (masked) index for out-of-range bands
     int resume = valid ? 0 : 0x7fffffff;
     int node = 0;
     while (node < a.n_nodes) {
@@ -161,6 +184,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         bool open = false;
         if (node >= resume) {
             if (COUNT) ++k_nodes;
+            // distance from p to the node box per axis (0 inside the slab)
             const float bx = fmaxf(fmaxf(h.bminx - px, px - h.bmaxx), 0.f);
             const float by = fmaxf(fmaxf(h.bminy - py, py - h.bmaxy), 0.f);
             const float bz = fmaxf(fmaxf(h.bminz - pz, pz - h.bmaxz), 0.f);
@@ -170,13 +194,13 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             } else {
                 const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
                 const float d2 = dx * dx + dy * dy + dz * dz;
-                const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
-                                    pz >= h.bminz && pz <= h.bmaxz;
+                // nodeBound.Inside(p) <=> every per-axis distance is 0 (the subtractions' signs are exact)
+                const bool inside = fmaxf(fmaxf(bx, by), bz) == 0.f;
                 if (dw_below(h.sum_area, d2, a.max_error) && !inside) {
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-                    band_rd_accumulate<false>(tb, rcp, lm1, smax, d2, e, 1.f, acc, lt);
+                    band_rd_accumulate<false, KLDS, FLAT>(b, d2, e, 1.f, acc, lt);
                 } else {
                     open = true;
                 }
@@ -186,7 +210,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         if (h.leaf_first >= 0) {
             if (any_open) {
                 // the leaf's non-black points only (DeviceOctree::upload puts them first, h.pad)
-                float lacc[4] = {0.f, 0.f, 0.f, 0.f};
+                f2v lacc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
                 const int live = (int)h.pad;
                 for (int i = 0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
@@ -197,10 +221,10 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-                    band_rd_accumulate<true>(tb, rcp, lm1, smax, d2, e, ph.w, lacc, lt);
+                    band_rd_accumulate<true, KLDS, FLAT>(b, d2, e, ph.w, lacc, lt);
                 }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] += lacc[j];
+                acc[0] += lacc[0];
+                acc[1] += lacc[1];
             }
             if (open) resume = skip;
             node = skip;
@@ -210,6 +234,10 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             node = skip;
         }
     }
+    out[0] = acc[0].x;
+    out[1] = acc[0].y;
+    out[2] = acc[1].x;
+    out[3] = acc[1].y;
 }
 #endif
 

@@ -210,16 +210,16 @@ struct BandArgs {
     unsigned long long *__restrict__ counts;  // render COUNT: [2 * kGroups]
 };
 
-template <bool COUNT>
-__global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
-    __shared__ float lt[4][kLdsRd];
+template <bool COUNT, int KLDS, bool FLAT>
+__device__ __forceinline__ void mo_band_body(const BandArgs &a, float *lt) {
     const int grp = (int)(blockIdx.x & (kGroups - 1));
     const int base = (int)(blockIdx.x / kGroups) * kBandBlock;
     const int nq = a.count ? *a.count : a.nq;
     if (base >= nq) return;
-    for (int i = (int)threadIdx.x; i < 4 * kLdsRd; i += kBandBlock) {  // the group's near-field Rd entries
-        const int j = i / kLdsRd, k = i % kLdsRd, c = a.t.groups.band[grp][j];
-        lt[j][k] = (c >= 0 && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+    // the group's near-field Rd entries, KLDS per band + a zero pair
+    for (int i = (int)threadIdx.x; i < 4 * (KLDS + 2); i += kBandBlock) {
+        const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
+        lt[i] = (c >= 0 && k < KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
     }
     __syncthreads();
     const int q = base + (int)threadIdx.x;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
     }
     float acc[4];
     int kn = 0, kp = 0;
-    mo_band_traverse<COUNT>(a.t, grp, px, py, pz, live, acc, kn, kp, lt);
+    mo_band_traverse<COUNT, KLDS, FLAT>(a.t, grp, px, py, pz, live, acc, kn, kp, lt);
     if (!live) return;
     if (a.out4) {
         a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -262,6 +262,52 @@ __global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
             atomicAdd(&a.counts[2 * grp + 1], (unsigned long long)kp);
         }
     }
+}
+
+// Variants of one body: 64 KB of LDS (two workgroups = 32 waves a CU) with wave-uniform LDS /
+// table reads; the same with one per-lane flat load (address in LDS or in the table); one
+// workgroup a CU with 160 KB of LDS (a larger near field in LDS).
+template <bool COUNT>
+__global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
+    __shared__ float lt[4 * (kLdsRd + 2)];
+    mo_band_body<COUNT, kLdsRd, false>(a, lt);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(kBandBlock) void mo_band_kernel_flat(BandArgs a) {
+    __shared__ float lt[4 * (kLdsRd + 2)];
+    mo_band_body<COUNT, kLdsRd, true>(a, lt);
+}
+template <bool COUNT>
+__global__ __launch_bounds__(kBandBlock) void mo_band_kernel_big(BandArgs a) {
+    __shared__ float lt[4 * (kLdsRdBig + 2)];
+    mo_band_body<COUNT, kLdsRdBig, false>(a, lt);
+}
+
+// MPSS_MO_BAND selects the variant (0 default, 1 flat, 2 big LDS) -- a tuning knob
+int band_variant() {
+    const char *v = getenv("MPSS_MO_BAND");
+    return v ? atoi(v) : 0;
+}
+
+void launch_band(const BandArgs &a, unsigned blocks, bool count, hipStream_t stream) {
+    const int var = band_variant();
+    if (var == 1) {
+        if (count)
+            hipLaunchKernelGGL(mo_band_kernel_flat<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mo_band_kernel_flat<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+    } else if (var == 2) {
+        if (count)
+            hipLaunchKernelGGL(mo_band_kernel_big<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mo_band_kernel_big<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+    } else {
+        if (count)
+            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+    }
+    MPSS_HIP(hipGetLastError());
 }
 
 __global__ void band_permute_kernel(const float *__restrict__ rows, int n, BandGroups g, float4 *__restrict__ out) {
@@ -339,7 +385,11 @@ void DeviceOctree::upload(const FlatOctree &t) {
 }
 
 void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
-    table.upload(tab, (size_t)NB * len);
+    // two zero floats after the last band: the sharded gather's read for "past the profile end"
+    const size_t n = (size_t)NB * len;
+    if (table.n != n + 2) table.alloc(n + 2);
+    MPSS_HIP(hipMemcpy(table.ptr, tab, n * sizeof(float), hipMemcpyHostToDevice));
+    MPSS_HIP(hipMemset(table.ptr + n, 0, 2 * sizeof(float)));
     rcp.upload(rcp_, NB);
     L = len;
     rcp_min = rcp_[0];
@@ -374,11 +424,7 @@ void launch_mo_band(DeviceOctree &t, const DeviceProfile &p, float max_error, in
     a.out4 = out4;
     a.counts = counts;
     const unsigned blocks = (unsigned)((nq_max + kBandBlock - 1) / kBandBlock) * kGroups;
-    if (counts)
-        hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-    else
-        hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-    MPSS_HIP(hipGetLastError());
+    launch_band(a, blocks, counts != nullptr, stream);
 }
 
 void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_error, int nq, const float *queries,
@@ -417,11 +463,7 @@ void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_
         b.out_stride = out_stride;
         b.counters = counters;
         const unsigned blocks = (unsigned)((nq + kBandBlock - 1) / kBandBlock) * kGroups;
-        if (count)
-            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, b);
-        else
-            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, b);
-        MPSS_HIP(hipGetLastError());
+        launch_band(b, blocks, count, stream);
         return;
     }
     if (!exact) {
