@@ -199,7 +199,12 @@ def main():
                            "mo_gbs": round(mo_gbs, 1), "mo_sss_samples": cnt["sss_samples"],
                            "mo_record_visits_per_sss_sample": round((cnt["mo_nodes"] + cnt["mo_points"]) /
                                                                     max(1, cnt["sss_samples"]), 2),
-                           "mo_group_visits": [a + b for a, b in zip(cnt["group_nodes"], cnt["group_points"])]},
+                           "mo_group_visits": [a + b for a, b in zip(cnt["group_nodes"], cnt["group_points"])],
+                           "mo_lane_efficiency": round((cnt["mo_nodes"] + cnt["mo_points"]) /
+                                                       max(1, 64 * (cnt["mo_wave_node_iters"] +
+                                                                    cnt["mo_wave_point_iters"])), 4),
+                           "mo_lookup_near_fraction": [round(x / max(1, cnt["mo_lookups"]), 4)
+                                                       for x in cnt["mo_lookups_near"]]},
                 "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if a.out and rank == 0:

@@ -22,6 +22,11 @@
  * Error convention: every entry point returns MPSS_OK (0) or a negative MPSS_ERR_* code and
  * records a message retrievable with mpss_last_error() (thread-local). No exception ever
  * crosses the boundary; the reference's Severe()/abort() paths become error returns.
+ * Thread safety (SamplerRendererTask calls Li from every worker thread, parallel.cpp:800-878):
+ * mpss_mo_batch, mpss_render_tile(s) and the query functions may be called concurrently from
+ * several host threads, each with its own stream; every call takes its own device workspace.
+ * Calls that change the context (materials, meshes, lights, camera, points, preprocess) are
+ * serialized against each other and must not race with renders that depend on what they change.
  * Pointers named *_dev are HIP device pointers (e.g. torch CUDA tensors' data_ptr());
  * all other arrays are caller-owned host memory that is copied in.
  * stream: a hipStream_t (NULL = legacy default stream).
@@ -192,6 +197,12 @@ int mpss_render_tile(mpss_ctx *ctx, int spp, uint32_t seed, int x0, int x1, int 
 int mpss_render_tiles(mpss_ctx *ctx, int spp, uint32_t seed, int n, const int32_t *rects, float *const *xyzw_dev,
                       void *stream);
 
+/* Cost probe for dealing tiles to GPUs (the bench's multi-GPU path; not a reference entry point):
+ * one camera ray through the centre of every pixel, counted per rectangle (rects[4*i..] = x0, x1,
+ * y0, y1): sss_hits[i] = rays that hit a surface with a MultipoleBSSRDF (they will run the Mo()
+ * gather), surf_hits[i] = rays that hit any mesh. Synchronous; identical counts on every device. */
+int mpss_tile_costs(mpss_ctx *ctx, int n, const int32_t *rects, int64_t *sss_hits, int64_t *surf_hits);
+
 /* Accumulated per-kernel statistics of mpss_render_tile / mpss_preprocess since the last reset.
  * Kernel times need kernel_timing = 1; traversal counts need count_traversal = 1. Synchronizes. */
 typedef struct {
@@ -205,6 +216,12 @@ typedef struct {
     int32_t group_bands[8][4];                /* band indices of each group (-1: empty slot) */
     double ms_direct;     /* shading + direct lighting kernel (ms_camera: primary rays only) */
     int64_t n_direct;
+    /* count_traversal: iterations of the gather's node loop and leaf-point loop summed over waves
+     * (one wave = 64 queries x one band group); 64 x iterations / visits = 1 / lane efficiency */
+    int64_t mo_wave_node_iters, mo_wave_point_iters;
+    /* count_traversal: Rd table lookups inside the profile (lane x band), and how many of them
+     * fall in the first 4096 / 8192 / 16384 entries of their band */
+    int64_t mo_lookups, mo_lookups_near[3];
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal after creation (instrumented passes). */

@@ -183,6 +183,7 @@ int o_envmap_build(int W, int H, const float *img, o_envmap *m) {
     float filter = 1.f / (W > H ? W : H);
     for (int v = 0; v < H; ++v) {
         float vp = (float)v / (float)H;
+        /* infinite.cpp:94 with pbrt's float M_PI (core/pbrt.h:193-196): a float argument */
         float sin_theta = (float)sin((double)(PI_F * (float)(v + .5f) / (float)H));
         for (int u = 0; u < W; ++u) {
             float up = (float)u / (float)W, rgb[3];

@@ -22,16 +22,91 @@ Context::Context(const mpss_config &cfg) : cfg_(cfg) {
 
 Context::~Context() {
     (void)hipSetDevice(cfg_.device);
+    (void)hipDeviceSynchronize();
     for (const Timed &t : timed_) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
     }
 }
 
+RenderWorkspace::~RenderWorkspace() {
+    if (done) {
+        (void)hipSetDevice(device);
+        (void)hipEventSynchronize(done);
+        (void)hipEventDestroy(done);
+    }
+}
+
+// A free workspace from the pool, or a new one (mu_ held).
+RenderWorkspace *Context::acquire_ws() {
+    if (!ws_free_.empty()) {
+        RenderWorkspace *w = ws_free_.back().release();
+        ws_free_.pop_back();
+        return w;
+    }
+    auto w = std::make_unique<RenderWorkspace>();
+    w->device = cfg_.device;
+    MPSS_HIP(hipEventCreateWithFlags(&w->done, hipEventDisableTiming));
+    w->work.alloc(kGroups);
+    w->count.alloc(1);
+    return w.release();
+}
+
+// Back to the pool after its last kernel on `stream` (the next user waits on `done`).
+void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) {
+    const hipError_t e = hipEventRecord(ws->done, stream);
+    ws->pending = e == hipSuccess;
+    std::lock_guard<std::mutex> g(mu_);
+    ws_free_.emplace_back(ws);
+    MPSS_HIP(e);
+}
+
+void Context::ensure_layouts() {
+    if (!have_octree_) return;
+    for (const auto &m : materials_) dev_octree_.ensure_layout(m->dev_profile.groups);
+}
+
+// SubsurfaceOctreeNode::Mo for a batch of points (mpss_mo_batch). The octree, profile and band
+// layout are read-only here; the chunk counters of the sharded gather come from a pooled
+// workspace, so concurrent calls on different streams share nothing they write.
+void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, int32_t *counters_dev,
+                       hipStream_t stream) {
+    activate();
+    RenderWorkspace *ws = nullptr;
+    const BandLayout *layout = nullptr;
+    const Material *m = nullptr;
+    int mode;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!have_octree_) throw Error(MPSS_ERR_INVALID, "no irradiance points: call mpss_set_irradiance_points first");
+        if (mid >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(mid));
+        m = materials_[mid].get();
+        mode = cfg_.exact_mo;
+        if (mode == 0) {
+            layout = &dev_octree_.ensure_layout(m->dev_profile.groups);
+            ws = acquire_ws();
+        }
+    }
+    if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
+    try {
+        launch_mo_gather(dev_octree_, layout, m->dev_profile, max_error_, q, p_dev, out_dev, NB, counters_dev,
+                         ws ? ws->work.ptr : nullptr, stream, mode);
+    } catch (...) {
+        if (ws) release_ws(ws, stream);
+        throw;
+    }
+    if (ws) release_ws(ws, stream);
+}
+
 void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }
+
+// Material ids travel in 8 bits of the render path's per-sample records (render.h REC_MAT_SHIFT).
+constexpr size_t kMaxMaterials = 256;
 
 uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (materials_.size() >= kMaxMaterials) throw Error(MPSS_ERR_INVALID, "at most 256 materials per context");
     auto mat = std::make_unique<Material>();
     SkinParams sp;
     sp.roughness = m.roughness;
@@ -63,12 +138,16 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));
+    scene_dirty_ = true;
+    ensure_layouts();
     return (uint32_t)materials_.size() - 1;
 }
 
 uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float *rcp, const float *rho,
                                       uint32_t n_rho, const float *albedo, bool is_mc) {
     activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (materials_.size() >= kMaxMaterials) throw Error(MPSS_ERR_INVALID, "at most 256 materials per context");
     auto mat = std::make_unique<Material>();
     mat->profile.length = (int)len;
     mat->profile.table.assign(rd, rd + (size_t)NB * len);
@@ -87,6 +166,8 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));
+    scene_dirty_ = true;
+    ensure_layouts();
     return (uint32_t)materials_.size() - 1;
 }
 
@@ -132,12 +213,14 @@ std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m) {
 }
 
 uint32_t Context::add_imagemap(const mpss_imagemap &m) {
+    std::lock_guard<std::mutex> g(mu_);
     textures_.push_back(build_imagemap(m));
     scene_dirty_ = true;
     return (uint32_t)textures_.size() - 1;
 }
 
 void Context::set_material_textures(uint32_t material, int albedo, int bump) {
+    std::lock_guard<std::mutex> g(mu_);
     if (material >= materials_.size()) throw Error(MPSS_ERR_INVALID, "set_material_textures: unknown material id");
     auto check = [&](int id, bool want_float, const char *what) {
         if (id < 0) return;
@@ -162,15 +245,25 @@ std::vector<const TexView *> Context::host_bump_views() const {
 }
 
 const Material &Context::material(uint32_t id) const {
+    std::lock_guard<std::mutex> g(mu_);
     if (id >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(id));
     return *materials_[id];
 }
 
 void Context::set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area) {
     activate();
+    std::lock_guard<std::mutex> g(mu_);
+    MPSS_HIP(hipDeviceSynchronize());  // no gather of the old octree may still be running
+    build_octree_locked(n, p, nrm, E, area);
+}
+
+// SubsurfaceOctreeNode::Insert / InitHierarchy over the points, the device copy and every
+// material's band layout (mu_ held).
+void Context::build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area) {
     build_octree(n, p, nrm, E, area, host_octree_);
     dev_octree_.upload(host_octree_);
     have_octree_ = true;
+    ensure_layouts();
 }
 
 const DeviceOctree &Context::octree() const {

@@ -2,6 +2,7 @@
 // MultipoleSubsurfaceIntegrator instance; reference integrators/multipolesubsurface.h:36-80).
 #pragma once
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/mpss.h"
@@ -49,6 +50,24 @@ struct ImageTexture {
 // or the one-valued map when the image could not be read (width == 0)
 std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m);
 
+// Device workspace of one render_tiles (or mo_batch) call. Calls on different streams may run
+// at once (pbrt calls Li from every worker thread), so each call takes a workspace of its own
+// from the context's pool; `done` (recorded on the call's stream) orders a later user of the
+// same workspace after the kernels of the previous one.
+struct RenderWorkspace {
+    DevBuf<uint32_t> flags, hs, spill;
+    DevBuf<int32_t> slot;
+    DevBuf<int> count, work;
+    DevBuf<float4> q, mo, ha, hb, xyz, alb, frame, st;
+    DevBuf<unsigned char> terms;
+    DevBuf<float> ld;
+    int64_t n = 0, hits = 0, tex_hits = 0, terms_n = 0, st_n = 0, px = 0;
+    hipEvent_t done = nullptr;
+    int device = 0;
+    bool pending = false;
+    ~RenderWorkspace();
+};
+
 class Context {
 public:
     explicit Context(const mpss_config &cfg);
@@ -78,12 +97,19 @@ public:
     // FindPoissonPointDistribution (usepoissonpointfinder): fills points_ (render_host.hip)
     void find_poisson_points(uint32_t seed);
     void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);
+    // SubsurfaceOctreeNode::Mo over q device-resident points with material `mid`'s profile
+    // (mpss_mo_batch); stream-ordered, safe for concurrent callers on their own streams
+    void mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, int32_t *counters_dev, hipStream_t stream);
+    // Cost probe for tile dealing: one camera ray through every pixel centre; per rect, the rays
+    // that hit a BSSRDF surface (sss) and any mesh surface (surf). Synchronous.
+    void tile_costs(int n, const int32_t *rects, int64_t *sss, int64_t *surf);
     const std::vector<SurfacePoint> &surface_points() const { return points_; }
     const std::vector<float> &irradiance() const { return irradiance_; }
     bool has_octree() const { return have_octree_; }
     mpss_render_stats render_stats();
     void reset_render_stats();
     void set_instrumentation(bool timing, bool counting) {
+        std::lock_guard<std::mutex> g(mu_);
         cfg_.kernel_timing = timing;
         cfg_.count_traversal = counting;
     }
@@ -108,31 +134,26 @@ private:
     DevBuf<struct RenderMaterial> d_materials_;
     std::vector<std::unique_ptr<ImageTexture>> textures_;
     DevBuf<float> d_lut_;  // EWA weight table
-    DevBuf<float4> ws_alb_, ws_frame_;  // per hit: albedo lookup, bumped frame (textured scenes)
-    int64_t ws_tex_hits_ = 0;
-    // render workspace: per camera sample (flags, slot) and per surface hit (ld, Mo query, Mo)
-    DevBuf<uint32_t> ws_flags_;
-    DevBuf<int32_t> ws_slot_;
-    DevBuf<int> ws_count_;
-    DevBuf<float4> ws_q_, ws_mo_, ws_ha_, ws_hb_, ws_xyz_;
-    DevBuf<uint32_t> ws_hs_, ws_spill_;
-    DevBuf<unsigned char> ws_terms_;
-    int64_t ws_terms_n_ = 0;
-    DevBuf<float4> ws_st_;  // infinite lights: radiance-map coordinates per direct-light lane
-    int64_t ws_st_n_ = 0;
-    int64_t ws_px_ = 0;
-    DevBuf<float> ws_ld_;
-    int64_t ws_n_ = 0, ws_hits_ = 0;
+    // workspace pool (render_tiles / mo_batch); guarded by mu_
+    std::vector<std::unique_ptr<RenderWorkspace>> ws_free_;
+    RenderWorkspace *acquire_ws();
+    void release_ws(RenderWorkspace *ws, hipStream_t stream);
+    // every BSSRDF material's band layout exists on the device octree (mu_ held)
+    void ensure_layouts();
+    void build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area);
+    // serializes everything that changes the context (scene, materials, octree, stats) and the
+    // workspace pool; launches happen outside it
+    mutable std::mutex mu_;
     // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)
     struct Timed {
         hipEvent_t a, b;
         int kind;
     };
-    std::vector<Timed> timed_;
-    void time_begin(hipStream_t s, hipEvent_t &a);
-    void time_end(hipStream_t s, hipEvent_t a, int kind);
+    std::vector<Timed> timed_;  // guarded by mu_
+    void time_begin(bool on, hipStream_t s, hipEvent_t &a);
+    void time_end(bool on, hipStream_t s, hipEvent_t a, int kind, std::vector<Timed> &out);
     mpss_render_stats stats_{};
-    DevBuf<unsigned long long> d_counts_;  // [2 * kGroups]: nodes, points per band group
+    DevBuf<unsigned long long> d_counts_;  // [kStatStride * kGroups] traversal counts (mo_kernel.h)
     mpss_config cfg_;
     float max_error_, min_dist_;
     std::vector<std::unique_ptr<Material>> materials_;

@@ -43,6 +43,9 @@ EnvMap build_envmap(int W, int H, const float *texels) {
     const float filter = 1.f / (float)std::max(W, H);
     for (int v = 0; v < H; ++v) {
         const float vp = (float)v / (float)H;
+        // sinf(M_PI * float(v+.5f)/float(height)) (infinite.cpp:94): pbrt redefines M_PI as the
+        // float literal 3.14159265358979323846f (core/pbrt.h:193-196), so the argument is a float
+        // product and quotient -- not a double one
         const float sin_theta = m_sin(kPiF * ((float)v + .5f) / (float)H);
         for (int u = 0; u < W; ++u) {
             const float up = (float)u / (float)W;

@@ -1,18 +1,26 @@
 // mo_band.h -- the spectrally sharded Mo() gather (device), used by the render path and by
 // mpss_mo_batch's default mode.
 //
-// Why: the gather's cost is the Rd(d^2) table lookups. The 30 per-band tables (L floats each,
-// 14 MB for skin) are hit at 30 unrelated offsets per (query, record) and do not fit one XCD's
-// 4 MB L2, so with every wave touching every band the lookups miss to the fabric (measured:
-// 39-61 % L2 hit rate, ~4x the algorithmic bytes through the fabric).
+// Why sharded: the gather's memory traffic is the Rd(d^2) table lookups. The 30 per-band
+// tables (L floats each, 14 MB for skin) are hit at 30 unrelated offsets per (query, record)
+// and do not fit one XCD's 4 MB L2, so with every wave touching every band the lookups miss
+// to the fabric (measured: 39-61 % L2 hit rate, ~4x the algorithmic bytes through the fabric).
 //
 // Mapping: the 30 bands are dealt into 8 groups of <= 4 (BandGroups) and group g runs only on
 // workgroups with blockIdx % 8 == g, i.e. on one XCD under the round-robin dispatch. Each XCD's
 // L2 then holds only its own <= 4 tables (< 2 MB). One wave64 = 64 queries x one group: lane
 // = query, 4 bands per lane. Node / point headers and the group's 16-byte Et/E slice are
-// wave-uniform scalar loads from a group-major copy of the octree (band_et / band_e, 16 B per
-// record per group, so consecutive pre-order records share lines); only the table lookups
-// are per-lane gathers.
+// wave-uniform scalar loads from a group-major copy of the octree (BandLayout, 16 B per record
+// per group, so consecutive pre-order records share lines); only the table lookups are per-lane
+// gathers (one 8-byte load per band: the lerp pair).
+//
+// What bounds it: VALU issue (profiles/r01i_pmc.json: 12.6 G wave-instructions per launch,
+// ~89 % of the chip's VALU issue rate), so the per-record instruction count and the fraction of
+// lanes doing useful work set the speed. The traversal is the UNION of the wave's 64 pruned
+// traversals, so the 64 queries of a wave should be neighbours: the kernel sorts each
+// 1024-query chunk by a Morton key of the query position before dealing queries to lanes
+// (mo_kernel.hip), and the per-record work below is kept to packed-f32 arithmetic on 32-bit
+// table offsets from one uniform base pointer.
 //
 // Each query walks exactly the node set of SubsurfaceOctreeNode::Mo (diffusionutil.h:175-210)
 // minus subtrees that lie past the end of all of the group's profiles (they add +0 for these
@@ -25,9 +33,7 @@
 namespace mpss {
 
 constexpr int kGroups = 8;
-constexpr int kBandBlock = 1024;  // queries per workgroup (16 waves of one band group)
-constexpr int kLdsRd = 4096;      // leading Rd entries per band kept in LDS (64 KB: two workgroups per CU)
-constexpr int kLdsRdBig = 10224;  // the same filling one CU's 160 KB (one workgroup per CU)
+constexpr int kBandBlock = 512;  // default queries per chunk / workgroup (MPSS_MO_BS)
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -66,14 +72,21 @@ inline BandGroups make_band_groups(const float *rcp) {
     return g;
 }
 
+inline bool same_groups(const BandGroups &a, const BandGroups &b) {
+    for (int g = 0; g < kGroups; ++g)
+        for (int s = 0; s < 4; ++s)
+            if (a.band[g][s] != b.band[g][s]) return false;
+    return true;
+}
+
 struct BandTree {
     const NodeHdr *__restrict__ nodes;
     const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
     const float4 *__restrict__ pt_hdr;   // [n_points] {p, area (sign bit: E black)}
     const float4 *__restrict__ band_e;   // [kGroups][n_points]
     const float *__restrict__ table;     // [NB][L] + 2 trailing zeros (DeviceProfile::upload)
-    const float *__restrict__ rcp;       // [NB]
     BandGroups groups;
+    float grcp[kGroups][4];              // rcpDsqSpacing of each group slot (0 for an empty slot)
     int L, n_nodes, n_points;
     float max_error, prune_f;
 };
@@ -85,48 +98,83 @@ struct __attribute__((aligned(4))) RdPair {
     float a, b;
 };
 typedef float f2v __attribute__((ext_vector_type(2)));  // v_pk_{add,mul}_f32 operands
+// The octree is read-only while a gather runs. Reading it through the constant address space
+// says so to the compiler: with stores of results earlier in the same (persistent) kernel it
+// otherwise cannot prove the node records unclobbered and turns the wave-uniform header loads
+// into vector loads (a full L2 round trip at the top of every node iteration).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using cptr = const __attribute__((address_space(4))) T *;
+#else  // the host pass of a HIP translation unit never runs these functions
+template <class T>
+using cptr = const T *;
+#endif
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T *p) {
+    return (cptr<T>)p;
+}
+
 typedef __attribute__((address_space(3))) const float lds_float;  // ds_read, never a flat load
 
-// The lane's view of its group's 4 bands.
+// The lane's view of its group's 4 bands: table offsets (floats from BandTree::table), rcp, and
+// the workgroup's LDS copy of the first entries of each band (the near field).
 struct BandLane {
-    const float *tb[4];  // band tables (an empty slot reads band 0's with rcp 0; its sum is unused)
+    uint32_t off[4];  // c * L (an empty slot reads band 0 with rcp 0; its sum is never stored)
     float rcp[4];
-    uint32_t zero[4];    // tb[j] + zero[j] = the table's trailing zero pair
-    float lm1;           // L - 1: sampleProfile's range end
-    float klim;          // min(KLDS, L) - 1: f < klim <=> the lerp pair is in LDS and in range
+    uint32_t zero;    // NB * L: the trailing zero pair
+    uint32_t lm1;     // L - 1: sampleProfile's range end
+    uint32_t klim;    // min(KLDS, L - 1): s < klim <=> the pair (s, s + 1) is in the LDS copy
+    const float *lt;  // LDS rows of KLDS + 2 floats per band slot (generic pointer)
 };
 
 // Rd lookups of one record for the lane's 4 bands, accumulated:
 // acc[j] += Rd_j(d2) * e[j] (* w), as sampleProfile + the Mo() product (multipole.cpp:60-73;
-// diffusionutil.h:185,197) -- the same IEEE operations in the same order as the scalar code.
-// lt: the workgroup's LDS copy of the first KLDS entries of each band, rows of KLDS + 2 floats
-// (the last two zero). Per band one wave-uniform choice: if every active lane's pair is in the
-// LDS copy (or the lane is past the profile end), all read LDS; otherwise all read the table
-// (L2). A lane past the profile end reads a zero pair, so its term is (0 * e) * w = +-0 and the
-// running sum (which starts at +0 and is never -0) is unchanged: no masking instruction. The
-// pairs of all 4 bands are requested before any is consumed (one memory round trip per
-// record); the lerp and the products run as packed f32 (two values per instruction).
-template <bool POINT, int KLDS, bool FLAT>
-__device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   const float *lt) {
-    float f[4];
+// diffusionutil.h:185,197) -- the same IEEE operations in the same order as the scalar code:
+// f = d2 * rcp in float (the reference multiplies two floats and widens the product), s = floor
+// f, t = f - s, (1 - t) * T[s] + t * T[s + 1]. s < L - 1 <=> f < L - 1 (sampleProfile's range
+// test); a lane past the end reads the zero pair, so its term is (0 * e) * w = +0 and the
+// running sum (which starts at +0 and is never -0) is unchanged: no masking instruction. All
+// four lookups are issued before any is consumed; the products run as packed f32.
+// COUNT: hist[0] += lookups inside the profile, hist[1..3] += those with s < 4096, 8192, 16384
+// (how much a near-field copy of that many entries per band in LDS would absorb).
+// Near field (KLDS > 0): a lane whose pair lies in the LDS copy reads it there, the others read
+// the table in L2 -- NEAR 1: two loads under complementary exec masks (ds_read2_b32 /
+// global_load_dwordx2), NEAR 2: one flat load whose per-lane address is in LDS or in the table.
+// The L2 request rate is what bounds the gather (profiles/r02b_pmc.json), and only lanes outside
+// the near field make requests.
+template <bool POINT, bool COUNT, int KLDS, int NEAR>
+__device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ table, const BandLane &b, float d2,
+                                                   const float e[4], float w, f2v acc[2], int hist[4]) {
+    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
+    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
+    const float f[4] = {f01.x, f01.y, f23.x, f23.y};
     RdPair v[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        f[j] = d2 * b.rcp[j];
-        const uint32_t s = (uint32_t)f[j];  // fSegId (the double product is exact: multipole.cpp:63-65)
-        const bool ok = f[j] < b.lm1;
-        const bool in_lds = f[j] < b.klim;  // implies ok
-        if (FLAT) {  // per lane: one flat load whose address is in LDS or in the table
-            const float *src = in_lds ? lt + j * (KLDS + 2) + s : b.tb[j] + (ok ? s : b.zero[j]);
+        const uint32_t s = (uint32_t)f[j];  // saturating convert: f >= 2^32 -> 0xffffffff >= lm1
+        const uint32_t idx = s < b.lm1 ? b.off[j] + s : b.zero;
+        if (KLDS > 0 && NEAR == 2) {
+            const float *src = s < b.klim ? b.lt + j * (KLDS + 2) + s : table + idx;
             v[j] = *reinterpret_cast<const RdPair *>(src);
-        } else if (__builtin_amdgcn_ballot_w64(ok && !in_lds) == 0) {
-            const lds_float *row =
-                (const lds_float *)lt + j * (KLDS + 2) + (in_lds ? s : (uint32_t)KLDS);
-            v[j].a = row[0];
-            v[j].b = row[1];
+        } else if (KLDS > 0) {
+            if (s < b.klim) {
+                const lds_float *row = (const lds_float *)b.lt + j * (KLDS + 2) + s;
+                v[j].a = row[0];
+                v[j].b = row[1];
+            } else {
+                v[j] = *reinterpret_cast<const RdPair *>(table + idx);
+            }
+        } else if (NEAR == 3) {  // no request for a lane past the profile end: its pair is (0, 0)
+            v[j].a = v[j].b = 0.f;
+            if (s < b.lm1) v[j] = *reinterpret_cast<const RdPair *>(table + b.off[j] + s);
         } else {
-            v[j] = *reinterpret_cast<const RdPair *>(b.tb[j] + (ok ? s : b.zero[j]));
+            v[j] = *reinterpret_cast<const RdPair *>(table + idx);
+        }
+        if (COUNT && s < b.lm1 && b.rcp[j] > 0.f) {
+            ++hist[0];
+            hist[1] += s < 4096u;
+            hist[2] += s < 8192u;
+            hist[3] += s < 16384u;
         }
     }
     float rd[4];
@@ -157,29 +205,36 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
     return below;
 }
 
-template <bool COUNT, int KLDS, bool FLAT>
+// COUNT: k_nodes / k_pts = this lane's node / point visits; w_nodes / w_pts = the wave's node-loop
+// and point-loop iterations (uniform).
+template <bool COUNT, int KLDS, int NEAR>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
-                                                 float out[4], int &k_nodes, int &k_pts, const float *lt) {
+                                                 float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
+                                                 int hist[4], const float *lt) {
     BandLane b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = a.groups.band[grp][j];
-        const int cc = c >= 0 ? c : 0;
-        b.rcp[j] = c >= 0 ? a.rcp[c] : 0.f;
-        b.tb[j] = a.table + (size_t)cc * a.L;
-        b.zero[j] = (uint32_t)(NB - cc) * (uint32_t)a.L;
+        b.rcp[j] = a.grcp[grp][j];
+        b.off[j] = (uint32_t)(c >= 0 ? c : 0) * (uint32_t)a.L;
     }
-    b.lm1 = (float)(a.L - 1);
-    b.klim = (float)((a.L < KLDS ? a.L : KLDS) - 1);
+    b.zero = (uint32_t)NB * (uint32_t)a.L;
+    b.lm1 = (uint32_t)(a.L - 1);
+    b.klim = (uint32_t)KLDS < b.lm1 ? (uint32_t)KLDS : b.lm1;
+    b.lt = lt;
+    const float *__restrict__ table = a.table;
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     const float rcp_min = a.groups.rcp_min[grp];
-    const float4 *__restrict__ et_g = a.band_et + (size_t)grp * a.n_nodes;
-    const float4 *__restrict__ e_g = a.band_e + (size_t)grp * a.n_points;
+    const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
+    const cptr<float4> e_g = as_const(a.band_e + (size_t)grp * a.n_points);
+    const cptr<NodeHdr> nodes = as_const(a.nodes);
+    const cptr<float4> pt_hdr = as_const(a.pt_hdr);
     int resume = valid ? 0 : 0x7fffffff;
     int node = 0;
     while (node < a.n_nodes) {
         node = __builtin_amdgcn_readfirstlane(node);
-        const NodeHdr h = a.nodes[node];
+        if (COUNT) ++w_nodes;
+        const NodeHdr h = nodes[node];
         const int skip = h.skip;
         bool open = false;
         if (node >= resume) {
@@ -188,8 +243,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             const float bx = fmaxf(fmaxf(h.bminx - px, px - h.bmaxx), 0.f);
             const float by = fmaxf(fmaxf(h.bminy - py, py - h.bmaxy), 0.f);
             const float bz = fmaxf(fmaxf(h.bminz - pz, pz - h.bmaxz), 0.f);
-            const bool prune = (bx * bx + by * by + bz * bz) * rcp_min >= a.prune_f;
-            if (prune || (h.flags & NODE_BLACK)) {
+            // exact-zero pruning with a 1e-4 margin (prune_f), so the test may round freely
+            const float box2 = __builtin_fmaf(bz, bz, __builtin_fmaf(by, by, bx * bx));
+            if (box2 * rcp_min >= a.prune_f || (h.flags & NODE_BLACK)) {
                 resume = skip;
             } else {
                 const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
@@ -200,7 +256,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-                    band_rd_accumulate<false, KLDS, FLAT>(b, d2, e, 1.f, acc, lt);
+                    band_rd_accumulate<false, COUNT, KLDS, NEAR>(table, b, d2, e, 1.f, acc, hist);
                 } else {
                     open = true;
                 }
@@ -212,16 +268,17 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 // the leaf's non-black points only (DeviceOctree::upload puts them first, h.pad)
                 f2v lacc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
                 const int live = (int)h.pad;
+                if (COUNT) w_pts += live;
                 for (int i = 0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
-                    const float4 ph = a.pt_hdr[kp];
+                    const float4 ph = pt_hdr[kp];
                     if (!open) continue;
                     if (COUNT) ++k_pts;
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-                    band_rd_accumulate<true, KLDS, FLAT>(b, d2, e, ph.w, lacc, lt);
+                    band_rd_accumulate<true, COUNT, KLDS, NEAR>(table, b, d2, e, ph.w, lacc, hist);
                 }
                 acc[0] += lacc[0];
                 acc[1] += lacc[1];
@@ -238,6 +295,23 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     out[1] = acc[0].y;
     out[2] = acc[1].x;
     out[3] = acc[1].y;
+}
+
+// 30-bit Morton code of a point in [lo, lo + 1/inv) per axis (10 bits per axis, clamped).
+__device__ __forceinline__ uint32_t morton_expand10(uint32_t v) {
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t morton30(float x, float y, float z, const float lo[3], const float inv[3]) {
+    const float q[3] = {(x - lo[0]) * inv[0], (y - lo[1]) * inv[1], (z - lo[2]) * inv[2]};
+    uint32_t c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = (uint32_t)fminf(fmaxf(q[k], 0.f), 1023.f);
+    return (morton_expand10(c[0]) << 2) | (morton_expand10(c[1]) << 1) | morton_expand10(c[2]);
 }
 #endif
 

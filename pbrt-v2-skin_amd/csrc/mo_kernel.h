@@ -1,10 +1,20 @@
-// mo_kernel.h -- device-resident octree / profile and the Mo() gather launcher.
+// mo_kernel.h -- device-resident octree / profile and the Mo() gather launchers.
 #pragma once
+#include <memory>
+#include <vector>
+
 #include "common.h"
 #include "mo_band.h"
 #include "octree.h"
 
 namespace mpss {
+
+// The group-major copy of the octree's E/Et rows for one band grouping (mo_band.h): et[g][node],
+// e[g][point] = the 4 bands of group g as a float4.
+struct BandLayout {
+    BandGroups groups{};
+    DevBuf<float4> et, e;
+};
 
 struct DeviceOctree {
     DevBuf<NodeHdr> nodes;
@@ -12,16 +22,18 @@ struct DeviceOctree {
     DevBuf<float4> pt_hdr;
     DevBuf<float> pt_e;
     int n_nodes = 0, n_points = 0, max_depth = 0;
-    // group-major copies for the spectrally sharded gather (mo_band.h), built on demand
-    DevBuf<float4> band_et, band_e;
-    BandGroups band_groups{};
-    bool band_valid = false;
+    float bmin[3] = {0.f, 0.f, 0.f}, bmax[3] = {0.f, 0.f, 0.f};  // root bounds (query sort keys)
+    // one group-major layout per distinct band grouping in use; built eagerly and synchronously
+    // (Context::set_irradiance_points / add material) so launches only read them
+    std::vector<std::unique_ptr<BandLayout>> layouts;
     void upload(const FlatOctree &t);
-    void ensure_band_layout(const BandGroups &g, hipStream_t stream);
+    const BandLayout *find_layout(const BandGroups &g) const;
+    // builds the layout if it is missing (synchronizes the device); the caller serializes calls
+    const BandLayout &ensure_layout(const BandGroups &g);
 };
 
 struct DeviceProfile {
-    DevBuf<float> table;  // [NB][L] channel-major
+    DevBuf<float> table;  // [NB][L] channel-major + 2 trailing zeros
     DevBuf<float> rcp;    // [NB]
     float rcp_min = 0.f;  // min over bands (exact subtree pruning, mo_kernel.hip)
     int L = 0;
@@ -32,16 +44,27 @@ struct DeviceProfile {
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
 // counters (nullable, q*4 int32): per query {reference-traversal nodes entered, points evaluated,
-// pruned-kernel nodes entered, points evaluated}. The packet kernel (exact=false)
-// reports only the last two (the first two are 0); exact=true follows the reference summation order.
-// mode: 0 spectrally sharded (default), 1 exact reference order, 2 packet.
-void launch_mo_gather(const DeviceOctree &t, const DeviceProfile &p, float max_error, int nq, const float *queries,
-                      float *out, int out_stride, int32_t *counters, hipStream_t stream, int mode);
+// pruned-kernel nodes entered, points evaluated}. The packet kernel reports only
+// the last two (the first two are 0); mode 1 follows the reference summation order.
+// mode: 0 spectrally sharded (default; needs `layout` for p.groups), 1 exact reference order, 2 packet.
+// work: kGroups ints of device scratch for mode 0 (the persistent grid's chunk counters).
+void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
+                      const float *queries, float *out, int out_stride, int32_t *counters, int *work,
+                      hipStream_t stream, int mode);
+
+// Traversal statistics of the sharded gather (count variant): per group g, counts[kStatStride*g + k]
+// for k = 0 node visits, 1 point visits (summed over queries), 2 wave node iterations, 3 wave
+// point iterations (summed over waves; 64 x these / the visits = 1 / lane efficiency), 4 table
+// lookups inside the profile (lane x band), 5..7 those at entries < 4096, 8192, 16384.
+constexpr int kStatStride = 8;
 
 // Spectrally sharded gather for the render path: queries4[i] = {p, *}, i < *count_dev (<= nq_max);
 // out4[i * 8 + g] = the 4 bands of group g (BandGroups::pos gives a band's float offset).
-// counts (nullable): [2 * kGroups] nodes / points visited per group (atomics).
-void launch_mo_band(DeviceOctree &t, const DeviceProfile &p, float max_error, int nq_max, const float4 *queries4,
-                    const int *count_dev, float4 *out4, unsigned long long *counts, hipStream_t stream);
+// hit_s / mat (hit_s nullable): only queries whose hit_s material field equals mat are evaluated
+// (scenes with several BSSRDF materials run one launch per material). counts: see kStatStride.
+// work: kGroups ints of device scratch (the chunk counters of the persistent grid).
+void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
+                    int nq_max, const float4 *queries4, const int *count_dev, float4 *out4,
+                    const uint32_t *hit_s, int mat, unsigned long long *counts, int *work, hipStream_t stream);
 
 }  // namespace mpss

@@ -194,119 +194,181 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Spectrally sharded gather (mo_band.h): block b runs band group b % 8 for queries
-// [1024 * (b / 8), +1024); query count read on the device (render path: compacted list).
+// Spectrally sharded gather (mo_band.h). Persistent grid: workgroup b runs band group b % 8
+// (one XCD under the round-robin dispatch) and takes 1024-query chunks from that group's
+// counter until the queries run out (the query count is read on the device: the render path's
+// compacted hit list). Each chunk is sorted by a Morton key of its query positions (bitonic
+// sort in LDS) before the queries are dealt to lanes, so the 64 queries of a wave are
+// neighbours and walk nearly the same records (the traversal is the union of the wave's);
+// every result goes to its query's own slot, so the order changes no bit of any result.
 // ---------------------------------------------------------------------------------------
+
 struct BandArgs {
     BandTree t;
     const float *__restrict__ queries3;  // q * 3 (batch API) or null
     const float4 *__restrict__ queries4; // {p, *} (render path) or null
     const int *__restrict__ count;       // device query count (nullable: use nq)
+    const uint32_t *__restrict__ hit_s;  // render path with several BSSRDF materials: material filter
+    int mat;
     int nq;
-    float *__restrict__ out;             // mode 0: out[q * stride + band]
-    float4 *__restrict__ out4;           // mode 1: out4[q * 8 + group]
+    float *__restrict__ out;             // batch: out[q * stride + band]
+    float4 *__restrict__ out4;           // render: out4[q * 8 + group]
     int out_stride;
     int32_t *__restrict__ counters;      // batch API COUNT: q * 4 (+= per group)
-    unsigned long long *__restrict__ counts;  // render COUNT: [2 * kGroups]
+    unsigned long long *__restrict__ counts;  // render COUNT: [kStatStride * kGroups]
+    int *__restrict__ work;              // [kGroups] chunk counters (zeroed before the launch)
+    float klo[3], kinv[3];               // Morton key quantization (octree root bounds)
+    int sort;                            // 0: keep slot order (MPSS_MO_SORT=0, a tuning knob)
 };
 
-template <bool COUNT, int KLDS, bool FLAT>
-__device__ __forceinline__ void mo_band_body(const BandArgs &a, float *lt) {
+__device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, float &py, float &pz) {
+    if (a.queries4) {
+        const float4 v = a.queries4[q];
+        px = v.x;
+        py = v.y;
+        pz = v.z;
+        bool live = v.w >= 0.f;  // render hit list: w < 0 marks hits without a BSSRDF
+        if (live && a.hit_s) live = (int)((a.hit_s[q] >> 16) & 0xffu) == a.mat;
+        return live;
+    }
+    px = a.queries3[3 * (size_t)q];
+    py = a.queries3[3 * (size_t)q + 1];
+    pz = a.queries3[3 * (size_t)q + 2];
+    return true;
+}
+
+template <bool COUNT, int BS, int KLDS, int NEAR>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_kernel(BandArgs a) {
+    __shared__ unsigned long long keys[BS];
+    __shared__ int chunk_s;
+    __shared__ float lt[KLDS > 0 ? 4 * (KLDS + 2) : 1];
     const int grp = (int)(blockIdx.x & (kGroups - 1));
-    const int base = (int)(blockIdx.x / kGroups) * kBandBlock;
+    const int tid = (int)threadIdx.x;
     const int nq = a.count ? *a.count : a.nq;
-    if (base >= nq) return;
-    // the group's near-field Rd entries, KLDS per band + a zero pair
-    for (int i = (int)threadIdx.x; i < 4 * (KLDS + 2); i += kBandBlock) {
-        const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
-        lt[i] = (c >= 0 && k < KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
-    }
-    __syncthreads();
-    const int q = base + (int)threadIdx.x;
-    const bool valid = q < nq;
-    float px = 0.f, py = 0.f, pz = 0.f;
-    bool live = valid;
-    if (valid) {
-        if (a.queries4) {
-            const float4 v = a.queries4[q];
-            px = v.x;
-            py = v.y;
-            pz = v.z;
-            live = v.w >= 0.f;  // render hit list: w < 0 marks hits without a BSSRDF
-        } else {
-            px = a.queries3[3 * (size_t)q];
-            py = a.queries3[3 * (size_t)q + 1];
-            pz = a.queries3[3 * (size_t)q + 2];
+    if (KLDS > 0 && (int)(blockIdx.x / kGroups) * BS < nq) {
+        // the group's near field: entries 0..KLDS of each band (past the table end: 0)
+        for (int i = tid; i < 4 * (KLDS + 2); i += BS) {
+            const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
+            lt[i] = (c >= 0 && k <= KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
     }
-    float acc[4];
-    int kn = 0, kp = 0;
-    mo_band_traverse<COUNT, KLDS, FLAT>(a.t, grp, px, py, pz, live, acc, kn, kp, lt);
-    if (!live) return;
-    if (a.out4) {
-        a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    } else {
+    for (;;) {
+        if (tid == 0) chunk_s = atomicAdd(&a.work[grp], 1);
+        __syncthreads();
+        const int base = chunk_s * BS;
+        if (base >= nq) return;  // uniform over the workgroup
+        float px = 0.f, py = 0.f, pz = 0.f;
+        const bool in = base + tid < nq && band_query(a, base + tid, px, py, pz);
+        const uint32_t key = in ? (a.sort ? morton30(px, py, pz, a.klo, a.kinv) : 0u) : 0xffffffffu;  // dead last
+        keys[tid] = ((unsigned long long)key << 32) | (unsigned)tid;
+        __syncthreads();
+        for (int k = 2; k <= BS; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int ixj = tid ^ j;
+                if (ixj > tid) {
+                    const unsigned long long x = keys[tid], y = keys[ixj];
+                    if ((x > y) == ((tid & k) == 0)) {
+                        keys[tid] = y;
+                        keys[ixj] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        const unsigned long long mine = keys[tid];
+        const int q = base + (int)(mine & 0xffffffffull);
+        const bool live = (mine >> 32) != 0xffffffffull;
+        if (live) band_query(a, q, px, py, pz);
+        float acc[4];
+        int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
+        mo_band_traverse<COUNT, KLDS, NEAR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        if (live) {
+            if (a.out4) {
+                a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = a.t.groups.band[grp][j];
-            if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
+                for (int j = 0; j < 4; ++j) {
+                    const int c = a.t.groups.band[grp][j];
+                    if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
+                }
+            }
         }
-    }
-    if (COUNT) {
-        if (a.counters) {
-            atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
-            atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
+        if (COUNT) {
+            if (a.counters && live) {
+                atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
+                atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
+            }
+            if (a.counts) {
+                if (kn) atomicAdd(&a.counts[kStatStride * grp], (unsigned long long)kn);
+                if (kp) atomicAdd(&a.counts[kStatStride * grp + 1], (unsigned long long)kp);
+                if ((tid & 63) == 0) {
+                    atomicAdd(&a.counts[kStatStride * grp + 2], (unsigned long long)wn);
+                    atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
+            }
         }
-        if (a.counts) {
-            atomicAdd(&a.counts[2 * grp], (unsigned long long)kn);
-            atomicAdd(&a.counts[2 * grp + 1], (unsigned long long)kp);
-        }
+        __syncthreads();  // chunk_s and keys are rewritten by the next chunk
     }
 }
 
-// Variants of one body: 64 KB of LDS (two workgroups = 32 waves a CU) with wave-uniform LDS /
-// table reads; the same with one per-lane flat load (address in LDS or in the table); one
-// workgroup a CU with 160 KB of LDS (a larger near field in LDS).
-template <bool COUNT>
-__global__ __launch_bounds__(kBandBlock) void mo_band_kernel(BandArgs a) {
-    __shared__ float lt[4 * (kLdsRd + 2)];
-    mo_band_body<COUNT, kLdsRd, false>(a, lt);
-}
-template <bool COUNT>
-__global__ __launch_bounds__(kBandBlock) void mo_band_kernel_flat(BandArgs a) {
-    __shared__ float lt[4 * (kLdsRd + 2)];
-    mo_band_body<COUNT, kLdsRd, true>(a, lt);
-}
-template <bool COUNT>
-__global__ __launch_bounds__(kBandBlock) void mo_band_kernel_big(BandArgs a) {
-    __shared__ float lt[4 * (kLdsRdBig + 2)];
-    mo_band_body<COUNT, kLdsRdBig, false>(a, lt);
+// Gather variant (tuning knobs; default 1024-query chunks, a 4096-entry near field read by
+// flat loads): MPSS_MO_BS = 1024 | 512, MPSS_MO_K = LDS entries per band (0, 2048, 4096, 9216),
+// MPSS_MO_NEAR = 1 (masked ds/global loads) | 2 (flat loads) | 3 (no near field, no request past
+// the profile end), MPSS_MO_SORT = 0 (no Morton sort). Measured on C2 (profiles/r02_variants.txt):
+// flat 4096 120 ms/frame, masked 4096 121, no near field 127, 512-query chunks 124-126, the
+// 9216-entry near field (one workgroup per CU) 140, no sort 128 (lane efficiency 0.47 vs 0.60).
+struct BandVariant {
+    int bs, k, near;
+};
+BandVariant band_variant() {
+    BandVariant v{1024, 4096, 2};
+    if (const char *e = getenv("MPSS_MO_BS")) v.bs = atoi(e);
+    if (const char *e = getenv("MPSS_MO_K")) v.k = atoi(e);
+    if (const char *e = getenv("MPSS_MO_NEAR")) v.near = atoi(e);
+    return v;
 }
 
-// MPSS_MO_BAND selects the variant (0 default, 1 flat, 2 big LDS) -- a tuning knob
-int band_variant() {
-    const char *v = getenv("MPSS_MO_BAND");
-    return v ? atoi(v) : 0;
+template <int BS, int KLDS, int NEAR>
+void launch_band_v(const BandArgs &a, int nq_max, bool count, hipStream_t stream) {
+    // persistent grid: enough resident workgroups per XCD (32 CUs) to fill it; late ones find no work
+    const int chunks = (nq_max + BS - 1) / BS;
+    const int cap = 32 * (2048 / BS);
+    const int per_group = chunks < cap ? chunks : cap;
+    if (per_group <= 0) return;
+    const dim3 grid((unsigned)(per_group * kGroups));
+    if (count)
+        hipLaunchKernelGGL((mo_band_kernel<true, BS, KLDS, NEAR>), grid, dim3(BS), 0, stream, a);
+    else
+        hipLaunchKernelGGL((mo_band_kernel<false, BS, KLDS, NEAR>), grid, dim3(BS), 0, stream, a);
 }
 
-void launch_band(const BandArgs &a, unsigned blocks, bool count, hipStream_t stream) {
-    const int var = band_variant();
-    if (var == 1) {
-        if (count)
-            hipLaunchKernelGGL(mo_band_kernel_flat<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-        else
-            hipLaunchKernelGGL(mo_band_kernel_flat<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-    } else if (var == 2) {
-        if (count)
-            hipLaunchKernelGGL(mo_band_kernel_big<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-        else
-            hipLaunchKernelGGL(mo_band_kernel_big<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-    } else {
-        if (count)
-            hipLaunchKernelGGL(mo_band_kernel<true>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
-        else
-            hipLaunchKernelGGL(mo_band_kernel<false>, dim3(blocks), dim3(kBandBlock), 0, stream, a);
+void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipStream_t stream) {
+    if (nq_max <= 0) return;
+    for (int k = 0; k < 3; ++k) {
+        const float ext = t.bmax[k] - t.bmin[k];
+        a.klo[k] = t.bmin[k];
+        a.kinv[k] = ext > 0.f ? 1023.99f / ext : 0.f;
     }
+    MPSS_HIP(hipMemsetAsync(a.work, 0, sizeof(int) * kGroups, stream));
+    const BandVariant v = band_variant();
+    const char *so = getenv("MPSS_MO_SORT");
+    a.sort = so ? atoi(so) : 1;
+    if (v.bs == 1024 && v.k == 0 && v.near == 3)
+        launch_band_v<1024, 0, 3>(a, nq_max, count, stream);
+    else if (v.bs == 1024 && v.k == 0)
+        launch_band_v<1024, 0, 0>(a, nq_max, count, stream);
+    else if (v.bs == 512 && v.k == 0)
+        launch_band_v<512, 0, 0>(a, nq_max, count, stream);
+    else if (v.bs == 512 && v.k == 2048)
+        launch_band_v<512, 2048, 1>(a, nq_max, count, stream);
+    else if (v.bs == 1024 && v.k == 9216)
+        launch_band_v<1024, 9216, 1>(a, nq_max, count, stream);
+    else if (v.near == 2)
+        launch_band_v<1024, 4096, 2>(a, nq_max, count, stream);
+    else
+        launch_band_v<1024, 4096, 1>(a, nq_max, count, stream);
     MPSS_HIP(hipGetLastError());
 }
 
@@ -321,15 +383,17 @@ __global__ void band_permute_kernel(const float *__restrict__ rows, int n, BandG
     out[i] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-BandTree band_tree(const DeviceOctree &t, const DeviceProfile &p, float max_error) {
+BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfile &p, float max_error) {
+    if (!same_groups(l.groups, p.groups)) throw Error(-2, "band layout does not match the profile's band groups");
     BandTree bt;
     bt.nodes = t.nodes.ptr;
-    bt.band_et = t.band_et.ptr;
+    bt.band_et = l.et.ptr;
     bt.pt_hdr = t.pt_hdr.ptr;
-    bt.band_e = t.band_e.ptr;
+    bt.band_e = l.e.ptr;
     bt.table = p.table.ptr;
-    bt.rcp = p.rcp.ptr;
     bt.groups = p.groups;
+    for (int g = 0; g < kGroups; ++g)
+        for (int s = 0; s < 4; ++s) bt.grcp[g][s] = p.groups.band[g][s] >= 0 ? p.host_rcp[p.groups.band[g][s]] : 0.f;
     bt.L = p.L;
     bt.n_nodes = t.n_nodes;
     bt.n_points = t.n_points;
@@ -374,14 +438,18 @@ void DeviceOctree::upload(const FlatOctree &t) {
                 if (pass == 0) ++h.pad;
             }
     }
+    layouts.clear();
     nodes.upload(hdr.data(), hdr.size());
     node_et.upload(t.node_et.data(), t.node_et.size());
     pt_hdr.upload(reinterpret_cast<const float4 *>(ph.data()), ph.size() / 4);
     pt_e.upload(pe.data(), pe.size());
-    band_valid = false;
     n_nodes = (int)t.hdr.size();
     n_points = (int)t.pt_index.size();
     max_depth = t.max_depth;
+    for (int k = 0; k < 3; ++k) {
+        bmin[k] = t.bmin[k];
+        bmax[k] = t.bmax[k];
+    }
 }
 
 void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
@@ -398,42 +466,69 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
     groups = make_band_groups(rcp_);
 }
 
-void DeviceOctree::ensure_band_layout(const BandGroups &g, hipStream_t stream) {
-    if (band_valid && memcmp(g.band, band_groups.band, sizeof(g.band)) == 0) return;
-    band_et.alloc((size_t)n_nodes * kGroups);
-    band_e.alloc((size_t)(n_points > 0 ? n_points : 1) * kGroups);
-    const int64_t tn = (int64_t)n_nodes * kGroups, tp = (int64_t)n_points * kGroups;
-    if (tn) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, stream,
-                               node_et.ptr, n_nodes, g, band_et.ptr);
-    if (tp) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, stream,
-                               pt_e.ptr, n_points, g, band_e.ptr);
-    MPSS_HIP(hipGetLastError());
-    band_groups = g;
-    band_valid = true;
+const BandLayout *DeviceOctree::find_layout(const BandGroups &g) const {
+    for (const auto &l : layouts)
+        if (same_groups(l->groups, g)) return l.get();
+    return nullptr;
 }
 
-void launch_mo_band(DeviceOctree &t, const DeviceProfile &p, float max_error, int nq_max, const float4 *queries4,
-                    const int *count_dev, float4 *out4, unsigned long long *counts, hipStream_t stream) {
-    if (nq_max <= 0) return;
-    t.ensure_band_layout(p.groups, stream);
+const BandLayout &DeviceOctree::ensure_layout(const BandGroups &g) {
+    if (const BandLayout *l = find_layout(g)) return *l;
+    auto lay = std::make_unique<BandLayout>();
+    lay->groups = g;
+    lay->et.alloc((size_t)(n_nodes > 0 ? n_nodes : 1) * kGroups);
+    lay->e.alloc((size_t)(n_points > 0 ? n_points : 1) * kGroups);
+    const int64_t tn = (int64_t)n_nodes * kGroups, tp = (int64_t)n_points * kGroups;
+    if (tn) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, 0, node_et.ptr,
+                               n_nodes, g, lay->et.ptr);
+    if (tp) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, 0, pt_e.ptr,
+                               n_points, g, lay->e.ptr);
+    MPSS_HIP(hipGetLastError());
+    // synchronous: every stream that launches a gather later sees a complete layout
+    MPSS_HIP(hipDeviceSynchronize());
+    layouts.push_back(std::move(lay));
+    return *layouts.back();
+}
+
+void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
+                    int nq_max, const float4 *queries4, const int *count_dev, float4 *out4, const uint32_t *hit_s,
+                    int mat, unsigned long long *counts, int *work, hipStream_t stream) {
+    if (nq_max <= 0 || t.n_nodes <= 0) return;
     BandArgs a{};
-    a.t = band_tree(t, p, max_error);
+    a.t = band_tree(t, layout, p, max_error);
     a.queries4 = queries4;
     a.count = count_dev;
+    a.hit_s = hit_s;
+    a.mat = mat;
     a.nq = nq_max;
     a.out4 = out4;
     a.counts = counts;
-    const unsigned blocks = (unsigned)((nq_max + kBandBlock - 1) / kBandBlock) * kGroups;
-    launch_band(a, blocks, counts != nullptr, stream);
+    a.work = work;
+    launch_band(a, nq_max, t, counts != nullptr, stream);
 }
 
-void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_error, int nq, const float *queries,
-                      float *out, int out_stride, int32_t *counters, hipStream_t stream, int mode) {
-    DeviceOctree &t = const_cast<DeviceOctree &>(t_);  // band layout is a cache of the octree
+void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
+                      const float *queries, float *out, int out_stride, int32_t *counters, int *work,
+                      hipStream_t stream, int mode) {
     const bool exact = mode == 1;
     if (nq <= 0) return;
     if (t.n_nodes <= 0) throw Error(-1, "launch_mo_gather: octree is empty");
     if (p.L < 2) throw Error(-1, "launch_mo_gather: profile table has fewer than 2 entries");
+    const bool count = counters != nullptr;
+    if (mode == 0) {
+        if (!layout || !work) throw Error(-2, "launch_mo_gather: the sharded gather needs a band layout and work counters");
+        if (count) MPSS_HIP(hipMemsetAsync(counters, 0, sizeof(int32_t) * 4 * (size_t)nq, stream));
+        BandArgs b{};
+        b.t = band_tree(t, *layout, p, max_error);
+        b.queries3 = queries;
+        b.nq = nq;
+        b.out = out;
+        b.out_stride = out_stride;
+        b.counters = counters;
+        b.work = work;
+        launch_band(b, nq, t, count, stream);
+        return;
+    }
     MoArgs a;
     a.nodes = t.nodes.ptr;
     a.node_et = t.node_et.ptr;
@@ -451,21 +546,6 @@ void launch_mo_gather(const DeviceOctree &t_, const DeviceProfile &p, float max_
     a.max_error = max_error;
     a.rcp_min = p.rcp_min > 0.f ? p.rcp_min : 0.f;  // rcp_min <= 0 disables pruning
     a.prune_f = (a.rcp_min > 0.f) ? (float)(p.L - 1) * 1.0001f : INFINITY;
-    const bool count = counters != nullptr;
-    if (mode == 0) {
-        t.ensure_band_layout(p.groups, stream);
-        if (count) MPSS_HIP(hipMemsetAsync(counters, 0, sizeof(int32_t) * 4 * (size_t)nq, stream));
-        BandArgs b{};
-        b.t = band_tree(t, p, max_error);
-        b.queries3 = queries;
-        b.nq = nq;
-        b.out = out;
-        b.out_stride = out_stride;
-        b.counters = counters;
-        const unsigned blocks = (unsigned)((nq + kBandBlock - 1) / kBandBlock) * kGroups;
-        launch_band(b, blocks, count, stream);
-        return;
-    }
     if (!exact) {
         const int packets = (nq + 7) / 8, blocks = (packets + 3) / 4;
         if (count)

@@ -41,7 +41,8 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 3; }  // 2: poisson point finder, infinite lights; 3: imagemap textures
+int mpss_abi_version(void) { return 4; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+                                          // 4: tile costs, wave-iteration stats, thread-safe calls
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -171,10 +172,7 @@ int mpss_mo_batch(mpss_ctx *c, uint32_t id, uint32_t q, const float *p_dev, floa
                   void *stream) {
     return guarded([&] {
         require(c && (q == 0 || (p_dev && mo_dev)), "mpss_mo_batch: null argument");
-        Context &ctx = *reinterpret_cast<Context *>(c);
-        const Material &m = ctx.material(id);
-        launch_mo_gather(ctx.octree(), m.dev_profile, ctx.max_error(), (int)q, p_dev, mo_dev, NB, counters_dev,
-                         (hipStream_t)stream, ctx.config().exact_mo);
+        reinterpret_cast<Context *>(c)->mo_batch(id, (int)q, p_dev, mo_dev, counters_dev, (hipStream_t)stream);
     });
 }
 
@@ -302,6 +300,13 @@ int mpss_render_tile(mpss_ctx *c, int spp, uint32_t seed, int x0, int x1, int y0
         const int32_t r[4] = {x0, x1, y0, y1};
         float *o[1] = {out};
         reinterpret_cast<Context *>(c)->render_tiles(spp, seed, 1, r, o, (hipStream_t)stream);
+    });
+}
+
+int mpss_tile_costs(mpss_ctx *c, int n, const int32_t *rects, int64_t *sss_hits, int64_t *surf_hits) {
+    return guarded([&] {
+        require(c && n >= 0 && (n == 0 || (rects && sss_hits && surf_hits)), "mpss_tile_costs: null argument");
+        reinterpret_cast<Context *>(c)->tile_costs(n, rects, sss_hits, surf_hits);
     });
 }
 

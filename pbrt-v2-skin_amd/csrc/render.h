@@ -46,6 +46,7 @@ struct RenderMaterial {
     int has_alb_tex, has_bump;
     float mix;
     TexView alb_tex, bump_tex;
+    int band_pos[NB];     // band c's float offset in a hit's Mo() row (this profile's BandGroups::pos)
 };
 
 struct RenderScene {
@@ -115,9 +116,6 @@ __global__ void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint 
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, const float *sp_uv, int n, uint32_t seed, float *E_out);
-struct BandPos {
-    int pos[NB];  // band c's float offset inside a sample's mo4 row (BandGroups::pos)
-};
 
 __global__ void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
 struct DirectTerms;
@@ -134,7 +132,10 @@ template <bool kInf>
 __global__ void direct_combine_kernel(RenderScene sc, SampleRecs rec, int max_hits, int ns_max,
                                       const DirectTerms *terms, const float4 *inf_st);
 // Li assembly per slot (L = Le + SSS + Ld, sample filter, ToXYZ), then the box-filtered film.
-__global__ void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits);
+__global__ void assemble_kernel(RenderScene sc, SampleRecs rec, int max_hits);
+// Tile-cost probe: one camera ray through the centre of every pixel of [x0, x1) x [y0, y1);
+// cls[i] = 0 miss or light, 1 mesh surface, 2 BSSRDF surface (render_host.hip tile_costs).
+__global__ void probe_kernel(RenderScene sc, int x0, int x1, int y0, int y1, uint8_t *cls);
 __global__ void sky_kernel(RenderScene sc, SampleRecs rec, int max_hits);
 __global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, float *out, int out_stride_px);
 

@@ -909,7 +909,7 @@ template __global__ void direct_combine_kernel<true>(RenderScene, SampleRecs, in
 // multipolesubsurface.cpp:253-303): L = 0 + Le; L += ((INV_PI * Ft) * Mo * Pow(albedo, 1 - mix))
 // .Clamp(0); L += Ld -- then the SamplerRenderer sample filter (NaN / y < -1e-5 / inf -> 0,
 // samplerrenderer.cpp:119-133) and Spectrum::ToXYZ in band order. One lane per slot.
-__global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRecs rec, BandPos bp, int max_hits) {
+__global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRecs rec, int max_hits) {
     const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int nhits = *rec.hit_count;
     if (slot >= nhits || slot >= max_hits) return;
@@ -945,7 +945,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
         if (le) L += le[c];
         if (mo) {
             const float ab = alb ? tex_albedo_pow(arg, c, 1.f - mat->mix) : mat->alb_1mmix[c];
-            float t = (kss * mo[bp.pos[c]]) * ab;
+            float t = (kss * mo[mat->band_pos[c]]) * ab;
             t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
             L += t;
         }
@@ -1064,6 +1064,27 @@ __global__ __launch_bounds__(256) void film_kernel(RenderScene sc, TileBatch tb,
     o[1] = Y;
     o[2] = Z;
     o[3] = W;
+}
+
+// ------------------------------------------------------------------ tile-cost probe
+// PerspectiveCamera::GenerateRay through the pixel centre and Scene::Intersect, as primary_kernel.
+__global__ __launch_bounds__(256) void probe_kernel(RenderScene sc, int x0, int x1, int y0, int y1, uint8_t *cls) {
+    __shared__ int stk_all[kStack * 256];
+    int *stk = stk_all + threadIdx.x;
+    const int w = x1 - x0;
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= w * (y1 - y0)) return;
+    const int px = x0 + i % w, py = y0 + i / w;
+    const V3 pcam = xform_point(sc.raster_to_camera, V3{(float)px + 0.5f, (float)py + 0.5f, 0.f});
+    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
+    const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
+    const Hit h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 256);
+    uint8_t c = 0;
+    if (h.tri >= 0) {
+        const uint32_t mid = sc.meshes[sc.tri_mesh[h.tri]].material;
+        c = (sc.materials[mid].has_bssrdf && sc.have_octree) ? 2 : 1;
+    }
+    cls[i] = c;
 }
 
 }  // namespace mpss

@@ -31,6 +31,7 @@ int bvh_depth(const std::vector<BvhNode> &n, int i) {
 
 void Context::add_mesh(uint32_t nv, const float *P, const float *N, const float *S, const float *uv, uint32_t nt,
                        const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material) {
+    std::lock_guard<std::mutex> g(mu_);
     if (material >= materials_.size()) throw Error(MPSS_ERR_INVALID, "add_mesh: unknown material id");
     Mesh m;
     m.P.assign(P, P + 3 * (size_t)nv);
@@ -50,6 +51,7 @@ void Context::add_mesh(uint32_t nv, const float *P, const float *N, const float 
 }
 
 void Context::add_sphere_light(const float *c, float r, const float *Lemit, int nsamples) {
+    std::lock_guard<std::mutex> g(mu_);
     if (!(r > 0.f)) throw Error(MPSS_ERR_INVALID, "add_sphere_light: radius must be positive");
     if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_sphere_light: nsamples must be >= 1");
     if (scene_.lights.size() >= 254) throw Error(MPSS_ERR_INVALID, "add_sphere_light: at most 254 lights");
@@ -67,6 +69,7 @@ void Context::add_sphere_light(const float *c, float r, const float *Lemit, int 
 // Spectrum(rgb, SPECTRUM_ILLUMINANT) on the device (render.hip).
 void Context::add_infinite_light(const float *L, int nsamples, const float *l2w, const float *w2l, int W, int H,
                                  const float *texels) {
+    std::lock_guard<std::mutex> g(mu_);
     if (nsamples < 1) throw Error(MPSS_ERR_INVALID, "add_infinite_light: nsamples must be >= 1");
     if (scene_.lights.size() >= 254) throw Error(MPSS_ERR_INVALID, "add_infinite_light: at most 254 lights");
     if (texels && (W < 1 || H < 1 || (int64_t)W * H > (int64_t)1 << 28))
@@ -99,6 +102,7 @@ void Context::add_infinite_light(const float *L, int nsamples, const float *l2w,
 }
 
 void Context::set_camera(const float *r2c, const float *c2w, int xres, int yres) {
+    std::lock_guard<std::mutex> g(mu_);
     if (xres <= 0 || yres <= 0) throw Error(MPSS_ERR_INVALID, "set_camera: bad resolution");
     memcpy(scene_.camera.raster_to_camera, r2c, sizeof(float) * 16);
     memcpy(scene_.camera.camera_to_world, c2w, sizeof(float) * 16);
@@ -233,6 +237,7 @@ void Context::upload_scene() {
         r.has_bssrdf = 1;
         r.is_mc = m.is_monte_carlo ? 1 : 0;
         r.mix = cfg_.mix;
+        for (int c = 0; c < NB; ++c) r.band_pos[c] = m.dev_profile.groups.pos[c];
         if (m.albedo_tex >= 0) {
             r.has_alb_tex = 1;
             r.alb_tex = textures_[m.albedo_tex]->device_view(d_lut_.ptr);
@@ -278,12 +283,16 @@ RenderScene Context::render_scene() const {
 }
 
 void Context::set_surface_points(uint32_t n, const SurfacePoint *pts) {
+    std::lock_guard<std::mutex> g(mu_);
     points_.assign(pts, pts + n);
     have_points_ = n > 0;
 }
 
-// MultipoleSubsurfaceIntegrator::Preprocess (multipolesubsurface.cpp:254-322 [file lines])
+// MultipoleSubsurfaceIntegrator::Preprocess (multipolesubsurface.cpp:170-238)
 void Context::preprocess(uint32_t seed) {
+    activate();
+    std::lock_guard<std::mutex> g(mu_);
+    MPSS_HIP(hipDeviceSynchronize());  // no render of the previous octree may still be running
     if (scene_dirty_) upload_scene();
     if (scene_.lights.empty()) {  // "if (scene->lights.size() == 0) return;" -> no octree, no SSS
         have_octree_ = false;
@@ -297,7 +306,15 @@ void Context::preprocess(uint32_t seed) {
             tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_, 0, host_bump_views().data());
     }
     const int n = (int)points_.size();
-    if (n == 0) throw Error(MPSS_ERR_INTERNAL, "tessellation produced no surface points");
+    if (n == 0) {
+        // the reference goes on with an empty point set: its octree holds nothing, so Mo() is 0
+        // and the frame has direct lighting only (surfacepoints.cpp:277-281, Preprocess :192-236)
+        fprintf(stderr, "mpss: Warning: no surface points with BSSRDFs were found; rendering without "
+                        "subsurface scattering\n");
+        have_octree_ = false;
+        irradiance_.clear();
+        return;
+    }
     std::vector<float> p(3 * (size_t)n), nr(3 * (size_t)n), eps(n);
     std::vector<uint32_t> mat(n);
     std::vector<float> uv(2 * (size_t)n);
@@ -328,17 +345,17 @@ void Context::preprocess(uint32_t seed) {
         for (int i = 0; i < n; ++i) memcpy(&irradiance_[(size_t)i * NB], s, sizeof(s));
     } else {
         hipEvent_t ev{};
-        time_begin(0, ev);
+        time_begin(cfg_.kernel_timing != 0, 0, ev);
         hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sc, dp.ptr, dn.ptr, de.ptr,
                            dm.ptr, duv.ptr, n, seed, dE.ptr);
         MPSS_HIP(hipGetLastError());
-        time_end(0, ev, 0);
+        time_end(cfg_.kernel_timing != 0, 0, ev, 0, timed_);
         irradiance_.resize((size_t)n * NB);
         MPSS_HIP(hipMemcpy(irradiance_.data(), dE.ptr, sizeof(float) * irradiance_.size(), hipMemcpyDeviceToHost));
     }
     std::vector<float> area(n);
     for (int i = 0; i < n; ++i) area[i] = points_[i].area;
-    set_irradiance_points(n, p.data(), nr.data(), irradiance_.data(), area.data());
+    build_octree_locked(n, p.data(), nr.data(), irradiance_.data(), area.data());
 }
 
 // FindPoissonPointDistribution -> SurfacePointsRenderer::Render (renderers/surfacepoints.cpp:115-150)
@@ -434,8 +451,12 @@ void Context::find_poisson_points(uint32_t seed) {
                         points_.push_back(sp);
                     }
                 }
-            if (!done && total_paths > 50000 && points_.empty())
-                throw Error(MPSS_ERR_INVALID, "Poisson point finder: no objects with BSSRDFs in the scene");
+            if (!done && total_paths > 50000 && points_.empty()) {
+                // Warning + return, as FindPoissonPointDistribution (surfacepoints.cpp:277-281)
+                fprintf(stderr, "mpss: Warning: There don't seem to be any objects with BSSRDFs in this scene. "
+                                "Giving up.\n");
+                return;
+            }
         }
     }
 }
@@ -444,9 +465,13 @@ void Context::find_poisson_points(uint32_t seed) {
 // pieces (a piece = the rows plus a one-pixel border of samples that the box filter carries
 // in); pieces are packed into batches of <= max_batch_samples camera samples. Per batch:
 // camera/direct kernel per piece (all pieces append their surface hits to one compacted
-// list) -> ONE sharded Mo() gather over the batch's hits -> film kernel per piece.
+// list) -> ONE sharded Mo() gather per BSSRDF material over the batch's hits -> film kernel per
+// piece. Calls on different streams may overlap: each takes its own workspace (RenderWorkspace),
+// and the scene, materials and octree are only read after the context lock is released.
 void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs,
                            hipStream_t stream) {
+    activate();
+    std::unique_lock<std::mutex> lk(mu_);
     if (scene_dirty_) upload_scene();
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
@@ -457,192 +482,259 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             throw Error(MPSS_ERR_INVALID, "render_tile: bad rectangle");
         if (!outs[i]) throw Error(MPSS_ERR_INVALID, "render_tile: null output");
     }
-    const int sss_mat = first_bssrdf_material();
-    const bool have_tree = have_octree_ && sss_mat >= 0;
-    Material *m = have_tree ? materials_[sss_mat].get() : nullptr;
-    RenderScene sc = render_scene();
-    sc.have_octree = have_tree ? 1 : 0;
-    BandPos bp{};
-    if (m)
-        for (int c = 0; c < NB; ++c) bp.pos[c] = m->dev_profile.groups.pos[c];
-    const int64_t max_batch = std::max<int64_t>(cfg_.max_batch_samples, 1 << 16);
-
-    // cut rectangles into pieces of <= max_batch samples
-    struct Piece {
-        TileBatch tb;
-        float *out;
+    // every LayeredSkin material has a MultipoleBSSRDF (GetMultipoleBSSRDF, layeredskin.cpp:180-185):
+    // each evaluates Mo() with its own profile (multipolesubsurface.cpp:267-280)
+    struct SssMat {
+        int id;
+        const Material *m;
+        const BandLayout *layout;
     };
-    std::vector<Piece> pieces;
-    for (int i = 0; i < n; ++i) {
-        const int x0 = rects[4 * i], x1 = rects[4 * i + 1], y0 = rects[4 * i + 2], y1 = rects[4 * i + 3];
-        const int tw = x1 - x0;
-        const int ex0 = std::max(x0 - 1, 0);
-        const int ew = std::min(x1 + 1, W) - ex0;
-        const int rows = (int)std::max<int64_t>(1, max_batch / ((int64_t)ew * spp) - 2);
-        for (int yb = y0; yb < y1; yb += rows) {
-            const int ye = std::min(y1, yb + rows);
-            Piece p;
-            p.tb.x0 = x0;
-            p.tb.x1 = x1;
-            p.tb.y0 = yb;
-            p.tb.y1 = ye;
-            p.tb.ex0 = ex0;
-            p.tb.ey0 = std::max(yb - 1, 0);
-            p.tb.ew = ew;
-            p.tb.eh = std::min(ye + 1, H) - p.tb.ey0;
-            p.tb.spp = spp;
-            p.tb.seed = seed;
-            p.tb.nsamples = (int64_t)p.tb.ew * p.tb.eh * spp;
-            p.out = outs[i] + (size_t)(yb - y0) * tw * 4;
-            pieces.push_back(p);
-        }
+    std::vector<SssMat> sss;
+    if (have_octree_)
+        for (size_t i = 0; i < materials_.size(); ++i)
+            sss.push_back(SssMat{(int)i, materials_[i].get(), &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
+    RenderScene sc = render_scene();
+    sc.have_octree = sss.empty() ? 0 : 1;
+    const bool timing = cfg_.kernel_timing != 0, counting = cfg_.count_traversal != 0;
+    if (counting && !d_counts_.ptr) {
+        d_counts_.alloc(kStatStride * kGroups);
+        MPSS_HIP(hipMemset(d_counts_.ptr, 0, kStatStride * kGroups * sizeof(unsigned long long)));
     }
-    if (!ws_count_.ptr) ws_count_.alloc(1);
-    size_t pi = 0;
-    while (pi < pieces.size()) {
-        // pack pieces into one batch
-        size_t pe = pi;
-        int64_t total = 0;
-        while (pe < pieces.size() && (pe == pi || total + pieces[pe].tb.nsamples <= max_batch))
-            total += pieces[pe++].tb.nsamples;
-        // hits <= samples; the hit arrays grow to the largest batch seen (<= ~290 B per hit)
-        if (ws_n_ < total) {
-            ws_flags_.alloc(total);
-            ws_slot_.alloc(total);
-            ws_n_ = total;
-        }
-        if (ws_hits_ < total) {
-            ws_ld_.alloc(total * ROW);
-            ws_q_.alloc(total);
-            ws_mo_.alloc(total * kGroups);
-            ws_ha_.alloc(total);
-            ws_hb_.alloc(total);
-            ws_hs_.alloc(total);
-            ws_xyz_.alloc(total);
-            ws_hits_ = total;
-        }
-        if (sc.any_tex && ws_tex_hits_ < total) {
-            ws_alb_.alloc(total);
-            ws_frame_.alloc(2 * total);
-            ws_tex_hits_ = total;
-        }
-        if (ws_px_ < total / spp) {
-            ws_spill_.alloc(total / spp);
-            ws_px_ = total / spp;
-        }
-        MPSS_HIP(hipMemsetAsync(ws_count_.ptr, 0, sizeof(int), stream));
-        MPSS_HIP(hipMemsetAsync(ws_spill_.ptr, 0, sizeof(uint32_t) * (size_t)(total / spp), stream));
-        int64_t off = 0;
-        hipEvent_t ev{};
-        time_begin(stream, ev);
-        for (size_t k = pi; k < pe; ++k) {
-            const TileBatch &tb = pieces[k].tb;
-            SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
-                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
-            hipLaunchKernelGGL(primary_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0,
-                               stream, sc, tb, rec);
-            off += tb.nsamples;
-        }
-        time_end(stream, ev, 1);
-        {
-            SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
-                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
-            int ns_max = 1;
-            for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
-            const int64_t lanes = total * std::max<int64_t>(1, (int64_t)scene_.lights.size()) * ns_max;
-            if (ws_terms_n_ < lanes) {
-                ws_terms_.alloc((size_t)lanes * 64);
-                ws_terms_n_ = lanes;
+    unsigned long long *const counts = counting ? d_counts_.ptr : nullptr;
+    const int64_t max_batch = std::max<int64_t>(cfg_.max_batch_samples, 1 << 16);
+    const int nlights = (int)scene_.lights.size();
+    int ns_max = 1;
+    for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
+    const float max_error = max_error_;
+    RenderWorkspace *ws = acquire_ws();
+    lk.unlock();
+
+    std::vector<Timed> timed;
+    int64_t n_samples = 0, n_sss = 0;
+    try {
+        if (ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
+        // a workspace buffer is reallocated only once its previous user's kernels are done
+        auto grow = [&](auto &buf, int64_t &have, int64_t want, size_t per) {
+            if (have >= want) return;
+            if (ws->pending) MPSS_HIP(hipEventSynchronize(ws->done));
+            buf.alloc((size_t)want * per);
+            have = want;
+        };
+        // cut rectangles into pieces of <= max_batch samples
+        struct Piece {
+            TileBatch tb;
+            float *out;
+        };
+        std::vector<Piece> pieces;
+        for (int i = 0; i < n; ++i) {
+            const int x0 = rects[4 * i], x1 = rects[4 * i + 1], y0 = rects[4 * i + 2], y1 = rects[4 * i + 3];
+            const int tw = x1 - x0;
+            const int ex0 = std::max(x0 - 1, 0);
+            const int ew = std::min(x1 + 1, W) - ex0;
+            const int rows = (int)std::max<int64_t>(1, max_batch / ((int64_t)ew * spp) - 2);
+            for (int yb = y0; yb < y1; yb += rows) {
+                const int ye = std::min(y1, yb + rows);
+                Piece p;
+                p.tb.x0 = x0;
+                p.tb.x1 = x1;
+                p.tb.y0 = yb;
+                p.tb.y1 = ye;
+                p.tb.ex0 = ex0;
+                p.tb.ey0 = std::max(yb - 1, 0);
+                p.tb.ew = ew;
+                p.tb.eh = std::min(ye + 1, H) - p.tb.ey0;
+                p.tb.spp = spp;
+                p.tb.seed = seed;
+                p.tb.nsamples = (int64_t)p.tb.ew * p.tb.eh * spp;
+                p.out = outs[i] + (size_t)(yb - y0) * tw * 4;
+                pieces.push_back(p);
             }
-            DirectTerms *terms = reinterpret_cast<DirectTerms *>(ws_terms_.ptr);
-            float4 *inf_st = nullptr;
-            if (sc.n_infinite > 0) {
-                if (ws_st_n_ < lanes) {
-                    ws_st_.alloc((size_t)lanes);
-                    ws_st_n_ = lanes;
+        }
+        size_t pi = 0;
+        while (pi < pieces.size()) {
+            // pack pieces into one batch
+            size_t pe = pi;
+            int64_t total = 0;
+            while (pe < pieces.size() && (pe == pi || total + pieces[pe].tb.nsamples <= max_batch))
+                total += pieces[pe++].tb.nsamples;
+            // hits <= samples; the hit arrays grow to the largest batch seen (<= ~290 B per hit)
+            if (ws->n < total) {
+                int64_t have = ws->n;
+                grow(ws->flags, have, total, 1);
+                have = ws->n;
+                grow(ws->slot, have, total, 1);
+                ws->n = total;
+            }
+            if (ws->hits < total) {
+                int64_t h0 = ws->hits;
+                for (auto *b : {&ws->q, &ws->ha, &ws->hb, &ws->xyz}) {
+                    int64_t have = h0;
+                    grow(*b, have, total, 1);
                 }
-                inf_st = ws_st_.ptr;
+                int64_t have = h0;
+                grow(ws->mo, have, total, kGroups);
+                have = h0;
+                grow(ws->ld, have, total, ROW);
+                have = h0;
+                grow(ws->hs, have, total, 1);
+                ws->hits = total;
             }
-            time_begin(stream, ev);
-            if (sc.any_tex)
-                hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
-                                   rec, spp, seed, (int)total);
-            if (!scene_.lights.empty()) {
-                hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, stream,
-                                   sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
+            if (sc.any_tex && ws->tex_hits < total) {
+                int64_t have = ws->tex_hits;
+                grow(ws->alb, have, total, 1);
+                have = ws->tex_hits;
+                grow(ws->frame, have, total, 2);
+                ws->tex_hits = total;
+            }
+            if (ws->px < total / spp) {
+                int64_t have = ws->px;
+                grow(ws->spill, have, total / spp, 1);
+                ws->px = total / spp;
+            }
+            MPSS_HIP(hipMemsetAsync(ws->count.ptr, 0, sizeof(int), stream));
+            MPSS_HIP(hipMemsetAsync(ws->spill.ptr, 0, sizeof(uint32_t) * (size_t)(total / spp), stream));
+            auto recs = [&](int64_t off) {
+                return SampleRecs{ws->flags.ptr + off, ws->spill.ptr + off / spp, ws->slot.ptr + off, ws->ld.ptr,
+                                  ws->ha.ptr, ws->hb.ptr, ws->hs.ptr, ws->q.ptr, ws->count.ptr, ws->mo.ptr,
+                                  ws->xyz.ptr, ws->alb.ptr, ws->frame.ptr};
+            };
+            int64_t off = 0;
+            hipEvent_t ev{};
+            time_begin(timing, stream, ev);
+            for (size_t k = pi; k < pe; ++k) {
+                const TileBatch &tb = pieces[k].tb;
+                hipLaunchKernelGGL(primary_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
+                                   sc, tb, recs(off));
+                off += tb.nsamples;
+            }
+            time_end(timing, stream, ev, 1, timed);
+            {
+                const SampleRecs rec = recs(0);
+                const int64_t lanes = total * std::max<int64_t>(1, (int64_t)nlights) * ns_max;
+                grow(ws->terms, ws->terms_n, lanes, 64);
+                DirectTerms *terms = reinterpret_cast<DirectTerms *>(ws->terms.ptr);
+                float4 *inf_st = nullptr;
+                if (sc.n_infinite > 0) {
+                    grow(ws->st, ws->st_n, lanes, 1);
+                    inf_st = ws->st.ptr;
+                }
+                time_begin(timing, stream, ev);
+                if (sc.any_tex)
+                    hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                                       sc, rec, spp, seed, (int)total);
+                if (nlights > 0) {
+                    hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
+                                       stream, sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
+                    if (sc.n_infinite > 0)
+                        hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((total + 255) / 256)),
+                                           dim3(256), 0, stream, sc, rec, (int)total, ns_max,
+                                           (const DirectTerms *)terms, (const float4 *)inf_st);
+                    else
+                        hipLaunchKernelGGL(direct_combine_kernel<false>, dim3((unsigned)((total + 255) / 256)),
+                                           dim3(256), 0, stream, sc, rec, (int)total, ns_max,
+                                           (const DirectTerms *)terms, (const float4 *)nullptr);
+                } else {
+                    hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                                       stream, sc, rec, (int)total);
+                }
+                time_end(timing, stream, ev, 4, timed);
+            }
+            if (!sss.empty()) {
+                time_begin(timing, stream, ev);
+                for (const SssMat &s : sss)
+                    launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)total, ws->q.ptr,
+                                   ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
+                                   ws->work.ptr, stream);
+                time_end(timing, stream, ev, 2, timed);
+            }
+            off = 0;
+            time_begin(timing, stream, ev);
+            {
+                const SampleRecs rec = recs(0);
+                hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
+                                   rec, (int)total);
                 if (sc.n_infinite > 0)
-                    hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                                       stream, sc, rec, (int)total, ns_max, (const DirectTerms *)terms,
-                                       (const float4 *)inf_st);
-                else
-                    hipLaunchKernelGGL(direct_combine_kernel<false>, dim3((unsigned)((total + 255) / 256)), dim3(256),
-                                       0, stream, sc, rec, (int)total, ns_max, (const DirectTerms *)terms,
-                                       (const float4 *)nullptr);
-            } else {
-                hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                                   sc, rec, (int)total);
+                    hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
+                                       rec, (int)total);
             }
-            time_end(stream, ev, 4);
-        }
-        if (m) {
-            if (cfg_.count_traversal && !d_counts_.ptr) {
-                d_counts_.alloc(2 * kGroups);
-                MPSS_HIP(hipMemset(d_counts_.ptr, 0, 2 * kGroups * sizeof(unsigned long long)));
+            for (size_t k = pi; k < pe; ++k) {
+                const TileBatch &tb = pieces[k].tb;
+                const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
+                hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, recs(off),
+                                   pieces[k].out, tw);
+                off += tb.nsamples;
             }
-            time_begin(stream, ev);
-            launch_mo_band(dev_octree_, m->dev_profile, max_error_, (int)total, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr,
-                           cfg_.count_traversal ? d_counts_.ptr : nullptr, stream);
-            time_end(stream, ev, 2);
+            time_end(timing, stream, ev, 3, timed);
+            MPSS_HIP(hipGetLastError());
+            n_samples += total;
+            if (counting) {  // instrumented pass only: synchronous read of the hit count
+                int cnt = 0;
+                MPSS_HIP(hipMemcpyAsync(&cnt, ws->count.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+                MPSS_HIP(hipStreamSynchronize(stream));
+                n_sss += cnt;
+            }
+            pi = pe;
         }
-        off = 0;
-        time_begin(stream, ev);
-        {
-            SampleRecs rec{ws_flags_.ptr, ws_spill_.ptr, ws_slot_.ptr, ws_ld_.ptr, ws_ha_.ptr, ws_hb_.ptr,
-                           ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
-            hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
-                               bp, (int)total);
-            if (sc.n_infinite > 0)
-                hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc, rec,
-                                   (int)total);
-        }
-        for (size_t k = pi; k < pe; ++k) {
-            const TileBatch &tb = pieces[k].tb;
-            SampleRecs rec{ws_flags_.ptr + off, ws_spill_.ptr + off / spp, ws_slot_.ptr + off, ws_ld_.ptr,
-                           ws_ha_.ptr, ws_hb_.ptr, ws_hs_.ptr, ws_q_.ptr, ws_count_.ptr, ws_mo_.ptr, ws_xyz_.ptr, ws_alb_.ptr, ws_frame_.ptr};
-            const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
-            hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, rec,
-                               pieces[k].out, tw);
-            off += tb.nsamples;
-        }
-        time_end(stream, ev, 3);
-        MPSS_HIP(hipGetLastError());
-        stats_.samples += total;
-        if (cfg_.count_traversal) {  // instrumented pass only: synchronous read of the hit count
-            int cnt = 0;
-            MPSS_HIP(hipMemcpyAsync(&cnt, ws_count_.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
-            MPSS_HIP(hipStreamSynchronize(stream));
-            stats_.sss_samples += cnt;
-        }
-        pi = pe;
+    } catch (...) {
+        release_ws(ws, stream);
+        throw;
+    }
+    release_ws(ws, stream);
+    lk.lock();
+    timed_.insert(timed_.end(), timed.begin(), timed.end());
+    stats_.samples += n_samples;
+    stats_.sss_samples += n_sss;
+}
+
+// Tile-cost probe (mpss_tile_costs): classes per pixel centre, summed per rectangle on the host.
+void Context::tile_costs(int n, const int32_t *rects, int64_t *sss, int64_t *surf) {
+    activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (scene_dirty_) upload_scene();
+    const int W = scene_.camera.xres, H = scene_.camera.yres;
+    if (W <= 0) throw Error(MPSS_ERR_INVALID, "tile_costs: no camera");
+    RenderScene sc = render_scene();
+    sc.have_octree = have_octree_ ? 1 : 0;
+    DevBuf<uint8_t> cls;
+    cls.alloc((size_t)W * H);
+    hipLaunchKernelGGL(probe_kernel, dim3((unsigned)(((int64_t)W * H + 255) / 256)), dim3(256), 0, 0, sc, 0, W, 0, H,
+                       cls.ptr);
+    MPSS_HIP(hipGetLastError());
+    std::vector<uint8_t> h((size_t)W * H);
+    MPSS_HIP(hipMemcpy(h.data(), cls.ptr, h.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) {
+        const int32_t *r = rects + 4 * i;
+        if (r[0] < 0 || r[2] < 0 || r[1] > W || r[3] > H || r[0] >= r[1] || r[2] >= r[3])
+            throw Error(MPSS_ERR_INVALID, "tile_costs: bad rectangle");
+        int64_t a = 0, b = 0;
+        for (int y = r[2]; y < r[3]; ++y)
+            for (int x = r[0]; x < r[1]; ++x) {
+                const uint8_t c = h[(size_t)y * W + x];
+                a += c == 2;
+                b += c >= 1;
+            }
+        sss[i] = a;
+        surf[i] = b;
     }
 }
 
-void Context::time_begin(hipStream_t s, hipEvent_t &a) {
-    if (!cfg_.kernel_timing) return;
+void Context::time_begin(bool on, hipStream_t s, hipEvent_t &a) {
+    if (!on) return;
     MPSS_HIP(hipEventCreate(&a));
     MPSS_HIP(hipEventRecord(a, s));
 }
 
-void Context::time_end(hipStream_t s, hipEvent_t a, int kind) {
-    if (!cfg_.kernel_timing) return;
+void Context::time_end(bool on, hipStream_t s, hipEvent_t a, int kind, std::vector<Timed> &out) {
+    if (!on) return;
     hipEvent_t b;
     MPSS_HIP(hipEventCreate(&b));
     MPSS_HIP(hipEventRecord(b, s));
-    timed_.push_back(Timed{a, b, kind});
+    out.push_back(Timed{a, b, kind});
 }
 
 mpss_render_stats Context::render_stats() {
     activate();
+    std::lock_guard<std::mutex> g(mu_);
     MPSS_HIP(hipDeviceSynchronize());
     for (const Timed &t : timed_) {
         float ms = 0.f;
@@ -658,17 +750,21 @@ mpss_render_stats Context::render_stats() {
     timed_.clear();
     mpss_render_stats out = stats_;
     const int sm = first_bssrdf_material();
-    for (int g = 0; g < kGroups; ++g)
+    for (int g2 = 0; g2 < kGroups; ++g2)
         for (int s = 0; s < 4; ++s)
-            out.group_bands[g][s] = sm >= 0 ? materials_[sm]->dev_profile.groups.band[g][s] : -1;
+            out.group_bands[g2][s] = sm >= 0 ? materials_[sm]->dev_profile.groups.band[g2][s] : -1;
     if (d_counts_.ptr) {
-        unsigned long long c[2 * kGroups];
+        unsigned long long c[kStatStride * kGroups];
         MPSS_HIP(hipMemcpy(c, d_counts_.ptr, sizeof(c), hipMemcpyDeviceToHost));
-        for (int g = 0; g < kGroups; ++g) {
-            out.mo_nodes += (int64_t)c[2 * g];
-            out.mo_points += (int64_t)c[2 * g + 1];
-            out.group_nodes[g] = (int64_t)c[2 * g];
-            out.group_points[g] = (int64_t)c[2 * g + 1];
+        for (int g2 = 0; g2 < kGroups; ++g2) {
+            out.mo_nodes += (int64_t)c[kStatStride * g2];
+            out.mo_points += (int64_t)c[kStatStride * g2 + 1];
+            out.group_nodes[g2] = (int64_t)c[kStatStride * g2];
+            out.group_points[g2] = (int64_t)c[kStatStride * g2 + 1];
+            out.mo_wave_node_iters += (int64_t)c[kStatStride * g2 + 2];
+            out.mo_wave_point_iters += (int64_t)c[kStatStride * g2 + 3];
+            out.mo_lookups += (int64_t)c[kStatStride * g2 + 4];
+            for (int k = 0; k < 3; ++k) out.mo_lookups_near[k] += (int64_t)c[kStatStride * g2 + 5 + k];
         }
     }
     return out;
@@ -676,8 +772,9 @@ mpss_render_stats Context::render_stats() {
 
 void Context::reset_render_stats() {
     (void)render_stats();  // drain pending events
+    std::lock_guard<std::mutex> g(mu_);
     stats_ = mpss_render_stats{};
-    if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, 2 * kGroups * sizeof(unsigned long long)));
+    if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, kStatStride * kGroups * sizeof(unsigned long long)));
 }
 
 int Context::first_bssrdf_material() const { return materials_.empty() ? -1 : 0; }

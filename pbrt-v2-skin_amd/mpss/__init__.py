@@ -12,7 +12,7 @@ import numpy as np
 
 NB = 30
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmpss.so")
+LIB_PATH = os.environ.get("MPSS_LIB") or os.path.join(_HERE, "libmpss.so")  # MPSS_LIB: a variant build (tools/)
 
 if not os.path.exists(LIB_PATH):
     raise ImportError("libmpss.so not built (%s): run __graft_entry__.build() or make -C pbrt-v2-skin_amd/csrc"
@@ -51,7 +51,8 @@ class RenderStats(C.Structure):
                 ("n_shade", C.c_int64), ("n_film", C.c_int64), ("samples", C.c_int64), ("sss_samples", C.c_int64),
                 ("mo_nodes", C.c_int64), ("mo_points", C.c_int64), ("group_nodes", C.c_int64 * 8),
                 ("group_points", C.c_int64 * 8), ("group_bands", (C.c_int32 * 4) * 8), ("ms_direct", C.c_double),
-                ("n_direct", C.c_int64)]
+                ("n_direct", C.c_int64), ("mo_wave_node_iters", C.c_int64), ("mo_wave_point_iters", C.c_int64),
+                ("mo_lookups", C.c_int64), ("mo_lookups_near", C.c_int64 * 3)]
 
 
 class LayeredSkin(C.Structure):
@@ -107,6 +108,7 @@ _sig("mpss_reset_render_stats", C.c_int, [vp])
 _sig("mpss_set_instrumentation", C.c_int, [vp, C.c_int, C.c_int])
 _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp])
 _sig("mpss_render_tiles", C.c_int, [vp, C.c_int, u32, C.c_int, C.POINTER(C.c_int32), C.POINTER(vp), vp])
+_sig("mpss_tile_costs", C.c_int, [vp, C.c_int, C.POINTER(C.c_int32), vp, vp])
 _sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
 _sig("mpss_mc_profile", C.c_int, [vp, f32p, C.c_int, C.c_float, C.c_int, C.c_uint64, C.c_uint64, vp, vp,
                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64), vp])
@@ -422,7 +424,8 @@ class Context:
         out = {}
         for k, _ in RenderStats._fields_:
             v = getattr(st, k)
-            out[k] = [list(x) for x in v] if k == "group_bands" else (list(v) if k.startswith("group_") else v)
+            out[k] = [list(x) for x in v] if k == "group_bands" else (
+                list(v) if k.startswith("group_") or k == "mo_lookups_near" else v)
         return out
 
     def set_instrumentation(self, kernel_timing=False, count_traversal=False):
@@ -436,6 +439,16 @@ class Context:
 
     def render_tile(self, spp, seed, x0, x1, y0, y1, out_dev, stream=None):
         check(_lib.mpss_render_tile(self.h, spp, seed, x0, x1, y0, y1, out_dev, stream))
+
+    def tile_costs(self, rects):
+        """Per rectangle (x0, x1, y0, y1): camera rays through pixel centres that hit a BSSRDF
+        surface, and that hit any mesh (mpss_tile_costs) -> two int64 arrays."""
+        n = len(rects)
+        r = (C.c_int32 * (4 * max(n, 1)))(*[int(v) for rc in rects for v in rc])
+        sss = np.zeros(max(n, 1), np.int64)
+        surf = np.zeros(max(n, 1), np.int64)
+        check(_lib.mpss_tile_costs(self.h, n, r, sss.ctypes.data, surf.ctypes.data))
+        return sss[:n], surf[:n]
 
     def render_tiles(self, spp, seed, rects, outs_dev, stream=None):
         """rects: [(x0, x1, y0, y1)], outs_dev: device pointers (one float4 XYZW tile each)."""

@@ -1,11 +1,23 @@
 """Image-tile sharding of the pixel loop across ranks.
 
 pbrt splits the film into RoundUpPow2(max(32*cores, W*H/256)) sampler tasks
-(renderers/samplerrenderer.cpp:177-199, Sampler::ComputeSubWindow in core/sampler.cpp:55-78);
-here the unit is a T x T pixel tile handed to one GPU, tiles are dealt to ranks interleaved
-(balancing the face in the middle of the frame against empty background), and each rank's
-film tiles reach rank 0 through one collective gather at the end of the frame.
+(renderers/samplerrenderer.cpp:191-217; Sampler::ComputeSubWindow, core/sampler.cpp:55-78);
+here the unit is a T x T pixel tile handed to one GPU, and each rank's film tiles reach rank 0
+through one collective gather at the end of the frame.
+
+Dealing. The skin sits in the middle of the frame and a tile's cost is dominated by its
+subsurface (Mo() gather) hits, so round-robin over a row-major grid is not balanced: with a
+grid 8, 16 or 32 tiles wide every rank owns whole tile columns. ``deal_snake`` sorts the tiles
+by an estimated cost (``mpss.Context.tile_costs``: one camera ray through every pixel centre,
+hits counted per tile -- integer counts, identical on every rank, so every rank derives the same
+deal without communicating) and deals them boustrophedon: ranks 0..N-1, then N-1..0, and so on.
+Every prefix of that order -- in particular "the tiles that contain skin" -- is then split with
+per-rank counts differing by at most one, and the per-rank costs by at most one tile's cost.
+``deal_diagonal`` is the geometry-free fallback: tile (tx, ty) goes to rank (tx + s * ty) mod N
+with s coprime to N, so a compact blob is spread over all ranks instead of over column owners.
 """
+import math
+
 import numpy as np
 
 
@@ -21,6 +33,50 @@ def rank_items(n_items, rank, world):
 
 def slots_per_rank(n_items, world):
     return (n_items + world - 1) // world
+
+
+def deal_snake(costs, world):
+    """Items sorted by decreasing cost (ties: lower index first) dealt boustrophedon over `world`
+    ranks. Returns per rank its item indices in increasing order. Deterministic."""
+    costs = np.asarray(costs, np.float64)
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    out = [[] for _ in range(world)]
+    for k, i in enumerate(order):
+        rnd, pos = divmod(k, world)
+        out[pos if rnd % 2 == 0 else world - 1 - pos].append(i)
+    return [sorted(x) for x in out]
+
+
+def _coprime_shift(world):
+    for s in (3, 5, 7, 11, 13, 2, 1):
+        if s < max(world, 2) and math.gcd(s, world) == 1:
+            return s
+    return 1
+
+
+def deal_diagonal(nx, ny, world):
+    """Tile (tx, ty) of an nx x ny row-major grid -> rank (tx + s * ty) % world."""
+    s = _coprime_shift(world)
+    out = [[] for _ in range(world)]
+    for ty in range(ny):
+        for tx in range(nx):
+            out[(tx + s * ty) % world].append(ty * nx + tx)
+    return out
+
+
+def tile_cost_model(sss_hits, surf_hits, pixels):
+    """Relative cost of a tile from its probe counts (one camera ray per pixel centre): a
+    subsurface hit runs the Mo() gather (~85 % of a C2 frame), a surface hit the direct
+    lighting, every pixel its camera rays and film work."""
+    return (np.asarray(sss_hits, np.float64) * 1.0 + np.asarray(surf_hits, np.float64) * 0.1
+            + np.asarray(pixels, np.float64) * 0.004)
+
+
+def balance(costs, deal):
+    """max over ranks of the dealt cost / mean over ranks (1.0 = perfect)."""
+    costs = np.asarray(costs, np.float64)
+    per = np.array([costs[list(d)].sum() if len(d) else 0.0 for d in deal])
+    return float(per.max() / max(per.mean(), 1e-30))
 
 
 def render_items(ctx, items, tiles, spp, seeds, out, T, stream=None):
