@@ -1,23 +1,32 @@
 """bench.py -- headline benchmark of the MI355X multipole skin path (BASELINE.json metric).
 
-A step = the pixel loop of one skin.pbrt frame per GPU (config C2: 1024x1024, 64 spp,
-MultipoleSubsurfaceIntegrator + LayeredSkin; SamplerRenderer::Render's task loop,
-samplerrenderer.cpp:177-236): every camera sample is traced, shaded (direct lighting + the
-Mo() octree gather) and splatted into the film. Frames are cut into 128x128 tiles dealt to
-ranks round-robin; rank 0 collects every rank's film tiles with one RCCL gather per step.
-Weak scaling: at N GPUs a step renders N frames (different sampler seeds). --config c3 / c5
-run BASELINE.json's 8-GPU configs instead (one frame per step split over the GPUs: strong
-scaling); they are reference points, the driver's bench line is C2.
+A step = the pixel loop of one skin.pbrt frame (SamplerRenderer::Render's task loop,
+samplerrenderer.cpp:191-217): every camera sample is traced, shaded (direct lighting + the
+Mo() octree gather) and splatted into the film; the film tiles of every rank reach rank 0
+through one RCCL gather per step.
+
+* N = 1 (default): config C2, skin.pbrt 1024x1024 at 64 spp on one MI355X -- BASELINE.json's
+  metric configuration.
+* N > 1 (default): config C3, ONE skin.pbrt 2048x2048 frame at 256 spp per step split over the
+  N GPUs (strong scaling: north_star's tile scaling of one frame). Tiles (64x64) are dealt by
+  estimated cost (mpss_tile_costs: camera rays through the pixel centres that hit skin; the
+  deal is computed identically on every rank, mpss/tiles.py deal_snake), so the face is spread
+  evenly. A secondary C2 weak-scaling figure (one C2 frame per GPU per step) rides along in
+  the same JSON line.
+* --config c3 / c5 select BASELINE.json's other configurations explicitly.
 
 Preprocess (tessellation, irradiance kernel, octree build) runs once before timing and is
 reported separately, as SURVEY.md §8d prescribes.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+  Without torchrun, --gpus N > 1 starts the N rank processes itself (before any GPU call).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
 import sys
 import time
 
@@ -31,6 +40,12 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # groups + 16 B x the record visits of the busiest group (position/area counted once per
 # query-record, as the reference reads them once). Re-reads the sharding adds are not counted.
 REC_HDR_BYTES = 16
+# The gather's real ceiling: L2 requests of per-lane 8-byte table gathers, measured by
+# tools/microbench/l2_gather.hip on MI355X (profiles/r02_l2_gather_ceiling.json).
+L2_GATHER_CEILING_REQ_S = 2.46e11
+# sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
+KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
+                  "pbrt-v2-skin_amd/csrc/octree.h")
 
 
 # BASELINE.json configs this bench runs: (label, resolution, spp, default scaling, mesh subdivision
@@ -44,32 +59,141 @@ CONFIGS = {
 }
 
 
-def parse():
+def kernel_source_hash():
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2",
-                    help="BASELINE.json config: c2 (default; the metric's), c3 or c5 (8-GPU configs, strong scaling)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config (default: c2 on one GPU, c3 strong scaling on several)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
                     help="weak: one frame per GPU per step; strong: one frame per step split over the GPUs "
                          "(default: the config's)")
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"))
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--tile", type=int, default=128)
+    ap.add_argument("--tile", type=int, default=None, help="tile size (default 128 on one GPU, 64 on several)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 weak-scaling figure at N > 1")
     ap.add_argument("--out", default=None, help="write rank 0's first frame as .pfm/.exr")
     ap.add_argument("--pmc-json", default=None,
                     help="rocprofv3 PMC summary (tools/summarize_prof.py) of this bench command; default: the "
-                         "newest profiles/*_pmc.json with a FETCH_SIZE entry for mo_band_kernel")
-    return ap.parse_args()
+                         "newest profiles/*_pmc.json whose source_hash matches the kernel sources")
+    a = ap.parse_args(argv)
+    if a.config is None:
+        a.config = "c2" if a.gpus == 1 else "c3"
+    if a.tile is None:
+        a.tile = 128 if a.gpus == 1 else 64
+    return a
 
 
-def main():
-    a = parse()
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned(local_rank, world, port, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    main(parse(argv))
+
+
+def launch(a, argv):
+    """--gpus N > 1 without torchrun: one spawned process per GPU (the parent never touches the
+    GPU), rendezvous on 127.0.0.1."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned, args=(a.gpus, _free_port(), argv), nprocs=a.gpus, join=True, start_method="spawn")
+
+
+def build_scene(a, label_cfg, local):
+    from mpss import pbrtscene
+    label, res, spp, scaling, subdiv = CONFIGS[label_cfg]
+    res = a.res or res
+    spp = a.spp or spp
+    sc = pbrtscene.load(a.scene, xres=res, yres=res, spp=spp)
+    pts = None
+    if subdiv:
+        pts = pbrtscene.mesh_points(sc)
+        sc.meshes = [pbrtscene.subdivide_mesh(me, subdiv) for me in sc.meshes]
+    t0 = time.perf_counter()
+    ctx = pbrtscene.build_context(sc, device=local)
+    t_mat = time.perf_counter() - t0
+    if pts is not None:
+        ctx.set_surface_points(pts)
+    t0 = time.perf_counter()
+    ctx.preprocess(seed=1)
+    import torch
+    torch.cuda.synchronize()
+    t_pre = time.perf_counter() - t0
+    return sc, ctx, label, scaling, subdiv, t_mat, t_pre
+
+
+def deal(ctx, sc, T, frames, world):
+    """Tiles of `frames` frames dealt over `world` ranks by estimated cost (identical on every rank)."""
+    import numpy as np
+    from mpss import tiles as tl
+    tiles = tl.tile_grid(sc.xres, sc.yres, T)
+    sss, surf = ctx.tile_costs(tiles)
+    px = np.array([(x1 - x0) * (y1 - y0) for x0, x1, y0, y1 in tiles])
+    cost1 = tl.tile_cost_model(sss, surf, px)
+    items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
+    costs = [cost1[t] for _, t in items_all]
+    by_rank_idx = tl.deal_snake(costs, world)
+    items_by_rank = [[items_all[i] for i in idx] for idx in by_rank_idx]
+    return tiles, items_by_rank, tl.balance(costs, by_rank_idx), int((np.asarray(sss) > 0).sum())
+
+
+def timed_steps(a, ctx, sc, tiles, items_by_rank, frames, T, rank, world, steps, warmup):
+    """Warmup + `steps` timed steps (barrier + synchronize on both sides); returns (max seconds
+    over ranks, the gather buffers of rank 0 or None, this rank's output buffer)."""
+    import torch
+    import torch.distributed as dist
+    from mpss import tiles as tl
+    mine = items_by_rank[rank]
+    slots = max(len(x) for x in items_by_rank)
+    seeds = [a.seed + f for f in range(frames)]
+    out = torch.zeros((max(slots, 1), T * T * 4), dtype=torch.float32, device="cuda")
+    gath = [torch.zeros_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        tl.render_items(ctx, mine, tiles, sc.spp, seeds, out, T, stream)
+        if world > 1:
+            dist.gather(out, gath if rank == 0 else None, dst=0)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt, gath, out
+
+
+def main(a):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -83,79 +207,41 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    import mpss
-    from mpss import pbrtscene, tiles as tl
+    from mpss import tiles as tl
 
-    label, res, spp, scaling, subdiv = CONFIGS[a.config]
-    res = a.res or res
-    spp = a.spp or spp
+    sc, ctx, label, scaling, subdiv, t_materials, t_pre = build_scene(a, a.config, local)
     scaling = a.scaling or scaling
-    sc = pbrtscene.load(a.scene, xres=res, yres=res, spp=spp)
-    pts = None
-    if subdiv:
-        pts = pbrtscene.mesh_points(sc)
-        sc.meshes = [pbrtscene.subdivide_mesh(me, subdiv) for me in sc.meshes]
-    t0 = time.perf_counter()
-    ctx = pbrtscene.build_context(sc, device=local)
-    t_materials = time.perf_counter() - t0
-    if pts is not None:
-        ctx.set_surface_points(pts)
-    t0 = time.perf_counter()
-    ctx.preprocess(seed=1)
-    torch.cuda.synchronize()
-    t_pre = time.perf_counter() - t0
     n_points = ctx.octree_info()["n_points"] if ctx.surface_points().size else 0
-
     frames = world if scaling == "weak" else 1  # weak: one frame's worth of work per GPU
     T = a.tile
-    tiles = tl.tile_grid(sc.xres, sc.yres, T)
-    items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
-    items_by_rank = [[items_all[i] for i in tl.rank_items(len(items_all), r, world)] for r in range(world)]
+    t0 = time.perf_counter()
+    tiles, items_by_rank, deal_balance, skin_tiles = deal(ctx, sc, T, frames, world)
+    t_deal = time.perf_counter() - t0
     mine = items_by_rank[rank]
-    slots = tl.slots_per_rank(len(items_all), world)
     seeds = [a.seed + f for f in range(frames)]
-    out = torch.zeros((slots, T * T * 4), dtype=torch.float32, device="cuda")
-    gath = [torch.zeros_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step():
-        tl.render_items(ctx, mine, tiles, sc.spp, seeds, out, T, stream)
-        if world > 1:
-            dist.gather(out, gath if rank == 0 else None, dst=0)
-
     # traversal-count pass (untimed): octree records the Mo gather reads for this workload
+    out_c = torch.zeros((max(1, len(mine)), T * T * 4), dtype=torch.float32, device="cuda")
     ctx.set_instrumentation(kernel_timing=False, count_traversal=True)
     ctx.reset_render_stats()
-    tl.render_items(ctx, mine, tiles, sc.spp, seeds, out, T, stream)
+    tl.render_items(ctx, mine, tiles, sc.spp, seeds, out_c, T, stream)
     cnt = ctx.render_stats()
-    ctx.set_instrumentation(kernel_timing=False, count_traversal=False)
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    del out_c
     ctx.set_instrumentation(kernel_timing=True, count_traversal=False)
     ctx.reset_render_stats()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt, gath, out = timed_steps(a, ctx, sc, tiles, items_by_rank, frames, T, rank, world, a.steps, a.warmup)
     st = ctx.render_stats()
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    ctx.set_instrumentation(kernel_timing=False, count_traversal=False)
 
     samples_per_step = frames * sc.xres * sc.yres * sc.spp
     value = samples_per_step * a.steps / dt / 1e6
-    # dominant kernel + Mo gather roofline (per-launch averages over the timed region)
+    # SSS-shaded samples (camera samples that run the Mo() gather): counted on every rank
+    sss = torch.tensor([cnt["sss_samples"], cnt["samples"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(sss)
+    sss_per_step, traced_per_step = float(sss[0].item()), float(sss[1].item())
+    # dominant kernel + Mo gather roofline (per-launch averages over the timed region, this rank)
     kern = {"primary": (st["ms_camera"], st["n_camera"]), "shade_direct": (st["ms_direct"], st["n_direct"]),
             "mo_band": (st["ms_shade"], st["n_shade"]),
             "film": (st["ms_film"], st["n_film"])}
@@ -174,10 +260,14 @@ def main():
     # the committed PMC summaries are of the C2 command; other configs report traffic only with --pmc-json
     pt = pmc_traffic(a.pmc_json, shade_launch_ms) if (a.config == "c2" or a.pmc_json) else None
     if pt:
-        roofline["traffic"] = pt["traffic"]
-        roofline["traffic_source"] = pt["source"] + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"
+        roofline["traffic"] = pt.get("traffic")
+        roofline["traffic_source"] = pt["source"]
         if "l2" in pt:
             roofline["l2_request_roofline"] = pt["l2"]
+
+    secondary = None
+    if world > 1 and a.config != "c2" and not a.no_secondary:
+        secondary = c2_weak_secondary(a, rank, world, local)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -191,21 +281,26 @@ def main():
                 "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh%s)" % (", subdivided" if subdiv else ""),
-                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles, RCCL film gather"
+                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles dealt by cost, RCCL film gather"
                            % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T),
                            "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
-                           "material_build_s": round(t_materials, 3),
+                           "material_build_s": round(t_materials, 3), "tile_deal_s": round(t_deal, 3),
+                           "tiles": len(tiles), "skin_tiles": skin_tiles, "deal_balance": round(deal_balance, 4),
+                           "sss_hit_fraction": round(sss_per_step / max(1.0, traced_per_step), 4),
+                           "sss_samples_per_s": round(sss_per_step * a.steps / dt, 1),
                            "mo_gbs": round(mo_gbs, 1), "mo_sss_samples": cnt["sss_samples"],
                            "mo_record_visits_per_sss_sample": round((cnt["mo_nodes"] + cnt["mo_points"]) /
                                                                     max(1, cnt["sss_samples"]), 2),
-                           "mo_group_visits": [a + b for a, b in zip(cnt["group_nodes"], cnt["group_points"])],
+                           "mo_group_visits": [x + y for x, y in zip(cnt["group_nodes"], cnt["group_points"])],
                            "mo_lane_efficiency": round((cnt["mo_nodes"] + cnt["mo_points"]) /
                                                        max(1, 64 * (cnt["mo_wave_node_iters"] +
                                                                     cnt["mo_wave_point_iters"])), 4),
                            "mo_lookup_near_fraction": [round(x / max(1, cnt["mo_lookups"]), 4)
                                                        for x in cnt["mo_lookups_near"]]},
                 "roofline": roofline, "cpu_baseline": cpu}
+        if secondary:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if a.out and rank == 0:
         from mpss import film
@@ -219,31 +314,56 @@ def main():
         dist.destroy_process_group()
 
 
-L2_PEAK_REQ_PER_S = 34.5e12 / 128  # MI355X L2 ~34.5 TB/s aggregate (MI355X_MICROARCH.md), 128-B lines
+def c2_weak_secondary(a, rank, world, local):
+    """C2 weak scaling beside a strong-scaling line: one skin.pbrt 1024x1024 64-spp frame per GPU
+    per step, tiles of all N frames dealt by cost over the N ranks."""
+    import torch
+    sc, ctx, _, _, _, _, _ = build_scene(a, "c2", local)
+    T = 128
+    tiles, items_by_rank, _, _ = deal(ctx, sc, T, world, world)
+    torch.cuda.synchronize()
+    dt, _, _ = timed_steps(a, ctx, sc, tiles, items_by_rank, world, T, rank, world, max(1, min(a.steps, 3)), 1)
+    steps = max(1, min(a.steps, 3))
+    ctx.close()
+    return {"c2_weak": {"value": round(world * sc.xres * sc.yres * sc.spp * steps / dt / 1e6, 3),
+                        "unit": "Msamples/s", "ms_per_step": round(dt / steps * 1e3, 3), "frames_per_step": world,
+                        "scaling": "weak"}}
 
 
 def pmc_traffic(path, launch_ms):
     """HBM-side traffic of one mo_band_kernel launch from a committed rocprofv3 PMC summary of
     the same bench command: FETCH_SIZE x 2 (the gfx950 correction, MI355X_MICROARCH.md), and
-    the L2 request rate (TCC_HIT + TCC_MISS per launch / launch time)."""
+    the L2 request rate (TCP_TCC_READ_REQ per launch / launch time) against the measured gather
+    ceiling. Only a summary whose source_hash matches the current kernel sources is used; an
+    older one is named as stale and its numbers are not attached."""
     import glob
-    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
-                                       reverse=True)  # newest round tag first (r01j > r01i > ... > r01)
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True)
+    want = kernel_source_hash()
+    stale = None
     for f in cands:
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        e = d.get("void mpss::mo_band_kernel<false>")
+        e = next((v for k, v in d.items() if k.startswith("void mpss::mo_band_kernel<false")), None)
         if not e or "fetch_bytes_corrected_mean" not in e:
             continue
-        out = {"traffic": e["fetch_bytes_corrected_mean"], "source": os.path.relpath(f, ROOT)}
-        if "TCC_HIT_sum" in e and launch_ms > 0:
-            req = e["TCC_HIT_sum"]["mean"] + e["TCC_MISS_sum"]["mean"]
+        if d.get("__meta__", {}).get("source_hash") != want:
+            stale = stale or os.path.relpath(f, ROOT)
+            continue
+        out = {"traffic": e["fetch_bytes_corrected_mean"],
+               "source": os.path.relpath(f, ROOT) + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"}
+        if "TCP_TCC_READ_REQ_sum" in e and launch_ms > 0:
+            req = e["TCP_TCC_READ_REQ_sum"]["mean"]
             out["l2"] = {"requests_per_launch": req, "achieved_req_per_s": req / (launch_ms * 1e-3),
-                         "peak_req_per_s": L2_PEAK_REQ_PER_S,
-                         "frac": req / (launch_ms * 1e-3) / L2_PEAK_REQ_PER_S, "hit_rate": e.get("l2_hit_rate")}
+                         "measured_ceiling_req_per_s": L2_GATHER_CEILING_REQ_S,
+                         "frac": req / (launch_ms * 1e-3) / L2_GATHER_CEILING_REQ_S,
+                         "hit_rate": e.get("l2_hit_rate"),
+                         "ceiling_source": "tools/microbench/l2_gather.hip (profiles/r02_l2_gather_ceiling.json)"}
         return out
+    if stale:
+        return {"traffic": None, "source": "none current: newest PMC summary %s was profiled on other kernel "
+                                           "sources (source_hash mismatch)" % stale}
     return None
 
 
@@ -260,4 +380,8 @@ def cpu_baseline(sc, ctx, a):
 
 
 if __name__ == "__main__":
-    main()
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch(args, sys.argv[1:])
+    else:
+        main(args)

@@ -30,6 +30,8 @@ def main(tag):
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, d in agg.items():
             e = out.setdefault(k, {})
+            if not isinstance(e, dict):
+                continue
             for c, v in d.items():
                 e[c] = {"dispatches": len(v), "mean": sum(v) / len(v)}
                 if c == "FETCH_SIZE":
@@ -37,6 +39,12 @@ def main(tag):
             if "TCC_HIT_sum" in e and "TCC_MISS_sum" in e:
                 h, m = e["TCC_HIT_sum"]["mean"], e["TCC_MISS_sum"]["mean"]
                 e["l2_hit_rate"] = h / (h + m) if h + m else None
+    sys.path.insert(0, ROOT)
+    import subprocess
+    from bench import kernel_source_hash  # the Mo-gather sources the counters describe
+    head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
+                          text=True).stdout.strip()
+    out["__meta__"] = {"source_hash": kernel_source_hash(), "git_head_at_summary": head}
     with open(os.path.join(dst, "%s_pmc.json" % tag), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print("wrote profiles/%s_*" % tag)
