@@ -10,7 +10,7 @@ through one RCCL gather per step.
 * N > 1 (default): config C3, ONE skin.pbrt 2048x2048 frame at 256 spp per step split over the
   N GPUs (strong scaling: north_star's tile scaling of one frame). Tiles (64x64) are dealt by
   estimated cost (mpss_tile_costs: camera rays through the pixel centres that hit skin; the
-  deal is computed identically on every rank, mpss/tiles.py deal_snake), so the face is spread
+  deal is computed identically on every rank, mpss/tiles.py deal_balanced), so the face is spread
   evenly. A secondary C2 weak-scaling figure (one C2 frame per GPU per step) rides along in
   the same JSON line.
 * --config c3 / c5 select BASELINE.json's other configurations explicitly.
@@ -151,7 +151,7 @@ def deal(ctx, sc, T, frames, world):
     cost1 = tl.tile_cost_model(sss, surf, px)
     items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
     costs = [cost1[t] for _, t in items_all]
-    by_rank_idx = tl.deal_snake(costs, world)
+    by_rank_idx = tl.deal_balanced(costs, world)
     items_by_rank = [[items_all[i] for i in idx] for idx in by_rank_idx]
     return tiles, items_by_rank, tl.balance(costs, by_rank_idx), int((np.asarray(sss) > 0).sum())
 

@@ -245,8 +245,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     const int grp = (int)(blockIdx.x & (kGroups - 1));
     const int tid = (int)threadIdx.x;
     const int nq = a.count ? *a.count : a.nq;
-    if (KLDS > 0 && (int)(blockIdx.x / kGroups) * BS < nq) {
-        // the group's near field: entries 0..KLDS of each band (past the table end: 0)
+    if (KLDS > 0) {
+        // the group's near field: entries 0..KLDS of each band (past the table end: 0). Every
+        // workgroup fills it: chunks go to whichever workgroup asks first, not by block index.
         for (int i = tid; i < 4 * (KLDS + 2); i += BS) {
             const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
             lt[i] = (c >= 0 && k <= KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;

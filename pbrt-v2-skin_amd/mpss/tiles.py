@@ -7,12 +7,13 @@ through one collective gather at the end of the frame.
 
 Dealing. The skin sits in the middle of the frame and a tile's cost is dominated by its
 subsurface (Mo() gather) hits, so round-robin over a row-major grid is not balanced: with a
-grid 8, 16 or 32 tiles wide every rank owns whole tile columns. ``deal_snake`` sorts the tiles
-by an estimated cost (``mpss.Context.tile_costs``: one camera ray through every pixel centre,
-hits counted per tile -- integer counts, identical on every rank, so every rank derives the same
-deal without communicating) and deals them boustrophedon: ranks 0..N-1, then N-1..0, and so on.
-Every prefix of that order -- in particular "the tiles that contain skin" -- is then split with
-per-rank counts differing by at most one, and the per-rank costs by at most one tile's cost.
+grid 8, 16 or 32 tiles wide every rank owns whole tile columns. ``deal_balanced`` sorts the
+tiles by an estimated cost (``mpss.Context.tile_costs``: one camera ray through every pixel
+centre, hits counted per tile -- integer counts, identical on every rank, so every rank derives
+the same deal without communicating) and deals them in rounds, one tile per rank per round,
+the heaviest tile of a round to the least-loaded rank. Every prefix of that order -- in
+particular "the tiles that contain skin" -- is split with per-rank counts differing by at most
+one, and the costs balance as in longest-processing-time-first dealing.
 ``deal_diagonal`` is the geometry-free fallback: tile (tx, ty) goes to rank (tx + s * ty) mod N
 with s coprime to N, so a compact blob is spread over all ranks instead of over column owners.
 """
@@ -35,15 +36,23 @@ def slots_per_rank(n_items, world):
     return (n_items + world - 1) // world
 
 
-def deal_snake(costs, world):
-    """Items sorted by decreasing cost (ties: lower index first) dealt boustrophedon over `world`
-    ranks. Returns per rank its item indices in increasing order. Deterministic."""
+def deal_balanced(costs, world):
+    """Items dealt in rounds of `world`: items sorted by decreasing cost (ties: lower index
+    first); in each round the round's heaviest item goes to the rank with the least cost so far,
+    the next to the next-least, and so on (ties: lower rank). Every rank gets one item per round,
+    so any prefix of the order -- e.g. "the tiles that contain skin" -- is split with per-rank
+    counts differing by at most one, and costs stay balanced as in longest-processing-time-first
+    dealing. Returns per rank its item indices in increasing order. Deterministic."""
     costs = np.asarray(costs, np.float64)
     order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0.0] * world
     out = [[] for _ in range(world)]
-    for k, i in enumerate(order):
-        rnd, pos = divmod(k, world)
-        out[pos if rnd % 2 == 0 else world - 1 - pos].append(i)
+    for r0 in range(0, len(order), world):
+        rnd = order[r0:r0 + world]
+        ranks = sorted(range(world), key=lambda k: (load[k], k))
+        for i, k in zip(rnd, ranks):
+            out[k].append(i)
+            load[k] += costs[i]
     return [sorted(x) for x in out]
 
 
