@@ -96,6 +96,10 @@ typedef struct {
     int desired_length;   /* "desiredlength" = 512 */
     int lerp_on_thin_slab;/* "lerponthinslab" = true */
     int double_ref_sslf;  /* "doublerefsslf" = false (FixedFresnelDielectric) */
+    int use_monte_carlo;  /* "usemontecarlo" = false: the profile is a Monte-Carlo random walk per band
+                             (ComputeMonteCarloProfile, multipole.cpp:298-368) on this context's GPU,
+                             and Li uses Ft = 1 (multipolesubsurface.cpp:283-286) */
+    uint64_t photons;     /* "photons" = 10000000 (per band) */
 } mpss_layeredskin;
 
 void mpss_layeredskin_defaults(mpss_layeredskin *m);
@@ -237,6 +241,13 @@ typedef struct { float mua, musp, ior, thickness; } mpss_layer; /* core/layer.h:
 int mpss_mc_profile(mpss_ctx *ctx, const mpss_layer *layers, int nlayers, float mfp_range, int nsegments,
                     uint64_t nphotons, uint64_t seed, double *reflectance, double *transmittance, double *total_r,
                     double *total_t, uint64_t *events, void *stream);
+
+/* MultipoleReferenceTask (mcprofile.cpp:356-425): the multipole model of the same layers (MPC at
+ * desiredLength 1024, step extent * 1.01 / 1024, lerp on thin slabs or not) sampled at the ring
+ * centres (i + .5) * extent / nsegments, extent = mfp_range * mean_l 1/(mua + musp); host code,
+ * no device needed. Outputs per ring (double) and the MPC totals. */
+int mpss_mc_reference(const mpss_layer *layers, int nlayers, float mfp_range, int nsegments, int lerp_on_thin_slab,
+                      double *reflectance, double *transmittance, double *total_r, double *total_t);
 
 /* ---- host-side utilities (no HIP device needed): the product's own parse-time builders,
  * exposed so their results can be checked on a CPU-only machine. ---- */

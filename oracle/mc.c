@@ -42,7 +42,7 @@ int o_mc_profile(const o_mc_layer *layers, int n, float mfp_range, int nseg, uin
     depth[0] = 0.;
     for (int i = 0; i < n && i < 64; ++i) {
         depth[i + 1] = d += (double)layers[i].thickness;
-        mfp_total += 1. / ((double)layers[i].mua + (double)layers[i].musp);
+        mfp_total += 1. / (double)(layers[i].mua + layers[i].musp); /* float sum (mcprofile.cpp:458-460) */
     }
     const double extent = mfp_range * (mfp_total / (double)n);
     if (extent_out) *extent_out = extent;
@@ -132,7 +132,7 @@ int o_mc_profile(const o_mc_layer *layers, int n, float mfp_range, int nseg, uin
                     double u1 = rng_next(&rng), u2 = rng_next(&rng);
                     double z = 1. - 2. * u1;
                     double r = sqrt(fmax(0., 1. - z * z));
-                    double phi = 2. * 3.14159265358979323846 * u2;
+                    double phi = 2. * (double)3.14159265358979323846f * u2; /* pbrt's float M_PI (pbrt.h:196) */
                     dx = r * cos(phi);
                     dy = r * sin(phi);
                     dz = z;

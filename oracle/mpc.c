@@ -317,6 +317,20 @@ int o_mpc_profile(int nlayers, const o_layer_spec *sp, float step, int desired_l
     return outlen;
 }
 
+/* MPC_ResampleDistribution (MultipoleProfileCalculator.cpp:429-448): the profile at distances
+ * points[i] (squared before the lookup). */
+void o_mpc_resample(int len, const float *d, const float *R, const float *T, int n, const float *points, float *r,
+                    float *t) {
+    for (int i = 0; i < n; ++i) resample1(len, d, R, T, points[i] * points[i], r + i, t + i);
+}
+
+/* MPC_ResampleForUniformDistanceSquaredDistribution (:404-426) with an explicit target length:
+ * out[i] = the profile at d^2 = (float)i * d[len-1] / (float)(target - 1). */
+void o_mpc_resample_uniform(int len, const float *d, const float *R, int target, float *out) {
+    float ext = d[len - 1], dummy;
+    for (int i = 0; i < target; ++i) resample1(len, d, R, R, (float)i * ext / (float)(target - 1), out + i, &dummy);
+}
+
 int cmp_ent(const void *a, const void *b) {
     typedef struct { float dsq; unsigned ord; float r, t; } ent;
     const ent *x = (const ent *)a, *y = (const ent *)b;

@@ -61,6 +61,11 @@ int o_mpc_profile(int nlayers, const o_layer_spec *specs, float step, int desire
                   int lerp_on_thin_slab, int resample, float **dsq, float **refl, float **trans,
                   float *total_r, float *total_t);
 void o_free(void *p);
+/* MPC_ResampleDistribution (:429-448) of an unresampled o_mpc_profile output at distances points[] */
+void o_mpc_resample(int len, const float *d, const float *R, const float *T, int n, const float *points, float *r,
+                    float *t);
+/* MPC_ResampleForUniformDistanceSquaredDistribution (:404-426) to `target` entries */
+void o_mpc_resample_uniform(int len, const float *d, const float *R, int target, float *out);
 float o_dipole_rd(float eta0, float etad, float d, float mua, float musp, int zi, int lerp, float dsq);
 
 /* Per-channel profile (multipole.cpp:241-295). table: [O_NB][*len] floats (channel-major). */

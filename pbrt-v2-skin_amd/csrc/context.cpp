@@ -124,7 +124,9 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     sp.double_ref_sslf = m.double_ref_sslf != 0;
     LayerParams lp;
     skin_layer_params(sp, lp);
-    if (cfg_.profile_on_host || sp.desired_length > 1024)
+    if (m.use_monte_carlo)
+        build_profile_mc(lp, m.photons, 89, mat->profile);
+    else if (cfg_.profile_on_host || sp.desired_length > 1024)
         build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
     else
         build_profile_gpu(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
@@ -135,6 +137,7 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     mat->roughness = m.roughness;
     mat->ior = m.layer_ior[0];
     mat->double_ref_sslf = m.double_ref_sslf != 0;
+    mat->is_monte_carlo = m.use_monte_carlo != 0;  // Ft = 1 in Li (multipolesubsurface.cpp:285)
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));

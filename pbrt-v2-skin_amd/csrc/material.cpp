@@ -375,7 +375,159 @@ void parallel_for(int n, int nthreads, F &&fn) {
     for (auto &x : th) x.join();
 }
 
+// 2-D FFT with the rows, then the columns, spread over threads (the 4096^2 transforms of the
+// desiredLength-1024 reference profiles).
+void fft2_par(const FFT1 &f, std::vector<cd> &A, int M, bool inverse) {
+    parallel_for(M, 0, [&](int r) { f.run(&A[(size_t)r * M], inverse); });
+    constexpr int kCols = 8;
+    parallel_for(M / kCols, 0, [&](int cb) {
+        std::vector<cd> col((size_t)M);
+        for (int c = cb * kCols; c < (cb + 1) * kCols; ++c) {
+            for (int r = 0; r < M; ++r) col[r] = A[(size_t)r * M + c];
+            f.run(col.data(), inverse);
+            for (int r = 0; r < M; ++r) A[(size_t)r * M + c] = col[r];
+        }
+    });
+}
+
+void to_freq_par(const FFT1 &f, const std::vector<double> &P, int N, std::vector<cd> &out) {
+    const int M = 2 * N, c = (N - 1) / 2;
+    out.assign((size_t)M * M, cd(0, 0));
+    for (int i = 0; i < N; ++i) {
+        const int ii = (M - c + i) % M;
+        for (int j = 0; j < N; ++j) out[(size_t)ii * M + (M - c + j) % M] = cd(P[(size_t)i * N + j], 0);
+    }
+    fft2_par(f, out, M, false);
+}
+
+void to_time_par(const FFT1 &f, std::vector<cd> &F, int N, std::vector<double> &out) {
+    const int M = 2 * N, c = (N - 1) / 2;
+    fft2_par(f, F, M, true);
+    const double s = 1.0 / ((double)M * (double)M);
+    out.assign((size_t)N * N, 0.0);
+    for (int i = 0; i < N; ++i) {
+        const int ii = (M - c + i) % M;
+        for (int j = 0; j < N; ++j) out[(size_t)i * N + j] = F[(size_t)ii * M + (M - c + j) % M].real() * s;
+    }
+}
+
 }  // namespace
+
+// MPC_ComputeDiffusionProfile for any layer stack (MultipoleProfileCalculator.cpp:294-346):
+// layer grids (ComputeLayerProfile :151-230), pairwise frequency-domain combination with the
+// time-domain crop between combinations (CombineLayerProfiles :253-280 via ToTimeDomain
+// :243-250), the unique-d^2 readout of R and T (:316-345; the first (i, j) of each d^2 wins) and
+// the Kahan totals of both grids.
+void mpc_compute(const MpcLayer *L, int n, float step, int desired_length, bool lerp_thin, MpcOutput &out) {
+    if (n < 1) throw Error(-1, "mpc: no layers");
+    const int length = (int)round_up_pow2((unsigned)desired_length);
+    const int N = 2 * length;
+    std::vector<double> R0, T0, R1, T1;
+    layer_grid(L[0].ior, n > 1 ? L[0].ior / L[1].ior : L[0].ior, L[0].thickness, L[0].mua, L[0].musp, step,
+               lerp_thin, N, R0, T0);
+    if (n > 1) {
+        FFT1 f(2 * N);
+        for (int i = 1; i < n; ++i) {
+            const float lo = n > i + 1 ? L[i].ior / L[i + 1].ior : L[i].ior;
+            layer_grid(L[i].ior / L[i - 1].ior, lo, L[i].thickness, L[i].mua, L[i].musp, step, lerp_thin, N, R1, T1);
+            std::vector<cd> fR1, fR2, fT1, fT2;
+            to_freq_par(f, R0, N, fR1);
+            to_freq_par(f, R1, N, fR2);
+            to_freq_par(f, T0, N, fT1);
+            to_freq_par(f, T1, N, fT2);
+            std::vector<cd> &fR12 = fR2, &fT12 = fT2;  // in place: each k reads its own inputs first
+            for (size_t k = 0; k < fR1.size(); ++k) {
+                const cd r1 = fR1[k], r2 = fR2[k], t1 = fT1[k], t2 = fT2[k];
+                const cd one = cd(1, 0) - r2 * r1;  // fOneR2R1 = 1 - fR2 fR1
+                fR12[k] = t1 * r2 * t1 / one + r1;
+                fT12[k] = t1 * t2 / one;
+            }
+            fR1.clear();
+            fT1.clear();
+            to_time_par(f, fR12, N, R0);
+            to_time_par(f, fT12, N, T0);
+        }
+    }
+    const unsigned c = (unsigned)length - 1, ext = c;
+    const float denorm = 1.f / (step * step);
+    std::vector<uint8_t> seen((size_t)ext * ext * 2 + 1, 0);
+    struct Ent {
+        unsigned nsq;
+        float r, t;
+    };
+    std::vector<Ent> ents;
+    for (unsigned i = 0; i <= ext; ++i)
+        for (unsigned j = i; i * i + j * j <= ext * ext; ++j) {
+            const unsigned nsq = i * i + j * j;
+            if (seen[nsq]) continue;
+            seen[nsq] = 1;
+            const size_t at = (size_t)(c + i) * N + (c + j);
+            ents.push_back(Ent{nsq, (float)R0[at] * denorm, (float)T0[at] * denorm});
+        }
+    std::sort(ents.begin(), ents.end(), [](const Ent &a, const Ent &b) { return a.nsq < b.nsq; });
+    out.dsq.resize(ents.size());
+    out.refl.resize(ents.size());
+    out.trans.resize(ents.size());
+    for (size_t k = 0; k < ents.size(); ++k) {
+        out.dsq[k] = (float)ents[k].nsq * step * step;
+        out.refl[k] = ents[k].r;
+        out.trans[k] = ents[k].t;
+    }
+    out.total_reflectance = (float)kahan(R0);
+    out.total_transmittance = (float)kahan(T0);
+}
+
+// MPC_ResampleDistribution (MultipoleProfileCalculator.cpp:429-449): the profile at distances
+// samplePoints (d^2 = point * point in float) by the interpolation search of resample().
+void mpc_resample_distribution(const MpcOutput &in, int n, const float *points, float *refl, float *trans) {
+    for (int i = 0; i < n; ++i) {
+        const float dsq = points[i] * points[i];
+        refl[i] = resample_at(in.dsq, in.refl, dsq);
+        trans[i] = resample_at(in.dsq, in.trans, dsq);
+    }
+}
+
+// MultipoleReferenceTask::Run (renderers/mcprofile.cpp:381-425): the multipole profile of the
+// MC scene's layers at desiredLength 1024 with step extent * 1.01 / 1024, sampled at the ring
+// centres (i + .5) * extent / nSegments.
+void mc_reference_profile(const MpcLayer *layers, int n, double extent, int nsegments, bool lerp_thin, double *refl,
+                          double *trans, double *total_r, double *total_t) {
+    MpcOutput o;
+    const int desired = 1024;
+    mpc_compute(layers, n, (float)(extent * 1.01 / desired), desired, lerp_thin, o);
+    *total_r = o.total_reflectance;
+    *total_t = o.total_transmittance;
+    std::vector<float> pts(nsegments), r(nsegments), t(nsegments);
+    for (int i = 0; i < nsegments; ++i) pts[i] = (float)((i + .5) * (extent / nsegments));
+    mpc_resample_distribution(o, nsegments, pts.data(), r.data(), t.data());
+    for (int i = 0; i < nsegments; ++i) {
+        refl[i] = r[i];
+        trans[i] = t[i];
+    }
+}
+
+// ComputeMonteCarloProfile's conversion of one band's ring profile (multipole.cpp:328-355): the
+// rings as an MPC_Output at d^2 = (float)(((i + .5) * extent / n)^2), values cast to float,
+// resampled to `target` entries uniform in d^2.
+void profile_from_rings(const double *refl, int nseg, double extent, int target, std::vector<float> &table,
+                        float &rcp, float &spacing) {
+    std::vector<float> d(nseg), r(nseg);
+    for (int i = 0; i < nseg; ++i) {
+        const double x = (i + 0.5) * extent / (double)nseg;
+        d[i] = (float)(x * x);
+        r[i] = (float)refl[i];
+    }
+    const float ext = d.back();
+    table.resize(target);
+    float last = 0.f;
+    for (int i = 0; i < target; ++i) {
+        const float q = (float)i * ext / (float)(target - 1);
+        last = q;
+        table[i] = resample_at(d, r, q);
+    }
+    spacing = last / (float)(target - 1);
+    rcp = (float)(target - 1) / last;
+}
 
 void build_profile(const LayerParams &lp, int desired_length, bool lerp_thin, ProfileTables &out, int nthreads) {
     std::vector<std::vector<float>> tabs(NB);

@@ -47,4 +47,26 @@ void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_on_t
 void build_rho_table(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
                      RhoTable &out, int nthreads = 0);
 
+// MPC_LayerSpec (MultipoleProfileCalculator.h; g_HG unused by the multipole code)
+struct MpcLayer {
+    float mua, musp, ior, thickness;
+};
+struct MpcOutput {  // MPC_Output before resampling: the unique-d^2 samples
+    std::vector<float> dsq, refl, trans;
+    float total_reflectance = 0.f, total_transmittance = 0.f;
+};
+void mpc_compute(const MpcLayer *layers, int n, float step, int desired_length, bool lerp_on_thin_slab,
+                 MpcOutput &out);
+void mpc_resample_distribution(const MpcOutput &in, int n, const float *points, float *refl, float *trans);
+// MultipoleReferenceTask (mcprofile.cpp:381-425): ring-centre profile of the layers' multipole model
+void mc_reference_profile(const MpcLayer *layers, int n, double extent, int nsegments, bool lerp_on_thin_slab,
+                          double *refl, double *trans, double *total_r, double *total_t);
+
+// ComputeMonteCarloProfile's ring -> table conversion (multipole.cpp:328-355) for one band
+void profile_from_rings(const double *refl, int nseg, double extent, int target, std::vector<float> &table,
+                        float &rcp, float &spacing);
+// usemontecarlo (multipole.cpp:298-368): per band, a GPU random walk of `photons` photons over
+// 4096 rings within 12 mean free paths, resampled to 65536 entries uniform in d^2 (mc_profile.hip)
+void build_profile_mc(const LayerParams &lp, uint64_t photons, uint64_t seed, ProfileTables &out);
+
 }  // namespace mpss

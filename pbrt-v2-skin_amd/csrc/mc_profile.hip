@@ -9,6 +9,7 @@
 // (ds_add_f64) and are flushed to HBM once per workgroup. All arithmetic is FP64 as in the
 // reference (DVector / DRay / DPoint, mcprofile.cpp:46-49).
 #include "mc_profile.h"
+#include "material.h"
 
 #include <algorithm>
 #include <cstring>
@@ -18,13 +19,16 @@ namespace mpss {
 
 namespace {
 
-constexpr int kMcMaxSegments = 2048;
+constexpr int kMcMaxSegments = 4096;  // ComputeMonteCarloProfile tallies 4096 rings (multipole.cpp:322)
+// pbrt's M_PI is the float literal 3.14159265358979323846f (core/pbrt.h:193-196); the walk and the
+// ring normalisation use it widened to double
+constexpr double kPbrtPi = (double)3.14159265358979323846f;
 
 // UniformSampleSphereD (mcprofile.cpp:51-58); u1 is drawn before u2
 __device__ __forceinline__ void sample_sphere_d(double u1, double u2, double &x, double &y, double &z) {
     z = 1. - 2. * u1;
     const double r = sqrt(fmax(0., 1. - z * z));
-    const double phi = 2. * 3.14159265358979323846 * u2;
+    const double phi = 2. * kPbrtPi * u2;
     x = r * cos(phi);
     y = r * sin(phi);
 }
@@ -44,8 +48,9 @@ struct McArgs {
     unsigned long long *events;  // nullable: total free-flight events
 };
 
+template <int NSEG>
 __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
-    __shared__ double h_r[kMcMaxSegments], h_t[kMcMaxSegments];
+    __shared__ double h_r[NSEG], h_t[NSEG];
     const McScene &sc = a.sc;
     for (int i = threadIdx.x; i < sc.nsegments; i += blockDim.x) h_r[i] = h_t[i] = 0.;
     __syncthreads();
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
 
 McScene make_mc_scene(const McLayer *layers, int n, double mfp_range, int nsegments) {
     if (n < 1 || n > kMcMaxLayers) throw Error(-1, "mc_profile: 1..8 layers supported");
-    if (nsegments < 1 || nsegments > kMcMaxSegments) throw Error(-1, "mc_profile: 1..2048 segments supported");
+    if (nsegments < 1 || nsegments > kMcMaxSegments) throw Error(-1, "mc_profile: 1..4096 segments supported");
     McScene sc{};
     sc.nlayers = n;
     double depth = 0., mfp_total = 0.;
@@ -208,7 +213,7 @@ McScene make_mc_scene(const McLayer *layers, int n, double mfp_range, int nsegme
             throw Error(-1, "mc_profile: layers need musp > 0, mua >= 0, thickness > 0");
         sc.layer[i] = layers[i];
         sc.depth[i + 1] = depth += (double)layers[i].thickness;
-        mfp_total += 1. / ((double)layers[i].mua + (double)layers[i].musp);  // Render (:460-464)
+        mfp_total += 1. / (double)(layers[i].mua + layers[i].musp);  // float sum (Render :458-460)
     }
     sc.extent = mfp_range * (mfp_total / (double)n);
     sc.nsegments = nsegments;
@@ -231,7 +236,13 @@ void run_mc_profile(const McScene &sc, uint64_t nphotons, uint64_t seed, double 
     MPSS_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const uint64_t lanes_needed = (nphotons + 255) / 256;
     const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ncu * 8, lanes_needed));
-    if (nphotons > 0) hipLaunchKernelGGL(mc_profile_kernel, dim3(blocks), dim3(256), 0, stream, a);
+    // LDS ring tallies: 32 KB up to 2048 rings; 64 KB for ComputeMonteCarloProfile's 4096
+    if (nphotons > 0) {
+        if (sc.nsegments <= 2048)
+            hipLaunchKernelGGL(mc_profile_kernel<2048>, dim3(blocks), dim3(256), 0, stream, a);
+        else
+            hipLaunchKernelGGL(mc_profile_kernel<kMcMaxSegments>, dim3(blocks), dim3(256), 0, stream, a);
+    }
     MPSS_HIP(hipGetLastError());
     std::vector<double> r(sc.nsegments), t(sc.nsegments);
     unsigned long long cnt[2];
@@ -244,7 +255,7 @@ void run_mc_profile(const McScene &sc, uint64_t nphotons, uint64_t seed, double 
     for (int i = 0; i < sc.nsegments; ++i) {
         const double sum = (double)(2 * i + 1) * sc.extent / sc.nsegments;
         const double h = sc.extent / sc.nsegments;
-        const double area = 3.14159265358979323846 * sum * h;
+        const double area = kPbrtPi * sum * h;
         const double factor = (double)nphotons * area;
         tr += r[i];
         tt += t[i];
@@ -254,6 +265,28 @@ void run_mc_profile(const McScene &sc, uint64_t nphotons, uint64_t seed, double 
     *total_r = tr / (double)nphotons;
     *total_t = tt / (double)nphotons;
     if (events) *events = cnt[1];
+}
+
+void build_profile_mc(const LayerParams &lp, uint64_t photons, uint64_t seed, ProfileTables &out) {
+    constexpr int kSegments = 4096;        // multipole.cpp:318
+    constexpr double kMfpRange = 12.0f;    // :319
+    constexpr int kTarget = kSegments * 16;  // :341
+    std::vector<double> refl(kSegments), trans(kSegments);
+    out.length = kTarget;
+    out.table.resize((size_t)NB * kTarget);
+    std::vector<float> tab;
+    for (int c = 0; c < NB; ++c) {
+        McLayer l[2];
+        for (int k = 0; k < 2; ++k) l[k] = McLayer{lp.mua[k][c], lp.musp[k][c], lp.eta[k], lp.thickness[k]};
+        const McScene sc = make_mc_scene(l, 2, kMfpRange, kSegments);
+        double tr = 0., tt = 0.;
+        // every band walks the same photon streams, as every band's MonteCarloProfileRenderer
+        // seeds its tasks alike (RNG(89 * taskId), mcprofile.cpp:223)
+        run_mc_profile(sc, photons, seed, refl.data(), trans.data(), &tr, &tt, nullptr, nullptr);
+        profile_from_rings(refl.data(), kSegments, sc.extent, kTarget, tab, out.rcp[c], out.spacing[c]);
+        out.total_reflectance[c] = (float)tr;
+        std::copy(tab.begin(), tab.end(), out.table.begin() + (size_t)c * kTarget);
+    }
 }
 
 }  // namespace mpss

@@ -6,6 +6,7 @@
 
 #include "../../include/mpss.h"
 #include "context.h"
+#include "material.h"
 #include "mc_profile.h"
 #include "spectral.h"
 
@@ -92,6 +93,8 @@ void mpss_layeredskin_defaults(mpss_layeredskin *m) {
     m->desired_length = 512;
     m->lerp_on_thin_slab = 1;
     m->double_ref_sslf = 0;
+    m->use_monte_carlo = 0;
+    m->photons = 10000000ull;
 }
 
 int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {
@@ -333,6 +336,24 @@ int mpss_mc_profile(mpss_ctx *c, const mpss_layer *layers, int n, float mfp_rang
         static_assert(sizeof(mpss_layer) == sizeof(McLayer), "layer layout");
         const McScene sc = make_mc_scene(reinterpret_cast<const McLayer *>(layers), n, (double)mfp_range, nseg);
         run_mc_profile(sc, nphotons, seed, refl, trans, tr, tt, events, (hipStream_t)stream);
+    });
+}
+
+int mpss_mc_reference(const mpss_layer *layers, int n, float mfp_range, int nseg, int lerp, double *refl,
+                      double *trans, double *tr, double *tt) {
+    return guarded([&] {
+        require(layers && refl && trans && tr && tt, "mpss_mc_reference: null argument");
+        require(n >= 1 && n <= 8 && nseg >= 1 && nseg <= (1 << 16), "mpss_mc_reference: bad layer or ring count");
+        std::vector<MpcLayer> ml(n);
+        double mfp_total = 0.;
+        for (int i = 0; i < n; ++i) {
+            require(layers[i].musp > 0.f && layers[i].mua >= 0.f && layers[i].thickness > 0.f,
+                    "mpss_mc_reference: layers need musp > 0, mua >= 0, thickness > 0");
+            ml[i] = MpcLayer{layers[i].mua, layers[i].musp, layers[i].ior, layers[i].thickness};
+            mfp_total += 1. / (double)(layers[i].mua + layers[i].musp);  // Render, mcprofile.cpp:457-463
+        }
+        const double extent = mfp_range * (mfp_total / (double)n);
+        mc_reference_profile(ml.data(), n, extent, nseg, lerp != 0, refl, trans, tr, tt);
     });
 }
 

@@ -62,7 +62,7 @@ class LayeredSkin(C.Structure):
                 ("b_derm", C.c_float), ("layer_thickness_nm", C.c_float * 2), ("layer_ior", C.c_float * 2),
                 ("albedo", C.c_float * NB), ("Kr", C.c_float * NB), ("Kt", C.c_float * NB),
                 ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
-                ("double_ref_sslf", C.c_int)]
+                ("double_ref_sslf", C.c_int), ("use_monte_carlo", C.c_int), ("photons", C.c_uint64)]
 
 
 class Imagemap(C.Structure):
@@ -110,6 +110,8 @@ _sig("mpss_render_tile", C.c_int, [vp, C.c_int, u32, C.c_int, C.c_int, C.c_int, 
 _sig("mpss_render_tiles", C.c_int, [vp, C.c_int, u32, C.c_int, C.POINTER(C.c_int32), C.POINTER(vp), vp])
 _sig("mpss_tile_costs", C.c_int, [vp, C.c_int, C.POINTER(C.c_int32), vp, vp])
 _sig("mpss_host_from_rgb", C.c_int, [f32p, C.c_int, f32p])
+_sig("mpss_mc_reference", C.c_int, [f32p, C.c_int, C.c_float, C.c_int, C.c_int, vp, vp, C.POINTER(C.c_double),
+                                    C.POINTER(C.c_double)])
 _sig("mpss_mc_profile", C.c_int, [vp, f32p, C.c_int, C.c_float, C.c_int, C.c_uint64, C.c_uint64, vp, vp,
                                   C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64), vp])
 _sig("mpss_host_tessellate", C.c_int, [u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32,
@@ -260,6 +262,18 @@ def host_build_profile(mua, musp, thickness, eta, desired_length=512, lerp=True)
     check(_lib.mpss_host_build_profile(*args, desired_length, int(lerp), tab.ctypes.data, C.byref(n),
                                        rcp.ctypes.data, tot.ctypes.data))
     return tab, rcp, tot
+
+
+def mc_reference(layers, mfp_range=16.0, nsegments=1024, lerp=True):
+    """MultipoleReferenceTask (mcprofile.cpp:356-425): the multipole model of `layers`
+    [(mua, musp, ior, thickness), ...] at the MC profile's ring centres; host code."""
+    lay = np.ascontiguousarray(layers, np.float32).reshape(-1, 4)
+    r = np.zeros(nsegments, np.float64)
+    t = np.zeros(nsegments, np.float64)
+    tr, tt = C.c_double(), C.c_double()
+    check(_lib.mpss_mc_reference(lay, len(lay), mfp_range, nsegments, int(lerp), r.ctypes.data, t.ctypes.data,
+                                 C.byref(tr), C.byref(tt)))
+    return dict(reflectance=r, transmittance=t, total_r=tr.value, total_t=tt.value)
 
 
 def host_rho_table(roughness, eta, n=1025, sqrt_samples=256, double_ref_sslf=False):

@@ -123,7 +123,7 @@ class OracleScene:
             alb = mpss.host_from_rgb(m["albedo"]) if "albedo" in m else np.ones(NB, np.float32)
             tab, rcp, rho = tables[mid]
             L.o_scene_add_material(self.h, Kr, Kt, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
-                                   int(skin.double_ref_sslf), rho, len(rho), 0,
+                                   int(skin.double_ref_sslf), rho, len(rho), int(skin.use_monte_carlo),
                                    np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
             for which, key in ((0, "albedo_tex"), (1, "bump_tex")):
                 if m.get(key) is not None:

@@ -1,22 +1,25 @@
 #!/bin/bash
-# One GPU session: tests, bench (with CPU baseline and an image), rocprofv3 kernel trace and
-# PMC passes of the bench. Every GPU step has its own time limit; the first failure ends it.
+# One GPU session: bench (with CPU baseline and an image), rocprofv3 kernel trace and PMC passes
+# of the bench (separate runs, --kernel-trace/--stats only with PMC off). Every GPU step has its own
+# time limit; the first failure ends it. Usage: bash tools/gpu_round.sh TAG
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-mkdir -p gpurun_out gpurun_out/prof_${1:-r01}
+TAG=${1:-r02}
+mkdir -p gpurun_out gpurun_out/prof_$TAG
 export TMPDIR=/tmp
-TAG=${1:-r01}
-step() { echo "== $*"; }
-step pytest
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/pytest_gpu.log
-step bench
-timeout -k 10 400 python bench.py --steps 3 --warmup 1 --out gpurun_out/skin.exr > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -40 gpurun_out/bench.log; exit 1; }
-cat gpurun_out/bench.log
-step rocprof-kernel-trace
+echo "== bench"
+timeout -k 10 400 python bench.py --steps 5 --warmup 1 --out gpurun_out/skin.exr > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -40 gpurun_out/bench_$TAG.log; exit 1; }
+grep metric gpurun_out/bench_$TAG.log
+echo "== rocprof kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG/kt -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG/kt.log 2>&1 || { echo "rocprof kt failed"; tail -30 gpurun_out/prof_$TAG/kt.log; exit 1; }
-step rocprof-pmc-fetch
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_$TAG/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$TAG/pmc_fetch.log 2>&1 || { echo "rocprof pmc failed"; tail -30 gpurun_out/prof_$TAG/pmc_fetch.log; exit 1; }
-step rocprof-pmc-l2
-timeout -k 10 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/prof_$TAG/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$TAG/pmc_l2.log 2>&1 || { echo "rocprof pmc2 failed"; tail -30 gpurun_out/prof_$TAG/pmc_l2.log; exit 1; }
+grep metric gpurun_out/prof_$TAG/kt.log > gpurun_out/prof_$TAG/kt_bench.jsonl || true
+i=0
+while read -r line; do
+  [ -z "$line" ] && continue
+  i=$((i+1))
+  echo "== pmc $i: $line"
+  timeout -s KILL 240 rocprofv3 --pmc $line -d gpurun_out/prof_$TAG/pmc_$i -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/prof_$TAG/pmc_$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 gpurun_out/prof_$TAG/pmc_$i.log; exit 1; }
+done <<< "FETCH_SIZE
+TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
 echo ALL_OK
