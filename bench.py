@@ -308,7 +308,7 @@ def main(a):
         g = [x.cpu().numpy() for x in gath] if gath is not None else [out.cpu().numpy()]
         tl.assemble(img, g, items_by_rank, tiles, T)
         rgb = film.finalize(img[0])
-        (film.write_exr if a.out.endswith(".exr") else film.write_pfm)(a.out, rgb)
+        film.write_image(a.out, rgb)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -110,6 +110,14 @@ int mpss_add_layeredskin(mpss_ctx *ctx, const mpss_layeredskin *m, uint32_t *mat
 int mpss_set_material_tables(mpss_ctx *ctx, const float *rd_table, uint32_t length, const float *rcp,
                              const float *rho_hd, uint32_t n_rho, const float *albedo, int is_monte_carlo,
                              uint32_t *material_id);
+/* The dipolesubsurface integrator's Rd functor, DiffusionReflectance(sigma_a, sigmap_s, eta)
+ * (integrators/diffusionutil.h:38-83, built per hit at dipolesubsurface.cpp:171): a material whose
+ * mpss_mo_batch evaluates the closed-form single dipole per band inside the reference-order gather
+ * (SubsurfaceOctreeNode::Mo, diffusionutil.h:175-210; nothing pruned). sigma_a / sigmap_s: [30].
+ * It is not a surface material: mpss_add_mesh rejects it (the dipole integrator's Li is not part of
+ * this library). */
+int mpss_add_dipole_material(mpss_ctx *ctx, const float *sigma_a, const float *sigmap_s, float eta,
+                             uint32_t *material_id);
 /* Query sizes first with NULL buffers: *length and *n_rho are always written. */
 int mpss_get_material_tables(mpss_ctx *ctx, uint32_t material_id, float *rd_table, uint32_t *length, float *rcp,
                              float *rho_hd, uint32_t *n_rho, float *total_reflectance);
@@ -274,6 +282,10 @@ int mpss_host_skin_layers(const mpss_layeredskin *m, float *mua, float *musp, fl
 int mpss_host_build_profile(const float *mua, const float *musp, const float *thickness, const float *eta,
                             int desired_length, int lerp_on_thin_slab, float *rd_table, uint32_t *length,
                             float *rcp, float *total_reflectance);
+/* DiffusionReflectance::operator() at n squared distances (rd: n x 30) and, if total is not NULL,
+ * TotalReflectance() (diffusionutil.h:69-77, a 1024-step sum in d^2 over (4 mfp)^2). */
+int mpss_host_dipole_rd(const float *sigma_a, const float *sigmap_s, float eta, uint32_t n, const float *d2,
+                        float *rd, float *total);
 /* rho_hd table (n entries, sqrt_samples^2 samples each) and rho_hh. */
 int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, int sqrt_samples, float *hd,
                         float *hh);

@@ -2,7 +2,9 @@
  * Restates SubsurfaceOctreeNode::{Insert, InitHierarchy, Mo} (reference
  * src/integrators/diffusionutil.h:86-234), octreeChildBound (core/octree.h:87-97),
  * the Preprocess octree build loop (integrators/multipolesubsurface.cpp:301-321)
- * and MultipoleReflectance -> sampleProfile (core/multipole.cpp:60-113).
+ * and MultipoleReflectance -> sampleProfile (core/multipole.cpp:60-113); the alternate Rd
+ * functor DiffusionReflectance (diffusionutil.h:38-83), the single dipole that the
+ * dipolesubsurface integrator hands to the same Mo (dipolesubsurface.cpp:171-172).
  * Points are inserted in index order (the reference inserts in mutex-completion
  * order, multipolesubsurface.cpp:230-234; index order is the deterministic choice
  * both this oracle and the product make). */
@@ -165,7 +167,62 @@ typedef struct {
     const float *rcp;
     float max_error;
     long nodes, points;
+    const o_diffusion *dip; /* non-NULL: DiffusionReflectance instead of the profile table */
 } mo_ctx;
+
+/* ---- DiffusionReflectance (diffusionutil.h:38-83) ---- */
+/* Fdr, core/reflection.h:64-71 */
+static float fdr_eta(float eta) {
+    if (eta >= 1) return -1.4399f / (eta * eta) + 0.7099f / eta + 0.6681f + 0.0636f * eta;
+    return -0.4399f + .7099f / eta - .3319f / (eta * eta) + .0636f / (eta * eta * eta);
+}
+
+/* pbrt.h:196 redefines M_PI as a float literal */
+#define O_PI_F 3.14159265358979323846f
+
+void o_diffusion_init(const float sigma_a[O_NB], const float sigmap_s[O_NB], float eta, o_diffusion *d) {
+    /* constructor, diffusionutil.h:40-48; spectrum ops are per-band float ops (spectrum.h:125-240) */
+    d->A = (1.f + fdr_eta(eta)) / (1.f - fdr_eta(eta));
+    for (int c = 0; c < O_NB; ++c) {
+        d->sigmap_t[c] = sigma_a[c] + sigmap_s[c];
+        /* 3.f * sigma_a is s * 3.f (operator*(float, Spectrum), spectrum.h:180-184), then * sigmap_t */
+        d->sigma_tr[c] = sqrtf((sigma_a[c] * 3.f) * d->sigmap_t[c]);
+        d->alphap[c] = sigmap_s[c] / d->sigmap_t[c];
+        d->zpos[c] = 1.f / d->sigmap_t[c];
+        d->zneg[c] = (-d->zpos[c]) * (1.f + (4.f / 3.f) * d->A);
+    }
+}
+
+/* operator()(float d2), diffusionutil.h:49-58: Rd = (alphap / (4 M_PI)) * (pos - neg), Clamp() */
+void o_diffusion_eval(const o_diffusion *d, float d2, float out[O_NB]) {
+    const float four_pi = 4.f * O_PI_F;
+    for (int c = 0; c < O_NB; ++c) {
+        float dpos = sqrtf(d2 + d->zpos[c] * d->zpos[c]);
+        float dneg = sqrtf(d2 + d->zneg[c] * d->zneg[c]);
+        float e_pos = (float)exp((double)((-d->sigma_tr[c]) * dpos));
+        float e_neg = (float)exp((double)((-d->sigma_tr[c]) * dneg));
+        float pos = ((d->zpos[c] * (dpos * d->sigma_tr[c] + 1.f)) * e_pos) / ((dpos * dpos) * dpos);
+        float neg = ((d->zneg[c] * (dneg * d->sigma_tr[c] + 1.f)) * e_neg) / ((dneg * dneg) * dneg);
+        float rd = (d->alphap[c] / four_pi) * (pos - neg);
+        /* Spectrum::Clamp(0, INFINITY) -> ::Clamp (pbrt.h) */
+        out[c] = rd < 0.f ? 0.f : (rd > INFINITY ? INFINITY : rd);
+    }
+}
+
+/* TotalReflectance, diffusionutil.h:69-77 */
+void o_diffusion_total(const o_diffusion *d, float out[O_NB]) {
+    for (int c = 0; c < O_NB; ++c) {
+        float mfp = 1.f / d->sigmap_t[c];
+        float step = ((4.f * mfp) * (4.f * mfp)) / 1024.f;
+        float integral = 0.f;
+        for (int i = 0; i < 1024; ++i) {
+            float v[O_NB];
+            o_diffusion_eval(d, step * (float)i, v); /* the Spectrum-d2 overload, band c */
+            integral += v[c];
+        }
+        out[c] = (integral * step) * O_PI_F;
+    }
+}
 
 static float dist2(const float *a, const float *b) {
     float x = a[0] - b[0], y = a[1] - b[1], z = a[2] - b[2];
@@ -173,6 +230,10 @@ static float dist2(const float *a, const float *b) {
 }
 
 static void rd_eval(const mo_ctx *m, float d2, float out[O_NB]) {
+    if (m->dip) {
+        o_diffusion_eval(m->dip, d2, out);
+        return;
+    }
     for (int c = 0; c < O_NB; ++c) out[c] = o_sample_profile(m->tab + (size_t)c * m->len, m->len, m->rcp[c], d2);
 }
 
@@ -226,6 +287,7 @@ typedef struct {
     int32_t *nn, *np;
     int next;
     pthread_mutex_t mu;
+    const o_diffusion *dip;
 } mo_job;
 
 static void *mo_worker(void *arg) {
@@ -238,7 +300,7 @@ static void *mo_worker(void *arg) {
         if (start >= j->q) break;
         int end = start + 256 < j->q ? start + 256 : j->q;
         for (int i = start; i < end; ++i) {
-            mo_ctx m = {j->t, j->tab, j->len, j->rcp, j->max_error, 0, 0};
+            mo_ctx m = {j->t, j->tab, j->len, j->rcp, j->max_error, 0, 0, j->dip};
             mo_rec(&m, j->t->root, j->t->bmin, j->t->bmax, j->pts + 3 * (size_t)i, j->mo + (size_t)i * O_NB);
             if (j->nn) j->nn[i] = (int32_t)m.nodes;
             if (j->np) j->np[i] = (int32_t)m.points;
@@ -247,19 +309,33 @@ static void *mo_worker(void *arg) {
     return NULL;
 }
 
+static void mo_run(mo_job *jp, int nthreads);
+
+void o_mo_batch_diffusion(const o_octree *t, int q, const float *pts, const o_diffusion *d, float max_error,
+                          float *mo, int32_t *nn, int32_t *np, int nthreads) {
+    mo_job j;
+    memset(&j, 0, sizeof(j));
+    j.t = t; j.q = q; j.pts = pts; j.max_error = max_error; j.mo = mo; j.nn = nn; j.np = np; j.dip = d;
+    mo_run(&j, nthreads);
+}
+
 void o_mo_batch(const o_octree *t, int q, const float *pts, const float *tab, int len, const float rcp[O_NB],
                 float max_error, float *mo, int32_t *nn, int32_t *np, int nthreads) {
     mo_job j;
     memset(&j, 0, sizeof(j));
     j.t = t; j.q = q; j.pts = pts; j.tab = tab; j.rcp = rcp; j.len = len; j.max_error = max_error;
     j.mo = mo; j.nn = nn; j.np = np;
-    pthread_mutex_init(&j.mu, NULL);
+    mo_run(&j, nthreads);
+}
+
+static void mo_run(mo_job *jp, int nthreads) {
+    pthread_mutex_init(&jp->mu, NULL);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
-    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, mo_worker, &j);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, mo_worker, jp);
     for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
-    pthread_mutex_destroy(&j.mu);
+    pthread_mutex_destroy(&jp->mu);
 }
 
 /* Pre-order flattening (children in index order 0..7, leaves keep ips[] order). */

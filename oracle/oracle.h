@@ -14,7 +14,9 @@
  *   - kissfft vs brute-force DFT   (libkissfft/test/test_vs_dft.c)
  *   - MPC profile integral vs totalReflectance (src/multipole/test/test.cpp:74-75)
  *   - Mo() at maxError -> 0 equals the brute-force point sum (diffusionutil.h:175-210)
- *   - analytic single dipole (diffusionutil.h:38-83) as a closed-form Rd
+ *   - the analytic single dipole DiffusionReflectance (diffusionutil.h:38-83, o_diffusion_*
+ *     below) as a closed-form Rd: its TotalReflectance against Jensen's closed-form total
+ *     diffuse reflectance, and Mo() with it against the brute-force point sum
  * Every function cites the reference file:line it follows.
  *
  * Build: make -C oracle  (gcc -O2 -ffp-contract=off, no -ffast-math)
@@ -91,6 +93,17 @@ int o_octree_num_nodes(const o_octree *t);
 void o_mo_batch(const o_octree *t, int q, const float *pts /*q*3*/, const float *rd_table, int len,
                 const float rcp[O_NB], float max_error, float *mo /*q*O_NB*/, int32_t *n_nodes,
                 int32_t *n_points, int nthreads);
+/* DiffusionReflectance (diffusionutil.h:38-83): the single-dipole Rd functor */
+typedef struct {
+    float zpos[O_NB], zneg[O_NB], sigmap_t[O_NB], sigma_tr[O_NB], alphap[O_NB];
+    float A;
+} o_diffusion;
+void o_diffusion_init(const float sigma_a[O_NB], const float sigmap_s[O_NB], float eta, o_diffusion *d);
+void o_diffusion_eval(const o_diffusion *d, float d2, float out[O_NB]);
+void o_diffusion_total(const o_diffusion *d, float out[O_NB]);
+/* Mo with DiffusionReflectance as the Rd functor (dipolesubsurface.cpp:171-172) */
+void o_mo_batch_diffusion(const o_octree *t, int q, const float *pts, const o_diffusion *d, float max_error,
+                          float *mo, int32_t *nn, int32_t *np, int nthreads);
 /* Flatten for inspection: pre-order nodes (same order as the product's layout contract) */
 int o_octree_export(const o_octree *t, float *node_p /*N*3*/, float *node_area, float *node_et /*N*O_NB*/,
                     float *bmin /*N*3*/, float *bmax /*N*3*/, int32_t *depth, int32_t *skip,

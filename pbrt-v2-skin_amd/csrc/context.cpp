@@ -63,7 +63,8 @@ void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) {
 
 void Context::ensure_layouts() {
     if (!have_octree_) return;
-    for (const auto &m : materials_) dev_octree_.ensure_layout(m->dev_profile.groups);
+    for (const auto &m : materials_)
+        if (!m->dipole) dev_octree_.ensure_layout(m->dev_profile.groups);
 }
 
 // SubsurfaceOctreeNode::Mo for a batch of points (mpss_mo_batch). The octree, profile and band
@@ -82,10 +83,16 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         if (mid >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(mid));
         m = materials_[mid].get();
         mode = cfg_.exact_mo;
-        if (mode == 0) {
+        if (m->dipole) {
+            mode = -1;  // closed-form functor: the reference-order gather (dipole.h)
+        } else if (mode == 0) {
             layout = &dev_octree_.ensure_layout(m->dev_profile.groups);
             ws = acquire_ws();
         }
+    }
+    if (mode == -1) {
+        launch_mo_dipole(dev_octree_, m->dev_dipole.ptr, max_error_, q, p_dev, out_dev, NB, counters_dev, stream);
+        return;
     }
     if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
     try {
@@ -171,6 +178,32 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
     materials_.push_back(std::move(mat));
     scene_dirty_ = true;
     ensure_layouts();
+    return (uint32_t)materials_.size() - 1;
+}
+
+uint32_t Context::add_dipole_material(const float *sigma_a, const float *sigmap_s, float eta) {
+    activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (materials_.size() >= kMaxMaterials) throw Error(MPSS_ERR_INVALID, "at most 256 materials per context");
+    auto mat = std::make_unique<Material>();
+    mat->dipole = true;
+    dipole_init(sigma_a, sigmap_s, eta, mat->dip);
+    float packed[4 * NB];
+    for (int c = 0; c < NB; ++c) {
+        packed[c] = mat->dip.zpos[c];
+        packed[NB + c] = mat->dip.zneg[c];
+        packed[2 * NB + c] = mat->dip.sigma_tr[c];
+        packed[3 * NB + c] = mat->dip.k[c];
+        mat->albedo[c] = 1.f;
+        mat->Kr[c] = 1.f;
+        mat->Kt[c] = 0.f;
+    }
+    mat->ior = eta;
+    mat->dev_dipole.upload(packed, 4 * NB);
+    mat->rho.hd.assign(2, 0.f);
+    mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
+    materials_.push_back(std::move(mat));
+    scene_dirty_ = true;
     return (uint32_t)materials_.size() - 1;
 }
 

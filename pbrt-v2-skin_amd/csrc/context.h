@@ -7,6 +7,7 @@
 
 #include "../../include/mpss.h"
 #include "common.h"
+#include "dipole.h"
 #include "material.h"
 #include "mo_kernel.h"
 #include "octree.h"
@@ -29,6 +30,10 @@ struct Material {
     DeviceProfile dev_profile;
     DevBuf<float> dev_rho;  // [n_rho]
     int albedo_tex = -1, bump_tex = -1;  // ImageTexture ids ("texture albedo" / "texture bumpmap")
+    // a DiffusionReflectance functor instead of a profile (mpss_add_dipole_material): Mo only
+    bool dipole = false;
+    DipoleRd dip{};
+    DevBuf<float> dev_dipole;  // [4][NB] zpos, zneg, sigma_tr, k
 };
 
 // ImageTexture<RGBSpectrum, Spectrum> / ImageTexture<float, float> (textures/imagemap.{h,cpp})
@@ -75,6 +80,8 @@ public:
     uint32_t add_layeredskin(const mpss_layeredskin &m);
     uint32_t set_material_tables(const float *rd, uint32_t len, const float *rcp, const float *rho, uint32_t n_rho,
                                  const float *albedo, bool is_mc);
+    // the single-dipole Rd of the dipolesubsurface integrator (dipole.h); usable with mo_batch
+    uint32_t add_dipole_material(const float *sigma_a, const float *sigmap_s, float eta);
     const Material &material(uint32_t id) const;
     void set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area);
     const DeviceOctree &octree() const;

@@ -52,6 +52,11 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
                       const float *queries, float *out, int out_stride, int32_t *counters, int *work,
                       hipStream_t stream, int mode);
 
+// Mo with the closed-form single dipole (dipole.h) as Rd, in the reference summation order.
+// dipole_dev: [4][NB] device floats zpos, zneg, sigma_tr, k. Nothing is pruned.
+void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream);
+
 // Traversal statistics of the sharded gather (count variant): per group g, counts[kStatStride*g + k]
 // for k = 0 node visits, 1 point visits (summed over queries), 2 wave node iterations, 3 wave
 // point iterations (summed over waves; 64 x these / the visits = 1 / lane efficiency), 4 table

@@ -23,6 +23,7 @@
 // whole subtree adds only +0 terms in the reference and is skipped here without changing a
 // bit of the result. The COUNT variant reports both the reference traversal's visits and the
 // pruned traversal's visits (SURVEY.md 8d counters).
+#include "dipole.h"
 #include "mo_kernel.h"
 #include "mo_packet.h"
 
@@ -46,6 +47,7 @@ struct MoArgs {
     int L, n_nodes, nq, out_stride;
     float max_error, prune_f;           // prune when d2box * rcp_min >= prune_f
     float rcp_min;
+    const float *__restrict__ dipole;   // DIP: [4][NB] zpos, zneg, sigma_tr, k (dipole.h)
 };
 
 __device__ __forceinline__ float rd_lerp(const float *__restrict__ tb, float f) {
@@ -62,7 +64,9 @@ __device__ __forceinline__ float box_d2(float px, float py, float pz, const Node
     return bx * bx + by * by + bz * bz;
 }
 
-template <int MAXD, bool COUNT>
+// DIP: the Rd functor is the closed-form single dipole (DiffusionReflectance, dipole.h) instead
+// of the tabulated profile; it never returns an exact 0 past a range, so nothing is pruned.
+template <int MAXD, bool COUNT, bool DIP>
 __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
     __shared__ float S[4][MAXD + 1][64];
     const int lane = threadIdx.x & 63;
@@ -78,9 +82,17 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
         py = a.queries[3 * (size_t)q + 1];
         pz = a.queries[3 * (size_t)q + 2];
     }
-    const float rcp = c < NB ? a.rcp[c] : INFINITY;
+    const float rcp = (!DIP && c < NB) ? a.rcp[c] : INFINITY;
     const float lm1 = (float)(a.L - 1);
     const float *__restrict__ tb = a.table + (size_t)(c < NB ? c : 0) * a.L;
+    float dzp = 0.f, dzn = 0.f, dtr = 0.f, dk = 0.f;
+    if (DIP) {
+        const int cc = c < NB ? c : 0;
+        dzp = a.dipole[cc];
+        dzn = a.dipole[NB + cc];
+        dtr = a.dipole[2 * NB + cc];
+        dk = a.dipole[3 * NB + cc];
+    }
 
     int node = active ? 0 : a.n_nodes;
     int dlast = 0;
@@ -114,8 +126,12 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
             const bool inside = px >= h.bminx && px <= h.bmaxx && py >= h.bminy && py <= h.bmaxy &&
                                 pz >= h.bminz && pz <= h.bmaxz;
             if (dw < a.max_error && !inside) {
-                const float f = d2 * rcp;
-                if (f < lm1) St[d][lane] += rd_lerp(tb, f) * a.node_et[(size_t)node * ROW + c];
+                if (DIP) {
+                    St[d][lane] += dipole_band(dzp, dzn, dtr, dk, d2) * a.node_et[(size_t)node * ROW + c];
+                } else {
+                    const float f = d2 * rcp;
+                    if (f < lm1) St[d][lane] += rd_lerp(tb, f) * a.node_et[(size_t)node * ROW + c];
+                }
             } else if (h.leaf_first >= 0) {
                 float acc = 0.f;
                 for (int i = 0; i < h.leaf_count; ++i) {
@@ -127,6 +143,11 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
                         if (node >= pruned_until) ++k_pts;
                     }
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
+                    if (DIP) {
+                        acc += dipole_band(dzp, dzn, dtr, dk, ex * ex + ey * ey + ez * ez) *
+                               a.pt_e[(size_t)k * ROW + c] * ph.w;
+                        continue;
+                    }
                     const float f = (ex * ex + ey * ey + ez * ez) * rcp;
                     if (f < lm1) acc += rd_lerp(tb, f) * a.pt_e[(size_t)k * ROW + c] * ph.w;
                 }
@@ -405,15 +426,28 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     return bt;
 }
 
-template <int MAXD>
+template <int MAXD, bool DIP>
 void launch_t(const MoArgs &a, bool count, hipStream_t s) {
     const int waves = (a.nq + 1) / 2;
     const int blocks = (waves + 3) / 4;
     if (blocks == 0) return;
     if (count)
-        hipLaunchKernelGGL((mo_gather_kernel<MAXD, true>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, true, DIP>), dim3(blocks), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((mo_gather_kernel<MAXD, false>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, false, DIP>), dim3(blocks), dim3(256), 0, s, a);
+}
+
+template <bool DIP>
+void launch_exact(const MoArgs &a, int max_depth, bool count, hipStream_t s) {
+    if (max_depth < 16)
+        launch_t<16, DIP>(a, count, s);
+    else if (max_depth < 32)
+        launch_t<32, DIP>(a, count, s);
+    else if (max_depth < 64)
+        launch_t<64, DIP>(a, count, s);
+    else
+        throw Error(-2, "octree deeper than 63 levels is not supported by the gather kernel");
+    MPSS_HIP(hipGetLastError());
 }
 
 }  // namespace
@@ -556,15 +590,31 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
         MPSS_HIP(hipGetLastError());
         return;
     }
-    if (t.max_depth < 16)
-        launch_t<16>(a, count, stream);
-    else if (t.max_depth < 32)
-        launch_t<32>(a, count, stream);
-    else if (t.max_depth < 64)
-        launch_t<64>(a, count, stream);
-    else
-        throw Error(-2, "octree deeper than 63 levels is not supported by the gather kernel");
-    MPSS_HIP(hipGetLastError());
+    a.dipole = nullptr;
+    launch_exact<false>(a, t.max_depth, count, stream);
+}
+
+void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
+                      float *out, int out_stride, int32_t *counters, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (t.n_nodes <= 0) throw Error(-1, "launch_mo_dipole: octree is empty");
+    MoArgs a{};
+    a.nodes = t.nodes.ptr;
+    a.node_et = t.node_et.ptr;
+    a.pt_hdr = t.pt_hdr.ptr;
+    a.pt_e = t.pt_e.ptr;
+    a.queries = queries;
+    a.out = out;
+    a.counters = counters;
+    a.L = 2;
+    a.n_nodes = t.n_nodes;
+    a.nq = nq;
+    a.out_stride = out_stride;
+    a.max_error = max_error;
+    a.rcp_min = 0.f;
+    a.prune_f = INFINITY;
+    a.dipole = dipole_dev;
+    launch_exact<true>(a, t.max_depth, counters != nullptr, stream);
 }
 
 }  // namespace mpss

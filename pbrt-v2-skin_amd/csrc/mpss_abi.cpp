@@ -138,6 +138,14 @@ int mpss_set_material_tables(mpss_ctx *c, const float *rd, uint32_t len, const f
     });
 }
 
+int mpss_add_dipole_material(mpss_ctx *c, const float *sigma_a, const float *sigmap_s, float eta, uint32_t *id) {
+    return guarded([&] {
+        require(c && sigma_a && sigmap_s && id, "mpss_add_dipole_material: null argument");
+        require(eta > 0.f, "mpss_add_dipole_material: eta must be positive");
+        *id = reinterpret_cast<Context *>(c)->add_dipole_material(sigma_a, sigmap_s, eta);
+    });
+}
+
 int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len, float *rcp, float *rho,
                              uint32_t *n_rho, float *total) {
     return guarded([&] {
@@ -460,6 +468,17 @@ int mpss_host_build_profile(const float *mua, const float *musp, const float *th
         if (rd) memcpy(rd, pt.table.data(), sizeof(float) * pt.table.size());
         if (rcp) memcpy(rcp, pt.rcp, sizeof(pt.rcp));
         if (total) memcpy(total, pt.total_reflectance, sizeof(pt.total_reflectance));
+    });
+}
+
+int mpss_host_dipole_rd(const float *sigma_a, const float *sigmap_s, float eta, uint32_t n, const float *d2, float *rd,
+                        float *total) {
+    return guarded([&] {
+        require(sigma_a && sigmap_s && (n == 0 || (d2 && rd)), "mpss_host_dipole_rd: null argument");
+        DipoleRd d;
+        dipole_init(sigma_a, sigmap_s, eta, d);
+        for (uint32_t i = 0; i < n; ++i) dipole_eval(d, d2[i], rd + (size_t)i * NB);
+        if (total) dipole_total(d, total);
     });
 }
 

@@ -33,6 +33,8 @@ void Context::add_mesh(uint32_t nv, const float *P, const float *N, const float 
                        const int32_t *idx, const float *o2w, const float *w2o, bool reverse, uint32_t material) {
     std::lock_guard<std::mutex> g(mu_);
     if (material >= materials_.size()) throw Error(MPSS_ERR_INVALID, "add_mesh: unknown material id");
+    if (materials_[material]->dipole)
+        throw Error(MPSS_ERR_INVALID, "add_mesh: a dipole material is an Rd functor for mpss_mo_batch, not a surface");
     Mesh m;
     m.P.assign(P, P + 3 * (size_t)nv);
     if (N) m.N.assign(N, N + 3 * (size_t)nv);
@@ -492,7 +494,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     std::vector<SssMat> sss;
     if (have_octree_)
         for (size_t i = 0; i < materials_.size(); ++i)
-            sss.push_back(SssMat{(int)i, materials_[i].get(), &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
+            if (!materials_[i]->dipole) sss.push_back(SssMat{(int)i, materials_[i].get(), &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
     sc.have_octree = sss.empty() ? 0 : 1;
     const bool timing = cfg_.kernel_timing != 0, counting = cfg_.count_traversal != 0;
@@ -777,6 +779,10 @@ void Context::reset_render_stats() {
     if (d_counts_.ptr) MPSS_HIP(hipMemset(d_counts_.ptr, 0, kStatStride * kGroups * sizeof(unsigned long long)));
 }
 
-int Context::first_bssrdf_material() const { return materials_.empty() ? -1 : 0; }
+int Context::first_bssrdf_material() const {
+    for (size_t i = 0; i < materials_.size(); ++i)
+        if (!materials_[i]->dipole) return (int)i;
+    return -1;
+}
 
 }  // namespace mpss

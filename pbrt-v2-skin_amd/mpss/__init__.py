@@ -88,6 +88,8 @@ _sig("mpss_destroy", None, [vp])
 _sig("mpss_layeredskin_defaults", None, [C.POINTER(LayeredSkin)])
 _sig("mpss_add_layeredskin", C.c_int, [vp, C.POINTER(LayeredSkin), u32p])
 _sig("mpss_set_material_tables", C.c_int, [vp, f32p, u32, f32p, f32p, u32, vp, C.c_int, u32p])
+_sig("mpss_add_dipole_material", C.c_int, [vp, f32p, f32p, C.c_float, u32p])
+_sig("mpss_host_dipole_rd", C.c_int, [f32p, f32p, C.c_float, u32, vp, vp, vp])
 _sig("mpss_get_material_tables", C.c_int, [vp, u32, vp, u32p, vp, vp, u32p, vp])
 _sig("mpss_set_irradiance_points", C.c_int, [vp, u32, f32p, f32p, f32p, f32p])
 _sig("mpss_octree_info", C.c_int, [vp, u32p, u32p, u32p])
@@ -276,6 +278,17 @@ def mc_reference(layers, mfp_range=16.0, nsegments=1024, lerp=True):
     return dict(reflectance=r, transmittance=t, total_r=tr.value, total_t=tt.value)
 
 
+def host_dipole_rd(sigma_a, sigmap_s, eta, d2):
+    """DiffusionReflectance(sigma_a, sigmap_s, eta)(d2) per squared distance (n x 30) and its
+    TotalReflectance() (diffusionutil.h:38-83)."""
+    d2 = np.ascontiguousarray(np.atleast_1d(d2), np.float32)
+    rd = np.zeros((len(d2), NB), np.float32)
+    tot = np.zeros(NB, np.float32)
+    check(_lib.mpss_host_dipole_rd(np.ascontiguousarray(sigma_a, np.float32), np.ascontiguousarray(sigmap_s, np.float32),
+                                   eta, len(d2), d2.ctypes.data, rd.ctypes.data, tot.ctypes.data))
+    return rd, tot
+
+
 def host_rho_table(roughness, eta, n=1025, sqrt_samples=256, double_ref_sslf=False):
     hd = np.zeros(n, np.float32)
     hh = C.c_float()
@@ -327,6 +340,13 @@ class Context:
         check(_lib.mpss_set_material_tables(self.h, table, table.shape[1], np.ascontiguousarray(rcp, np.float32),
                                             np.ascontiguousarray(rho_hd, np.float32), len(rho_hd),
                                             None if al is None else al.ctypes.data, int(is_mc), C.byref(mid)))
+        return mid.value
+
+    def add_dipole_material(self, sigma_a, sigmap_s, eta):
+        """A DiffusionReflectance Rd functor for mo_batch (the dipolesubsurface integrator's Rd)."""
+        mid = C.c_uint32()
+        check(_lib.mpss_add_dipole_material(self.h, np.ascontiguousarray(sigma_a, np.float32),
+                                            np.ascontiguousarray(sigmap_s, np.float32), eta, C.byref(mid)))
         return mid.value
 
     def material_tables(self, mid):

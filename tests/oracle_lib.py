@@ -75,6 +75,11 @@ def lib():
     L.o_octree_num_nodes.argtypes = [C.c_void_p]
     L.o_mo_batch.argtypes = [C.c_void_p, C.c_int, f32p, f32p, C.c_int, f32p, C.c_float, f32p,
                              C.c_void_p, C.c_void_p, C.c_int]
+    L.o_diffusion_init.argtypes = [f32p, f32p, C.c_float, C.c_void_p]
+    L.o_diffusion_eval.argtypes = [C.c_void_p, C.c_float, f32p]
+    L.o_diffusion_total.argtypes = [C.c_void_p, f32p]
+    L.o_mo_batch_diffusion.argtypes = [C.c_void_p, C.c_int, f32p, C.c_void_p, C.c_float, f32p, C.c_void_p,
+                                       C.c_void_p, C.c_int]
     L.o_octree_export.restype = C.c_int
     L.o_octree_export.argtypes = [C.c_void_p] + [C.c_void_p] * 10
     L.o_octree_bounds.argtypes = [C.c_void_p, f32p, f32p]
@@ -145,6 +150,30 @@ def rho_table(roughness, eta, n_entries=1025, sqrt_samples=256):
     return hd, hh.value
 
 
+class Diffusion:
+    """DiffusionReflectance (diffusionutil.h:38-83): the single-dipole Rd functor."""
+
+    def __init__(self, sigma_a, sigmap_s, eta):
+        # o_diffusion: 5 x 30 floats + A
+        self.buf = C.create_string_buffer(4 * (5 * NB + 1))
+        lib().o_diffusion_init(np.ascontiguousarray(sigma_a, np.float32), np.ascontiguousarray(sigmap_s, np.float32),
+                               eta, self.buf)
+
+    def __call__(self, d2):
+        d2 = np.atleast_1d(np.asarray(d2, np.float32))
+        out = np.zeros((len(d2), NB), np.float32)
+        row = np.zeros(NB, np.float32)
+        for i, v in enumerate(d2):
+            lib().o_diffusion_eval(self.buf, float(v), row)
+            out[i] = row
+        return out
+
+    def total(self):
+        out = np.zeros(NB, np.float32)
+        lib().o_diffusion_total(self.buf, out)
+        return out
+
+
 class Octree:
     def __init__(self, p, n, E, area):
         self.p = np.ascontiguousarray(p, np.float32)
@@ -175,6 +204,16 @@ class Octree:
         lib().o_mo_batch(self.handle, len(q), q, table, table.shape[1], np.ascontiguousarray(rcp, np.float32),
                          max_error, out, nn.ctypes.data if counters else None,
                          npt.ctypes.data if counters else None, nthreads())
+        return (out, nn, npt) if counters else out
+
+    def mo_diffusion(self, q, dip, max_error, counters=False):
+        q = np.ascontiguousarray(q, np.float32)
+        out = np.zeros((len(q), NB), np.float32)
+        nn = np.zeros(len(q), np.int32) if counters else None
+        npt = np.zeros(len(q), np.int32) if counters else None
+        lib().o_mo_batch_diffusion(self.handle, len(q), q, dip.buf, max_error, out,
+                                   nn.ctypes.data if counters else None, npt.ctypes.data if counters else None,
+                                   nthreads())
         return (out, nn, npt) if counters else out
 
     def export(self):

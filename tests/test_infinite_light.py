@@ -317,3 +317,17 @@ def test_oracle_irradiance_under_env_map(mpss, oracle):
             acc += ft * le * mu * np.sin(th) * (np.pi / 2 / nt) * (2 * np.pi / nphi * 4)
     em.close()
     np.testing.assert_allclose(E, acc, rtol=0.03)
+
+
+def test_reads_reference_envmap(mpss):
+    """The reference's own environment map (scenes/textures/grace_latlong.exr, an OpenEXR file
+    written by OpenEXR, ZIP-compressed, copied to tests/golden/): ReadImageEXR's HALF slices
+    (imageio.cpp:120-150) decoded by this package, rows top to bottom."""
+    import hashlib
+    from mpss import imageio
+    tex = imageio.read_image(os.path.join(ROOT, "tests", "golden", "grace_latlong.exr"))
+    assert tex.shape == (512, 1024, 3) and tex.dtype == np.float32
+    assert np.all(np.isfinite(tex)) and tex.min() >= 0
+    assert np.array_equal(tex.astype(np.float16).astype(np.float32), tex)  # HALF values
+    assert float(tex.max()) == 18.375
+    assert hashlib.sha256(tex.tobytes()).hexdigest()[:16] == "27123b8a7e761b7d"

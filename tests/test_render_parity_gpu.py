@@ -147,7 +147,8 @@ def _sky_light(deg, axis, L=(0.3, 0.35, 0.45), scale=(2, 2, 2), ns=4):
 
 
 @pytest.mark.parametrize("scene,lights", [("tissue_sky.pbrt", None), ("skin.pbrt", "sky+area"),
-                                          ("skin.pbrt", "sky"), ("tissue.pbrt", "map+area"), ("skin.pbrt", "map")])
+                                          ("skin.pbrt", "sky"), ("tissue.pbrt", "map+area"), ("skin.pbrt", "map"),
+                                          ("skin.pbrt", "grace")])
 def test_image_parity_infinite_light(mpss, oracle, scene, lights):
     """LightSource "infinite" (lights/infinite.cpp), constant or with a radiance map: Sample_L /
     Pdf (Distribution2D) for irradiance and both MIS halves of EstimateDirect, Le (MIPMap
@@ -173,6 +174,11 @@ def test_image_parity_infinite_light(mpss, oracle, scene, lights):
         sky = _sky_light(-60, [0, 1, 0], L=(1, 1, 1), ns=4)
         sky["texels"] = envmap_texels(64, 32, seed=4)
         sc.lights = [sky]
+    elif lights == "grace":  # the reference's own map (scenes/textures/grace_latlong.exr, 1024x512 ZIP)
+        from mpss import imageio
+        sky = _sky_light(-90, [1, 0, 0], L=(1, 1, 1), ns=4)
+        sky["texels"] = imageio.read_exr(os.path.join(ROOT, "tests", "golden", "grace_latlong.exr"))
+        sc.lights = [sc.lights[0], sky]
     ctx = pbrtscene.build_context(sc)
     ctx.preprocess(seed=6)
     o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
