@@ -67,8 +67,8 @@ typedef struct {
                                   terms with one running sum per band and agree bit for bit */
     int kernel_timing;         /* 1: time every render kernel with HIP events (mpss_get_render_stats) */
     int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
-    int profile_on_host;       /* 1: build LayeredSkin profiles on the host CPU (threads); 0 (default):
-                                  on the GPU (profile_gpu.hip) */
+    int profile_on_host;       /* 1: build LayeredSkin profiles and rho_hd tables on the host CPU
+                                  (threads); 0 (default): on the GPU (profile_gpu.hip, rho_gpu.hip) */
     int64_t max_batch_samples; /* camera samples per render batch; the workspace is sized for the
                                   worst case (every sample a hit): ~280 B/sample, 4.7 GB at the
                                   default 1 << 24 */

@@ -69,6 +69,14 @@ static void stratified2d(float *s, int nx, int ny, mt_rng *r) {
         }
 }
 
+/* Transcendentals: evaluated in double and rounded once to float, the convention the product
+ * shares with this oracle on host and device (pbrt_math.h); the reference calls float libm. */
+static float fe(float x) { return (float)exp((double)x); }
+static float fl(float x) { return (float)log((double)x); }
+static float fat(float x) { return (float)atan((double)x); }
+static float fc(float x) { return (float)cos((double)x); }
+static float fs(float x) { return (float)sin((double)x); }
+
 typedef struct { float x, y, z; } v3;
 static float dot3(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
@@ -80,7 +88,7 @@ static float beck_d(const mf *m, v3 wh) { /* reflection.h:514-521 */
     float d = c2 * c2 * O_PIF;
     if (d == 0.f) return 0.f;
     float e = (c2 - 1) * m->rcp_rms2 / c2;
-    return m->rcp_rms2 * expf(e) / d;
+    return m->rcp_rms2 * fe(e) / d;
 }
 
 static float fresnel_diel(float cosi, float eta_i, float eta_t) { /* reflection.cpp:132-153 */
@@ -121,10 +129,10 @@ static float mf_f(const mf *m, v3 wo, v3 wi) { /* reflection.cpp:228-240 with R 
 
 /* Beckmann::Sample_f (reflection.cpp:548-570) + Microfacet::Sample_f (:391-397) */
 static float mf_sample_f(const mf *m, v3 wo, v3 *wi, float u1, float u2, float *pdf) {
-    float theta = atanf(sqrtf(-m->rms2 * logf(1.f - u1)));
-    float ct = cosf(theta), st = sinf(theta);
+    float theta = fat(sqrtf(-m->rms2 * fl(1.f - u1)));
+    float ct = fc(theta), st = fs(theta);
     float phi = u2 * 2.f * O_PIF;
-    v3 wh = {st * cosf(phi), st * sinf(phi), ct};
+    v3 wh = {st * fc(phi), st * fs(phi), ct};
     if (!(wo.z * wh.z > 0.f)) { wh.x = -wh.x; wh.y = -wh.y; wh.z = -wh.z; }
     float d = dot3(wo, wh);
     wi->x = -wo.x + 2.f * d * wh.x;
@@ -152,7 +160,7 @@ static float rho_entry(const rho_job *j, int id) { /* RhoTask::Run, multipole.cp
     stratified2d(s, j->sqrt_samples, j->sqrt_samples, &r);
     float ct = (float)id / (float)(j->n_entries - 1);
     if (ct == 0.f) ct = 0.01f / (float)(j->n_entries - 1);
-    v3 wo = {sqrtf(1 - ct * ct) * cosf(0.f), sqrtf(1 - ct * ct) * sinf(0.f), ct};
+    v3 wo = {sqrtf(1 - ct * ct) * fc(0.f), sqrtf(1 - ct * ct) * fs(0.f), ct};
     float sum = 0.f, c = 0.f; /* KahanSum<Spectrum>, one channel */
     for (int i = 0; i < n; ++i) {
         v3 wi;
@@ -195,7 +203,7 @@ static float rho_hh(const mf *m, int sq) {
         float z = s1[2 * i];
         float rr = sqrtf(fmaxf(0.f, 1.f - z * z));
         float phi = 2 * O_PIF * s1[2 * i + 1];
-        v3 wo = {rr * cosf(phi), rr * sinf(phi), z}, wi;
+        v3 wo = {rr * fc(phi), rr * fs(phi), z}, wi;
         float pdf_o = O_INV_TWOPI, pdf_i = 0.f;
         float f = mf_sample_f(m, wo, &wi, s2[2 * i], s2[2 * i + 1], &pdf_i);
         if (pdf_i > 0.) {

@@ -137,7 +137,10 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
         build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
     else
         build_profile_gpu(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
-    build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
+    if (cfg_.profile_on_host)
+        build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
+    else
+        build_rho_table_gpu(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
     memcpy(mat->albedo, m.albedo, sizeof(mat->albedo));
     memcpy(mat->Kr, m.Kr, sizeof(mat->Kr));
     memcpy(mat->Kt, m.Kt, sizeof(mat->Kt));

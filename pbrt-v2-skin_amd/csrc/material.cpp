@@ -12,6 +12,7 @@
 #include <cstring>
 #include <thread>
 
+#include "rho.h"
 #include "spectral.h"
 
 namespace mpss {
@@ -544,9 +545,6 @@ void build_profile(const LayerParams &lp, int desired_length, bool lerp_thin, Pr
 
 // ------------------------------------------------------------ rho_hd table
 namespace {
-constexpr float kPi = 3.14159265358979323846f;  // pbrt.h:196 (float)
-constexpr float kOneMinusEps = 0x1.fffffep-1f;  // montecarlo.h:48-50
-
 struct MT {  // MT19937 (core/rng.cpp)
     uint32_t mt[624];
     int i;
@@ -569,136 +567,64 @@ struct MT {  // MT19937 (core/rng.cpp)
         y ^= y >> 18;
         return y;
     }
-    float uniform() { return (float)(next() & 0xffffff) / (float)(1 << 24); }
+    float uniform() { return (float)(next() & 0xffffff) / (float)(1 << 24); }  // RNG::RandomFloat
 };
 
-struct V3 { float x, y, z; };
-inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-
-struct Beckmann {
-    float rms2, rcp;
-    float D(V3 wh) const {  // reflection.h:514-521
-        const float ct = fabsf(wh.z), c2 = ct * ct, d = c2 * c2 * kPi;
-        if (d == 0.f) return 0.f;
-        return rcp * expf((c2 - 1) * rcp / c2) / d;
-    }
-};
-
-float fr_dielectric(float cosi, float ei, float et, bool fixed) {  // reflection.cpp:132-153; reflection.h:315-324
-    cosi = std::min(std::max(cosi, -1.f), 1.f);
-    if (!(cosi > 0.)) std::swap(ei, et);
-    const float sint = ei / et * sqrtf(std::max(0.f, 1.f - cosi * cosi));
-    float F;
-    if (sint >= 1.)
-        F = 1.f;
-    else {
-        const float cost = sqrtf(std::max(0.f, 1.f - sint * sint)), ci = fabsf(cosi);
-        const float par = ((et * ci) - (ei * cost)) / ((et * ci) + (ei * cost));
-        const float per = ((ei * ci) - (et * cost)) / ((ei * ci) + (et * cost));
-        F = (par * par + per * per) / 2.f;
-    }
-    if (fixed) F = F + F * (1.f - F) * (1.f - F);
-    return F;
-}
-
-struct MicrofacetR1 {  // Microfacet(R = 1, FresnelDielectric(1, eta), Beckmann)
-    Beckmann dist;
-    float eta;
-    bool fixed;
-    float G(V3 wo, V3 wi, V3 wh) const {
-        const float a = fabsf(wh.z), wowh = fabsf(dot(wo, wh));
-        return std::min(1.f, std::min(2.f * a * fabsf(wo.z) / wowh, 2.f * a * fabsf(wi.z) / wowh));
-    }
-    float f(V3 wo, V3 wi) const {  // reflection.cpp:228-240
-        const float co = fabsf(wo.z), ci = fabsf(wi.z);
-        if (ci == 0.f || co == 0.f) return 0.f;
-        V3 wh = {wi.x + wo.x, wi.y + wo.y, wi.z + wo.z};
-        if (wh.x == 0. && wh.y == 0. && wh.z == 0.) return 0.f;
-        const float inv = 1.f / sqrtf(wh.x * wh.x + wh.y * wh.y + wh.z * wh.z);
-        wh = {wh.x * inv, wh.y * inv, wh.z * inv};
-        const float F = fr_dielectric(dot(wi, wh), 1.f, eta, fixed);
-        return 1.f * dist.D(wh) * G(wo, wi, wh) * F / (4.f * ci * co);
-    }
-    float sample_f(V3 wo, V3 &wi, float u1, float u2, float &pdf) const {  // reflection.cpp:548-570, 391-397
-        const float th = atanf(sqrtf(-dist.rms2 * logf(1.f - u1)));
-        const float ct = cosf(th), st = sinf(th), phi = u2 * 2.f * kPi;
-        V3 wh = {st * cosf(phi), st * sinf(phi), ct};
-        if (!(wo.z * wh.z > 0.f)) wh = {-wh.x, -wh.y, -wh.z};
-        const float dw = dot(wo, wh);
-        wi = {-wo.x + 2.f * dw * wh.x, -wo.y + 2.f * dw * wh.y, -wo.z + 2.f * dw * wh.z};
-        float bp = dist.D(wh) * ct / (4.f * dot(wo, wh));
-        if (dot(wo, wh) <= 0.f || bp < 1e-20f) bp = 0.f;
-        pdf = bp;
-        if (!(wo.z * wi.z > 0.f)) return 0.f;
-        return f(wo, wi);
-    }
-};
-
-void stratified(std::vector<float> &s, int n, MT &rng) {  // montecarlo.cpp:158-168
+void stratified(std::vector<float> &s, int n, MT &rng) {  // StratifiedSample2D, montecarlo.cpp:158-168
     s.resize((size_t)2 * n * n);
-    const float dx = 1.f / n;
     float *p = s.data();
     for (int y = 0; y < n; ++y)
         for (int x = 0; x < n; ++x) {
             const float jx = rng.uniform(), jy = rng.uniform();
-            *p++ = std::min((x + jx) * dx, kOneMinusEps);
-            *p++ = std::min((y + jy) * dx, kOneMinusEps);
+            rho_stratum(x, y, n, jx, jy, p[0], p[1]);
+            p += 2;
         }
 }
-
-struct Kahan {
-    float sum = 0.f, c = 0.f;
-    void add(float v) {
-        const float y = v - c, t = sum + y;
-        c = (t - sum) - y;
-        sum = t;
-    }
-};
 }  // namespace
+
+// ComputeRhoHHFromBxDF, multipole.cpp:466-480; BxDF::rho(n, s1, s2), reflection.cpp:637-652
+float rho_hh(float roughness, float eta, bool fixed, int sqrt_samples) {
+    const Microfacet m = rho_bxdf(roughness, eta, fixed);
+    const int n = sqrt_samples * sqrt_samples;
+    MT rng(kRhoSeed * 3u * 7u);
+    std::vector<float> s1, s2;
+    stratified(s1, sqrt_samples, rng);
+    stratified(s2, sqrt_samples, rng);
+    KahanF k;
+    for (int i = 0; i < n; ++i) {
+        const float z = s1[2 * i], r = sqrtf(std::max(0.f, 1.f - z * z)), phi = 2 * kPiF * s1[2 * i + 1];
+        const V3 wo = {r * m_cos(phi), r * m_sin(phi), z};  // UniformSampleHemisphere
+        V3 wi;
+        float pdf = 0.f;
+        beckmann_sample(m, wo, s2[2 * i], s2[2 * i + 1], wi, pdf);
+        float f = 0.f;
+        if (wo.z * wi.z > 0.f) {
+            const MfTerms t = microfacet_terms(m, wo, wi);
+            if (!t.zero) f = 1.f * t.D * t.G * t.F / t.den;
+        }
+        if (pdf > 0.) k.add(f * fabsf(wi.z) * fabsf(wo.z) / (kInvTwoPiF * pdf));
+    }
+    return k.sum / (kPiF * n);
+}
 
 void build_rho_table(float roughness, float eta, bool fixed, int n_entries, int sqrt_samples, RhoTable &out,
                      int nthreads) {
-    MicrofacetR1 bx;
-    const float rms = roughness < 1e-3f ? 1e-3f : roughness;
-    bx.dist.rms2 = rms * rms;
-    bx.dist.rcp = 1 / bx.dist.rms2;
-    bx.eta = eta;
-    bx.fixed = fixed;
+    const Microfacet m = rho_bxdf(roughness, eta, fixed);
     out.hd.assign(n_entries, 0.f);
     const int n = sqrt_samples * sqrt_samples;
     parallel_for(n_entries, nthreads, [&](int id) {  // RhoTask::Run, multipole.cpp:506-518
-        MT rng((uint32_t)(6428263u * (uint32_t)id));
+        MT rng(kRhoSeed * (uint32_t)id);
         std::vector<float> s;
         stratified(s, sqrt_samples, rng);
-        float ct = (float)id / (float)(n_entries - 1);
-        if (ct == 0.f) ct = 0.01f / (float)(n_entries - 1);
-        const float st = sqrtf(1 - ct * ct);
-        const V3 wo = {st * cosf(0.f), st * sinf(0.f), ct};
-        Kahan k;
+        const V3 wo = rho_wo(rho_costheta(id, n_entries));
+        KahanF k;
         for (int i = 0; i < n; ++i) {
-            V3 wi;
-            float pdf = 0.f;
-            const float f = bx.sample_f(wo, wi, s[2 * i], s[2 * i + 1], pdf);
-            if (pdf > 0.) k.add(f * fabsf(wi.z) / pdf);
+            float t;
+            if (rho_term(m, wo, s[2 * i], s[2 * i + 1], t)) k.add(t);
         }
         out.hd[id] = k.sum / (float)n;
     });
-    {  // ComputeRhoHHFromBxDF, multipole.cpp:466-480; BxDF::rho(n, s1, s2), reflection.cpp:637-652
-        MT rng(6428263u * 3u * 7u);
-        std::vector<float> s1, s2;
-        stratified(s1, sqrt_samples, rng);
-        stratified(s2, sqrt_samples, rng);
-        Kahan k;
-        for (int i = 0; i < n; ++i) {
-            const float z = s1[2 * i], r = sqrtf(std::max(0.f, 1.f - z * z)), phi = 2 * kPi * s1[2 * i + 1];
-            const V3 wo = {r * cosf(phi), r * sinf(phi), z};
-            V3 wi;
-            float pdf = 0.f;
-            const float f = bx.sample_f(wo, wi, s2[2 * i], s2[2 * i + 1], pdf);
-            if (pdf > 0.) k.add(f * fabsf(wi.z) * fabsf(wo.z) / (0.15915494309189533577f * pdf));
-        }
-        out.hh = k.sum / (kPi * n);
-    }
+    out.hh = rho_hh(roughness, eta, fixed, sqrt_samples);
 }
 
 }  // namespace mpss

@@ -44,6 +44,12 @@ void build_profile(const LayerParams &lp, int desired_length, bool lerp_on_thin_
 // The same profile built on the current HIP device (profile_gpu.hip); out is filled on the host.
 void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
                        hipStream_t stream = 0);
+// The same rho_hd table on the current HIP device (rho_gpu.hip): bit-identical to build_rho_table
+// (one MT19937 stream per entry, terms Kahan-summed in sample order); rho_hh on the host.
+void build_rho_table_gpu(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
+                         RhoTable &out, hipStream_t stream = 0);
+// ComputeRhoHHFromBxDF (multipole.cpp:466-480)
+float rho_hh(float roughness, float eta, bool fixed_fresnel, int sqrt_samples);
 void build_rho_table(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
                      RhoTable &out, int nthreads = 0);
 

@@ -45,7 +45,8 @@ def test_gpu_profile_512_and_rho(mpss, torch_dev, golden):
     ref = golden["profile_512"]
     assert np.all(np.abs(got - ref) <= 1e-6 * np.abs(ref).max(axis=1, keepdims=True))
     assert np.allclose(tot, golden["profile_512_total"], rtol=1e-5)
-    assert np.array_equal(rho, golden["rho_hd"])
+    ulps = np.abs(rho.view(np.int32).astype(np.int64) - golden["rho_hd"].view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1 and (ulps == 0).mean() >= 0.999  # GPU rho_hd (rho_gpu.hip)
 
 
 @pytest.mark.parametrize("mode", [1, 0])
