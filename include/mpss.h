@@ -74,7 +74,19 @@ typedef struct {
                                   default 1 << 24 */
     int use_poisson_point_finder; /* "usepoissonpointfinder" = false: SurfacePoints by random-walk
                                   dart throwing (FindPoissonPointDistribution) instead of tessellation */
+    int sampler;               /* MPSS_SAMPLER_HASH (default): counter-hash scrambled (0,2) sequences, a
+                                  sample's values depend only on (seed, pixel, index) -- any tiling,
+                                  any GPU count; MPSS_SAMPLER_REFERENCE: the reference's own streams
+                                  replayed -- LDSampler's per-task MT19937 (RNG(task)) scrambles and
+                                  shuffles, Li's 6 draws per camera hit, IrradianceTask's RNG(47 k)
+                                  (samplerrenderer.cpp:60-225, montecarlo.cpp:200-250,
+                                  multipolesubsurface.cpp:72-152); seeds are then ignored and spp is
+                                  rounded up to a power of two as LDSampler does */
+    int replay_cores;          /* NumSystemCores() of the reference run being replayed (its task
+                                  counts, samplerrenderer.cpp:207, multipolesubsurface.cpp:198) = 8 */
 } mpss_config;
+
+enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };
 
 void mpss_config_defaults(mpss_config *cfg);
 int mpss_create(const mpss_config *cfg, mpss_ctx **out);
@@ -196,6 +208,11 @@ int mpss_load_pointsfile(mpss_ctx *ctx, const char *path);
 int mpss_save_pointsfile(mpss_ctx *ctx, const char *path);
 /* Irradiance E[n][30] of the last Preprocess. */
 int mpss_get_irradiance(mpss_ctx *ctx, float *E, uint32_t *n);
+/* The reference sampler's sample values (mpss_config.sampler = MPSS_SAMPLER_REFERENCE) for the
+ * film's whole sample extent at spp (rounded up to a power of two): (yres + 1) x (xres + 1)
+ * pixels x spp samples x *k floats -- image u, v, then per light and light sample: light
+ * position u0, u1, BSDF component, BSDF direction u0, u1. Query *k and *n_floats with out NULL. */
+int mpss_replay_samples(mpss_ctx *ctx, int spp, float *out, uint64_t *n_floats, int *k);
 /* MultipoleSubsurfaceIntegrator::Preprocess: tessellation, irradiance (GPU), octree. */
 int mpss_preprocess(mpss_ctx *ctx, uint32_t seed);
 /* Render pixels [x0,x1) x [y0,y1) at spp samples per pixel; xyzw_dev receives

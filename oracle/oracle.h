@@ -82,6 +82,10 @@ float o_sample_profile(const float *data, int len, float rcp, float dsq);
 void o_rho_table(float roughness, float eta, int n_entries /*1025*/, int sqrt_samples /*256*/,
                  int nthreads, float *hd, float *hh);
 uint32_t o_mt_first(uint32_t seed, int n, uint32_t *out); /* MT19937 stream check */
+/* MT19937, core/rng.cpp (RNG::Seed, RNG::RandomUInt) */
+typedef struct { uint32_t mt[624]; int mti; } o_mt;
+void o_mt_seed(o_mt *r, uint32_t seed);
+uint32_t o_mt_u32(o_mt *r);
 
 /* ---- octree + Mo (diffusionutil.h:86-234; multipolesubsurface.cpp:301-321) ---- */
 typedef struct o_octree o_octree;
@@ -159,6 +163,21 @@ void o_envmap_lookup(const o_envmap *m, float s, float t, float out[3]);
 void o_envmap_sample(const o_envmap *m, float u0, float u1, float uv[2], float *pdf);
 float o_envmap_pdf(const o_envmap *m, float u, float v);
 long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_point *out, long cap);
+
+/* ---- the reference sampler (samplerrenderer.cpp:60-225, lowdiscrepancy.cpp:40-93,
+ *      montecarlo.{h:254-333, cpp:200-250}, multipolesubsurface.cpp:72-152) ----
+ * Sample values of the film's whole sample extent ((xres+1) x (yres+1) pixels, spp a power of two)
+ * as the reference's render tasks draw them with `cores` = NumSystemCores(); one row of K floats
+ * per camera sample (pixel-major, then sample): image u, v, then per light (scene order) and light
+ * sample j: light pos u0, u1, BSDF component, BSDF dir u0, u1. li_draws: RNG values Li draws per
+ * camera-ray hit (6 with maxdepth > 0). Returns K; vals may be NULL to query it. */
+int o_replay_render_table(o_scene *s, int spp, int cores, int li_draws, int nthreads, float *vals);
+/* IrradianceTask's RNG(47 k) scrambles: scr[(i * nlights + l) * 2 + {0, 1}] */
+void o_replay_irradiance_scr(int n, int nlights, int cores, uint32_t *scr);
+/* o_irradiance / o_render_tile with the reference sampler's values instead of counter hashes */
+void o_irradiance_replay(o_scene *s, int n, const o_surface_point *pts, const uint32_t *scr, int nthreads, float *E);
+void o_render_tile_replay(o_scene *s, int spp, const float *vals, int K, int x0, int x1, int y0, int y1,
+                          int nthreads, float *xyzw);
 void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E);
 void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, const float *E, const float *area,
                         float max_error);

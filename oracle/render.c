@@ -134,6 +134,7 @@ typedef struct {
     float r, phimax, thetamin, thetamax, area;
     float Le[O_NB];
     int ns_pow2;
+    int replay_off;       /* first float of this light's values in a reference-sampler row */
     float l2w[9], w2l[9]; /* kind 1: LightToWorld, WorldToLight */
     o_envmap em;          /* kind 1: radiance map + Distribution2D */
 } o_light;
@@ -1175,6 +1176,7 @@ typedef struct {
     int n, nthreads, tid;
     uint32_t seed;
     float *E;
+    const uint32_t *scr; /* reference-sampler scrambles (o_replay_irradiance_scr) or NULL */
 } irr_job;
 
 static void *irr_worker(void *arg) {
@@ -1191,8 +1193,14 @@ static void *irr_worker(void *arg) {
             float El[O_NB];
             for (int c = 0; c < O_NB; ++c) El[c] = 0.f;
             int ns = L->ns_pow2;
-            uint32_t sc0 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS);
-            uint32_t sc1 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS + 8u);
+            uint32_t sc0, sc1;
+            if (j->scr) { /* IrradianceTask: scramble[2] = {rng.RandomUInt(), rng.RandomUInt()} */
+                sc0 = j->scr[((size_t)i * s->nlights + l) * 2];
+                sc1 = j->scr[((size_t)i * s->nlights + l) * 2 + 1];
+            } else {
+                sc0 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS);
+                sc1 = hash3(j->seed, (uint32_t)i, 16u * l + D_IRR_POS + 8u);
+            }
             for (int k = 0; k < ns; ++k) {
                 lsamp ls = light_sample(L, p, sp->ray_eps, vdc((uint32_t)k, sc0), sobol((uint32_t)k, sc1));
                 if (dot(ls.wi, n) <= 0.f) continue;
@@ -1225,16 +1233,25 @@ static void run_threads(void *(*fn)(void *), void *jobs, size_t job_size, int nt
     free(th);
 }
 
-void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E) {
+static void irradiance_run(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, const uint32_t *scr,
+                           int nthreads, float *E) {
     scene_prepare(s);
     if (nthreads < 1) nthreads = 1;
     irr_job *jobs = (irr_job *)malloc(nthreads * sizeof(irr_job));
     for (int t = 0; t < nthreads; ++t) {
-        irr_job j = {s, pts, n, nthreads, t, seed, E};
+        irr_job j = {s, pts, n, nthreads, t, seed, E, scr};
         jobs[t] = j;
     }
     run_threads(irr_worker, jobs, sizeof(irr_job), nthreads);
     free(jobs);
+}
+
+void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E) {
+    irradiance_run(s, n, pts, seed, NULL, nthreads, E);
+}
+
+void o_irradiance_replay(o_scene *s, int n, const o_surface_point *pts, const uint32_t *scr, int nthreads, float *E) {
+    irradiance_run(s, n, pts, 0, scr, nthreads, E);
 }
 
 void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nr, const float *E, const float *area,
@@ -1263,8 +1280,9 @@ static void to_xyz(const float L[O_NB], float xyz[3]) { /* Spectrum::ToXYZ + sam
     xyz[0] = X; xyz[1] = Y; xyz[2] = Z;
 }
 
+/* row: the sample's reference-sampler values (o_replay_render_table layout) or NULL (hashes) */
 static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, int si, float X, float Y,
-                      float xyz[3]) {
+                      const float *row, float xyz[3]) {
     const uint32_t pix = (uint32_t)py * (uint32_t)s->xres + (uint32_t)px;
     float L[O_NB];
     for (int c = 0; c < O_NB; ++c) L[c] = 0.f;
@@ -1347,7 +1365,15 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
             uint32_t k = base + (uint32_t)j;
             float ed[O_NB], f[O_NB];
             for (int c = 0; c < O_NB; ++c) ed[c] = 0.f;
-            lsamp ls = light_sample(Lt, fr.p, reps, vdc(k, a0), sobol(k, a1));
+            /* LightSample(sample, lightSampleOffsets[l], j), BSDFSample(sample, bsdfSampleOffsets[l], j) */
+            float lu0, lu1, ubc, ub0, ub1;
+            if (row) {
+                const float *e = row + s->lights[l].replay_off + 5 * j;
+                lu0 = e[0]; lu1 = e[1]; ubc = e[2]; ub0 = e[3]; ub1 = e[4];
+            } else {
+                lu0 = vdc(k, a0); lu1 = sobol(k, a1); ubc = vdc(k, bc); ub0 = vdc(k, b0); ub1 = sobol(k, b1);
+            }
+            lsamp ls = light_sample(Lt, fr.p, reps, lu0, lu1);
             float lightPdf = ls.pdf;
             if (lightPdf > 0.f && ls.nonblack && (mat->has_refl || mat->has_trans)) {
                 if (bsdf_f(mat, &fr, wo, ls.wi, to_local(&fr, wo), to_local(&fr, ls.wi), f) &&
@@ -1361,13 +1387,13 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
             int ncomp = mat->has_refl + mat->has_trans;
             if (ncomp > 0) {
                 /* BSDF::Sample_f: component by uComponent, R before T */
-                int which = (int)floorf(vdc(k, bc) * (float)ncomp);
+                int which = (int)floorf(ubc * (float)ncomp);
                 if (which > ncomp - 1) which = ncomp - 1;
                 int pick_t = !mat->has_refl || which == 1;
                 v3 wil, wol = to_local(&fr, wo);
                 float bsdfPdf;
-                if (pick_t) mt_sample(mat, wol, vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
-                else mf_sample(mat, wol, vdc(k, b0), sobol(k, b1), &wil, &bsdfPdf);
+                if (pick_t) mt_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
+                else mf_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
                 if (bsdfPdf != 0.f) {
                     v3 wi = to_world(&fr, wil);
                     if (ncomp > 1) {
@@ -1416,6 +1442,8 @@ typedef struct {
     int spp, x0, x1, y0, y1, nthreads, tid;
     uint32_t seed;
     float *out;
+    const float *vals; /* reference-sampler table (o_replay_render_table) or NULL */
+    int K;
 } tile_job;
 
 /* One pixel: its own samples, then neighbours' samples whose rounded image position lands
@@ -1431,13 +1459,23 @@ static void render_pixel(const tile_job *j, int px, int py, float *o4) {
         uint32_t pix = (uint32_t)qy * (uint32_t)s->xres + (uint32_t)qx;
         uint32_t su = hash3(j->seed, pix, D_IMAGE), sv = hash3(j->seed, pix, D_IMAGE + 1);
         for (int si = 0; si < j->spp; ++si) {
-            float X = (float)qx + vdc((uint32_t)si, su), Y = (float)qy + sobol((uint32_t)si, sv);
+            const float *row = NULL;
+            float X, Y;
+            if (j->vals) { /* imageX = xPos + imageSamples[2 i] (montecarlo.cpp:236-237) */
+                row = j->vals + (((size_t)qy * (size_t)(s->xres + 1) + (size_t)qx) * (size_t)j->spp + (size_t)si) *
+                                    (size_t)j->K;
+                X = (float)qx + row[0];
+                Y = (float)qy + row[1];
+            } else {
+                X = (float)qx + vdc((uint32_t)si, su);
+                Y = (float)qy + sobol((uint32_t)si, sv);
+            }
             int lx, hx, ly, hy;
             extent(X, s->xres, &lx, &hx);
             extent(Y, s->yres, &ly, &hy);
             if (px < lx || px > hx || py < ly || py > hy) continue;
             float xyz[3];
-            sample_li(s, j->spp, j->seed, qx, qy, si, X, Y, xyz);
+            sample_li(s, j->spp, j->seed, qx, qy, si, X, Y, row, xyz);
             acc[0] += 1.f * xyz[0];
             acc[1] += 1.f * xyz[1];
             acc[2] += 1.f * xyz[2];
@@ -1457,16 +1495,202 @@ static void *tile_worker(void *arg) {
     return NULL;
 }
 
-void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw) {
+static void render_run(o_scene *s, int spp, uint32_t seed, const float *vals, int K, int x0, int x1, int y0, int y1,
+                       int nthreads, float *xyzw) {
     scene_prepare(s);
     if (nthreads < 1) nthreads = 1;
     tile_job *jobs = (tile_job *)malloc(nthreads * sizeof(tile_job));
     for (int t = 0; t < nthreads; ++t) {
-        tile_job j = {s, spp, x0, x1, y0, y1, nthreads, t, seed, xyzw};
+        tile_job j = {s, spp, x0, x1, y0, y1, nthreads, t, seed, xyzw, vals, K};
         jobs[t] = j;
     }
     run_threads(tile_worker, jobs, sizeof(tile_job), nthreads);
     free(jobs);
+}
+
+void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw) {
+    render_run(s, spp, seed, NULL, 0, x0, x1, y0, y1, nthreads, xyzw);
+}
+
+void o_render_tile_replay(o_scene *s, int spp, const float *vals, int K, int x0, int x1, int y0, int y1,
+                          int nthreads, float *xyzw) {
+    render_run(s, spp, 0, vals, K, x0, x1, y0, y1, nthreads, xyzw);
+}
+
+/* ------------------------------------------------------------------ the reference sampler */
+/* Shuffle (montecarlo.h:183-189) */
+static void shuffle(float *samp, uint32_t count, uint32_t dims, o_mt *rng) {
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t other = i + (o_mt_u32(rng) % (count - i));
+        for (uint32_t j = 0; j < dims; ++j) {
+            float t = samp[dims * i + j];
+            samp[dims * i + j] = samp[dims * other + j];
+            samp[dims * other + j] = t;
+        }
+    }
+}
+
+/* LDShuffleScrambled1D (montecarlo.h:314-322) */
+static void ld_shuffle_scrambled_1d(int n, int npix, float *samples, o_mt *rng) {
+    uint32_t scramble = o_mt_u32(rng);
+    for (int i = 0; i < n * npix; ++i) samples[i] = vdc((uint32_t)i, scramble);
+    for (int i = 0; i < npix; ++i) shuffle(samples + i * n, (uint32_t)n, 1, rng);
+    shuffle(samples, (uint32_t)npix, (uint32_t)n, rng);
+}
+
+/* LDShuffleScrambled2D (montecarlo.h:325-333); the scrambles are drawn left to right */
+static void ld_shuffle_scrambled_2d(int n, int npix, float *samples, o_mt *rng) {
+    uint32_t scramble[2];
+    scramble[0] = o_mt_u32(rng);
+    scramble[1] = o_mt_u32(rng);
+    for (int i = 0; i < n * npix; ++i) { /* Sample02 */
+        samples[2 * i] = vdc((uint32_t)i, scramble[0]);
+        samples[2 * i + 1] = sobol((uint32_t)i, scramble[1]);
+    }
+    for (int i = 0; i < npix; ++i) shuffle(samples + 2 * i * n, (uint32_t)n, 2, rng);
+    shuffle(samples, (uint32_t)npix, (uint32_t)(2 * n), rng);
+}
+
+/* Sampler::ComputeSubWindow (sampler.cpp:55-78) */
+static void sub_window(int num, int count, int xs, int xe, int ys, int ye, int *x0, int *x1, int *y0, int *y1) {
+    int dx = xe - xs, dy = ye - ys;
+    int nx = count, ny = 1;
+    while ((nx & 0x1) == 0 && 2 * dx * ny < dy * nx) {
+        nx >>= 1;
+        ny <<= 1;
+    }
+    int xo = num % nx, yo = num / nx;
+    float tx0 = (float)xo / (float)nx, tx1 = (float)(xo + 1) / (float)nx;
+    float ty0 = (float)yo / (float)ny, ty1 = (float)(yo + 1) / (float)ny;
+    *x0 = (int)floorf((1.f - tx0) * (float)xs + tx0 * (float)xe); /* Floor2Int(Lerp(..)) */
+    *x1 = (int)floorf((1.f - tx1) * (float)xs + tx1 * (float)xe);
+    *y0 = (int)floorf((1.f - ty0) * (float)ys + ty0 * (float)ye);
+    *y1 = (int)floorf((1.f - ty1) * (float)ys + ty1 * (float)ye);
+}
+
+typedef struct {
+    o_scene *s;
+    int spp, K, li_draws, ntasks, next;
+    float *vals;
+    pthread_mutex_t mu;
+} rtab_job;
+
+/* SamplerRendererTask::Run (samplerrenderer.cpp:60-167) for task `task`: RNG(task), then per pixel
+ * LDSampler::GetMoreSamples -> LDPixelSample (lowdiscrepancy.cpp:69-82, montecarlo.cpp:200-250),
+ * then per sample the camera ray and, when it hits, Li's BSDFSample(rng) draws. */
+static void render_task(rtab_job *jb, int task) {
+    o_scene *s = jb->s;
+    const int spp = jb->spp, K = jb->K, W1 = s->xres + 1, H1 = s->yres + 1;
+    int x0, x1, y0, y1;
+    sub_window(task, jb->ntasks, 0, W1, 0, H1, &x0, &x1, &y0, &y1);
+    if (x0 == x1 || y0 == y1) return; /* GetSubSampler returns NULL */
+    o_mt rng;
+    o_mt_seed(&rng, (uint32_t)task);
+    /* n1D: per light comp (L), comp (BSDF); then the emission integrator's 1, 1. n2D: pos, dir. */
+    const int nl = s->nlights, c1 = 2 * nl + 2, c2 = 2 * nl;
+    int n1[2 * 254 + 2], n2[2 * 254];
+    for (int l = 0; l < nl; ++l) {
+        n1[2 * l] = n1[2 * l + 1] = s->lights[l].ns_pow2;
+        n2[2 * l] = n2[2 * l + 1] = s->lights[l].ns_pow2;
+    }
+    n1[2 * nl] = n1[2 * nl + 1] = 1;
+    float *image = (float *)malloc(sizeof(float) * 2 * spp), *lens = (float *)malloc(sizeof(float) * 2 * spp);
+    float *time = (float *)malloc(sizeof(float) * spp);
+    float **one = (float **)malloc(sizeof(float *) * (c1 + 1)), **two = (float **)malloc(sizeof(float *) * (c2 + 1));
+    for (int a = 0; a < c1; ++a) one[a] = (float *)malloc(sizeof(float) * n1[a] * spp);
+    for (int a = 0; a < c2; ++a) two[a] = (float *)malloc(sizeof(float) * 2 * n2[a] * spp);
+    v3 o = xpoint(s->c2w, mk(0.f, 0.f, 0.f));
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            ld_shuffle_scrambled_2d(1, spp, image, &rng);
+            ld_shuffle_scrambled_2d(1, spp, lens, &rng);
+            ld_shuffle_scrambled_1d(1, spp, time, &rng);
+            for (int a = 0; a < c1; ++a) ld_shuffle_scrambled_1d(n1[a], spp, one[a], &rng);
+            for (int a = 0; a < c2; ++a) ld_shuffle_scrambled_2d(n2[a], spp, two[a], &rng);
+            for (int i = 0; i < spp; ++i) {
+                float *row = jb->vals + (((size_t)y * W1 + x) * spp + i) * K;
+                row[0] = image[2 * i];
+                row[1] = image[2 * i + 1];
+                for (int l = 0; l < nl; ++l) {
+                    const int n = n1[2 * l];
+                    for (int j = 0; j < n; ++j) { /* samples[i].oneD[a][j] = oneD[a][n i + j], twoD: 2 (n i + j) */
+                        float *e = row + s->lights[l].replay_off + 5 * j;
+                        e[0] = two[2 * l][2 * (n * i + j)];
+                        e[1] = two[2 * l][2 * (n * i + j) + 1];
+                        e[2] = one[2 * l + 1][n * i + j];
+                        e[3] = two[2 * l + 1][2 * (n * i + j)];
+                        e[4] = two[2 * l + 1][2 * (n * i + j) + 1];
+                    }
+                }
+            }
+            if (jb->li_draws > 0)
+                for (int i = 0; i < spp; ++i) {
+                    float X = (float)x + image[2 * i], Y = (float)y + image[2 * i + 1];
+                    v3 d = xvector(s->c2w, nrm(xpoint(s->r2c, mk(X, Y, 0.f))));
+                    if (intersect(s, o, d, 0.f, INFINITY).tri != NO_HIT)
+                        for (int k = 0; k < jb->li_draws; ++k) (void)o_mt_u32(&rng);
+                }
+        }
+    for (int a = 0; a < c1; ++a) free(one[a]);
+    for (int a = 0; a < c2; ++a) free(two[a]);
+    free(one); free(two); free(image); free(lens); free(time);
+}
+
+static void *rtab_worker(void *arg) {
+    rtab_job *jb = (rtab_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&jb->mu);
+        int task = jb->next++;
+        pthread_mutex_unlock(&jb->mu);
+        if (task >= jb->ntasks) break;
+        render_task(jb, task);
+    }
+    return NULL;
+}
+
+static int round_pow2_int(int v) { int r = 1; while (r < v) r <<= 1; return r; }
+
+int o_replay_render_table(o_scene *s, int spp, int cores, int li_draws, int nthreads, float *vals) {
+    int K = 2;
+    for (int l = 0; l < s->nlights; ++l) {
+        s->lights[l].replay_off = K;
+        K += 5 * s->lights[l].ns_pow2;
+    }
+    if (!vals) return K;
+    scene_prepare(s);
+    /* nTasks = RoundUpPow2(max(32 * NumSystemCores(), nPixels / (16 * 16))) */
+    int a = 32 * cores, b = (int)(((long)s->xres * s->yres) / (16 * 16));
+    rtab_job jb;
+    memset(&jb, 0, sizeof(jb));
+    jb.s = s; jb.spp = spp; jb.K = K; jb.li_draws = li_draws; jb.vals = vals;
+    jb.ntasks = round_pow2_int(a > b ? a : b);
+    pthread_mutex_init(&jb.mu, NULL);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, rtab_worker, &jb);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    pthread_mutex_destroy(&jb.mu);
+    return K;
+}
+
+/* IrradianceTask::Run (multipolesubsurface.cpp:72-152) with nTasks = RoundUpPow2(max(32 cores, N/4096)) */
+void o_replay_irradiance_scr(int n, int nlights, int cores, uint32_t *scr) {
+    int a = 32 * cores, b = n / 4096;
+    int T = round_pow2_int(a > b ? a : b);
+    for (int k = 0; k < T; ++k) {
+        size_t i0 = (size_t)((uint64_t)k * (uint64_t)n / (uint64_t)T);
+        size_t i1 = (size_t)((uint64_t)(k + 1) * (uint64_t)n / (uint64_t)T);
+        if (i0 == i1) continue;
+        o_mt rng;
+        o_mt_seed(&rng, (uint32_t)k * 47u);
+        for (size_t i = i0; i < i1; ++i)
+            for (int l = 0; l < nlights; ++l) {
+                scr[(i * nlights + l) * 2] = o_mt_u32(&rng);
+                scr[(i * nlights + l) * 2 + 1] = o_mt_u32(&rng);
+                (void)o_mt_u32(&rng); /* compScramble */
+            }
+    }
 }
 
 void o_scene_free(o_scene *s) {

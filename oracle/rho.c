@@ -19,13 +19,13 @@
 static const float ONE_M_EPS = 0x1.fffffep-1f; /* montecarlo.h:48-50 */
 
 /* ---- MT19937, rng.cpp ---- */
-typedef struct { uint32_t mt[624]; int mti; } mt_rng;
-static void mt_seed(mt_rng *r, uint32_t s) {
+typedef o_mt mt_rng;
+void o_mt_seed(mt_rng *r, uint32_t s) {
     r->mt[0] = s;
     for (r->mti = 1; r->mti < 624; r->mti++)
         r->mt[r->mti] = (1812433253u * (r->mt[r->mti - 1] ^ (r->mt[r->mti - 1] >> 30)) + (uint32_t)r->mti);
 }
-static uint32_t mt_u32(mt_rng *r) {
+uint32_t o_mt_u32(mt_rng *r) {
     static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
     uint32_t y;
     if (r->mti >= 624) {
@@ -49,12 +49,12 @@ static uint32_t mt_u32(mt_rng *r) {
     y ^= (y >> 18);
     return y;
 }
-static float mt_float(mt_rng *r) { return (float)(mt_u32(r) & 0xffffff) / (float)(1 << 24); }
+static float mt_float(mt_rng *r) { return (float)(o_mt_u32(r) & 0xffffff) / (float)(1 << 24); }
 
 uint32_t o_mt_first(uint32_t seed, int n, uint32_t *out) {
     mt_rng r;
-    mt_seed(&r, seed);
-    for (int i = 0; i < n; ++i) out[i] = mt_u32(&r);
+    o_mt_seed(&r, seed);
+    for (int i = 0; i < n; ++i) out[i] = o_mt_u32(&r);
     return n > 0 ? out[0] : 0;
 }
 
@@ -154,7 +154,7 @@ typedef struct {
 
 static float rho_entry(const rho_job *j, int id) { /* RhoTask::Run, multipole.cpp:506-518 */
     mt_rng r;
-    mt_seed(&r, (uint32_t)(6428263u * (uint32_t)id));
+    o_mt_seed(&r, (uint32_t)(6428263u * (uint32_t)id));
     int n = j->sqrt_samples * j->sqrt_samples;
     float *s = (float *)malloc(sizeof(float) * 2 * n);
     stratified2d(s, j->sqrt_samples, j->sqrt_samples, &r);
@@ -192,7 +192,7 @@ static void *rho_worker(void *arg) {
 /* ComputeRhoHHFromBxDF (multipole.cpp:466-480) with BxDF::rho(nSamples, s1, s2) (reflection.cpp:637-652) */
 static float rho_hh(const mf *m, int sq) {
     mt_rng r;
-    mt_seed(&r, (uint32_t)(6428263u * 3u * 7u));
+    o_mt_seed(&r, (uint32_t)(6428263u * 3u * 7u));
     int n = sq * sq;
     float *s1 = (float *)malloc(sizeof(float) * 2 * n), *s2 = (float *)malloc(sizeof(float) * 2 * n);
     stratified2d(s1, sq, sq, &r);

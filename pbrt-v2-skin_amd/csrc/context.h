@@ -11,6 +11,7 @@
 #include "material.h"
 #include "mo_kernel.h"
 #include "octree.h"
+#include "replay.h"
 #include "scene.h"
 #include "texture_build.h"
 
@@ -104,6 +105,8 @@ public:
     // FindPoissonPointDistribution (usepoissonpointfinder): fills points_ (render_host.hip)
     void find_poisson_points(uint32_t seed);
     void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);
+    // the replay sampler's table (mpss_replay_samples); out may be null to query sizes
+    void replay_samples(int spp, float *out, uint64_t *n_floats, int *k);
     // SubsurfaceOctreeNode::Mo over q device-resident points with material `mid`'s profile
     // (mpss_mo_batch); stream-ordered, safe for concurrent callers on their own streams
     void mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, int32_t *counters_dev, hipStream_t stream);
@@ -126,6 +129,10 @@ private:
     void upload_scene();
     RenderScene render_scene() const;
     int first_bssrdf_material() const;
+    // reference-sampler replay (mpss_config.sampler): sample table of the whole sample extent
+    void ensure_replay_table(int spp);
+    DevBuf<float> replay_vals_;
+    int replay_spp_ = 0, replay_k_ = kReplayImage;
     SceneData scene_;
     bool scene_dirty_ = true, have_points_ = false;
     std::vector<SurfacePoint> points_;

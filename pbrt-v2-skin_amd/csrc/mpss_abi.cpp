@@ -42,8 +42,9 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 4; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
-                                          // 4: tile costs, wave-iteration stats, thread-safe calls
+int mpss_abi_version(void) { return 5; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+                                          // 4: tile costs, wave-iteration stats, thread-safe calls;
+                                          // 5: reference-sampler replay, dipole materials
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -62,6 +63,8 @@ void mpss_config_defaults(mpss_config *c) {
     c->profile_on_host = 0;
     c->max_batch_samples = (int64_t)1 << 24;
     c->use_poisson_point_finder = 0;
+    c->sampler = MPSS_SAMPLER_HASH;
+    c->replay_cores = 8;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -265,6 +268,14 @@ int mpss_save_pointsfile(mpss_ctx *c, const char *path) {
         const size_t put = v.empty() ? 0 : fwrite(v.data(), sizeof(SurfacePoint), v.size(), f);
         fclose(f);
         if (put != v.size()) throw Error(MPSS_ERR_INVALID, "mpss_save_pointsfile: short write");
+    });
+}
+
+int mpss_replay_samples(mpss_ctx *c, int spp, float *out, uint64_t *n_floats, int *k) {
+    return guarded([&] {
+        require(c && n_floats && k, "mpss_replay_samples: null argument");
+        require(spp >= 1 && spp <= 32768, "mpss_replay_samples: spp out of range");
+        reinterpret_cast<Context *>(c)->replay_samples(spp, out, n_floats, k);
     });
 }
 

@@ -7,6 +7,7 @@
 #include "geom.h"
 #include "mo_kernel.h"
 #include "mo_band.h"
+#include "replay.h"
 #include "scene.h"
 #include "texture.h"
 
@@ -31,6 +32,7 @@ struct RenderLight {
     const float *tex, *func, *cdf, *rint, *mcdf;
     float mint;
     float l2w[9], w2l[9];
+    int replay_off;      // first float of this light's samples in a replay-table row (replay.h)
 };
 
 struct RenderMaterial {
@@ -62,7 +64,23 @@ struct RenderScene {
     int any_tex;      // some material has an albedo texture or a bump map: shade_tex_kernel runs
     float raster_to_camera[16], camera_to_world[16];
     float dx_camera[3], dy_camera[3];  // PerspectiveCamera dxCamera / dyCamera (perspective.cpp:47-48)
+    // reference-sampler replay (replay.h); null: the counter-hash sampler
+    const float *replay;      // [((y * replay_w + x) * replay_spp + s) * replay_k + ...] sample values
+    int replay_k, replay_w, replay_spp;
+    const uint32_t *irr_scr;  // [point][light][2] IrradianceTask Sample02 scrambles
 };
+
+// The GPU replay of the reference's render-task streams (replay.h): one lane per task, sample
+// values of the film's whole sample extent ((xres + 1) x (yres + 1) pixels x spp) into vals.
+// mt: 624 x ntasks words of MT state. li_draws: RNG values Li consumes per camera-ray hit.
+struct ReplayGen {
+    int ntasks, spp, K, li_draws;
+    uint32_t *mt;
+    float *vals;
+};
+__global__ void replay_render_kernel(RenderScene sc, ReplayGen g);
+// IrradianceTask streams: scr[(i * nlights + l) * 2 + {0, 1}] for points i < n
+__global__ void replay_irradiance_kernel(int n, int nlights, int ntasks, uint32_t *mt, uint32_t *scr);
 
 // A tile [x0,x1) x [y0,y1) extended by one pixel on every side that exists (origin ex0, ey0;
 // ew x eh pixels): a sample whose float image coordinate rounds onto a pixel edge also lands

@@ -401,8 +401,14 @@ __global__ __launch_bounds__(256) void irradiance_kernel(RenderScene sc, const f
         float El[NB];
         for (int c = 0; c < NB; ++c) El[c] = 0.f;
         const int ns = L.nsamples_pow2;
-        const uint32_t scr0 = hash3(seed, (uint32_t)i, 16u * l + DIM_IRR_POS);
-        const uint32_t scr1 = hash3(seed, (uint32_t)i, 16u * l + DIM_IRR_POS + 8u);
+        uint32_t scr0, scr1;
+        if (sc.irr_scr) {  // the reference's RNG(47 k) stream (replay_irradiance_kernel)
+            scr0 = sc.irr_scr[((size_t)i * sc.nlights + l) * 2];
+            scr1 = sc.irr_scr[((size_t)i * sc.nlights + l) * 2 + 1];
+        } else {
+            scr0 = hash3(seed, (uint32_t)i, 16u * l + DIM_IRR_POS);
+            scr1 = hash3(seed, (uint32_t)i, 16u * l + DIM_IRR_POS + 8u);
+        }
         for (int s = 0; s < ns; ++s) {
             const float u0 = van_der_corput((uint32_t)s, scr0), u1 = sobol2((uint32_t)s, scr1);  // Sample02
             const LightSampleOut ls = L.kind ? sample_infinite(L, p, eps, u0, u1) : sample_light(L, p, eps, u0, u1);
@@ -521,6 +527,25 @@ __global__ __launch_bounds__(256) void poisson_walk_kernel(RenderScene sc, Poiss
     count[i] = n;
 }
 
+// The replay-table row of camera sample s of pixel (px, py) (replay.h layout)
+__device__ __forceinline__ const float *replay_row(const RenderScene &sc, int px, int py, int s) {
+    return sc.replay + (((int64_t)py * sc.replay_w + px) * sc.replay_spp + s) * sc.replay_k;
+}
+
+// The image sample of camera sample s of pixel (px, py): LDPixelSample's imageX = xPos + u
+__device__ __forceinline__ void image_sample(const RenderScene &sc, uint32_t seed, int px, int py, int s, float &X,
+                                             float &Y) {
+    if (sc.replay) {
+        const float *r = replay_row(sc, px, py, s);
+        X = (float)px + r[0];
+        Y = (float)py + r[1];
+        return;
+    }
+    const uint32_t pix = (uint32_t)py * (uint32_t)sc.xres + (uint32_t)px;
+    X = (float)px + van_der_corput((uint32_t)s, hash3(seed, pix, DIM_IMAGE));
+    Y = (float)py + sobol2((uint32_t)s, hash3(seed, pix, DIM_IMAGE + 1));
+}
+
 // ------------------------------------------------------------------ camera rays (primary)
 // SamplerRendererTask::Run's per-sample head: image sample -> PerspectiveCamera::GenerateRay ->
 // Scene::Intersect. Surface hits are compacted (one atomic per wave, sample order kept inside
@@ -536,8 +561,8 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch 
     const int px = tb.ex0 + li % tb.ew, py = tb.ey0 + li / tb.ew;
     const uint32_t pix = (uint32_t)py * (uint32_t)sc.xres + (uint32_t)px;
     // image sample (LDPixelSample's imageSamples, montecarlo.cpp:200-250): imageX = x + u in float
-    const float X = (float)px + van_der_corput((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE));
-    const float Y = (float)py + sobol2((uint32_t)s, hash3(tb.seed, pix, DIM_IMAGE + 1));
+    float X, Y;
+    image_sample(sc, tb.seed, px, py, s, X, Y);
     // border samples matter only when the box filter carries them into the tile (film_kernel)
     int lx, hx, ly, hy;
     film_extent(X, sc.xres, lx, hx);
@@ -716,13 +741,26 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     const int ncomp = mat.has_refl + mat.has_trans;
     const V3 wo_l = to_local(fr, wo);
     const float ng_wo = dot(wo, fr.ng);
-    const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
-    const uint32_t nidx = (uint32_t)(s ^ (int)xr) * (uint32_t)ns + (uint32_t)j;
-    const uint32_t sl0 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS), sl1 = hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u),
-                   sb0 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR), sb1 = hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u),
-                   sbc = hash3(seed, pix, 16u * l + DIM_BSDF_COMP);
+    // LightSample(sample, offsets, j) / BSDFSample(sample, offsets, j) (light.cpp, reflection.cpp)
+    float lu0, lu1, ubc, ub0, ub1;
+    if (sc.replay) {
+        const float *r = replay_row(sc, (int)(pix % (uint32_t)sc.xres), (int)(pix / (uint32_t)sc.xres), s) +
+                         L.replay_off + j * kReplayPerLightSample;
+        lu0 = r[0];
+        lu1 = r[1];
+        ubc = r[2];
+        ub0 = r[3];
+        ub1 = r[4];
+    } else {
+        const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
+        const uint32_t nidx = (uint32_t)(s ^ (int)xr) * (uint32_t)ns + (uint32_t)j;
+        lu0 = van_der_corput(nidx, hash3(seed, pix, 16u * l + DIM_LIGHT_POS));
+        lu1 = sobol2(nidx, hash3(seed, pix, 16u * l + DIM_LIGHT_POS + 8u));
+        ubc = van_der_corput(nidx, hash3(seed, pix, 16u * l + DIM_BSDF_COMP));
+        ub0 = van_der_corput(nidx, hash3(seed, pix, 16u * l + DIM_BSDF_DIR));
+        ub1 = sobol2(nidx, hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u));
+    }
     // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
-    const float lu0 = van_der_corput(nidx, sl0), lu1 = sobol2(nidx, sl1);
     const LightSampleOut ls = L.kind ? sample_infinite(L, fr.p, reps, lu0, lu1) : sample_light(L, fr.p, reps, lu0, lu1);
     float lightPdf = ls.pdf;
     float4 st = make_float4(ls.ms, ls.mt, 0.f, 0.f);
@@ -738,15 +776,15 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     }
     // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
     if (ncomp > 0) {
-        int which = (int)floorf(van_der_corput(nidx, sbc) * (float)ncomp);
+        int which = (int)floorf(ubc * (float)ncomp);
         which = which < ncomp - 1 ? which : ncomp - 1;
         const bool pick_t = !mat.has_refl || which == 1;
         V3 wi_l;
         float bsdfPdf;
         if (pick_t)
-            mt_sample_ool(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+            mt_sample_ool(mat.mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
         else
-            beckmann_sample(mat.mf, wo_l, van_der_corput(nidx, sb0), sobol2(nidx, sb1), wi_l, bsdfPdf);
+            beckmann_sample(mat.mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
         if (bsdfPdf != 0.f) {
             const V3 wi = to_world(fr, wi_l);
             if (ncomp > 1) {
@@ -810,8 +848,8 @@ __global__ __launch_bounds__(256) void shade_tex_kernel(RenderScene sc, SampleRe
     const ShadingFrame fr = tri_shading(mesh.view, sc.tri_local[tri], p, 1.f - ha.y - ha.z, ha.y, ha.z);
     // the sample's image position (as primary_kernel) and its offset rays
     const int px = (int)(pix % (uint32_t)sc.xres), py = (int)(pix / (uint32_t)sc.xres);
-    const float X = (float)px + van_der_corput((uint32_t)s, hash3(seed, pix, DIM_IMAGE));
-    const float Y = (float)py + sobol2((uint32_t)s, hash3(seed, pix, DIM_IMAGE + 1));
+    float X, Y;
+    image_sample(sc, seed, px, py, s, X, Y);
     const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
     const V3 dxc = V3{sc.dx_camera[0], sc.dx_camera[1], sc.dx_camera[2]};
     const V3 dyc = V3{sc.dy_camera[0], sc.dy_camera[1], sc.dy_camera[2]};
@@ -1085,6 +1123,149 @@ __global__ __launch_bounds__(256) void probe_kernel(RenderScene sc, int x0, int 
         c = (sc.materials[mid].has_bssrdf && sc.have_octree) ? 2 : 1;
     }
     cls[i] = c;
+}
+
+// ------------------------------------------------------------------ reference-sampler replay
+// One lane per SamplerRendererTask (replay.h): RNG(task) through LDPixelSample for every pixel
+// of the task's sub-window, writing the sample values the render kernels consume into the
+// replay table, and the camera ray of every sample (only whether it hits: Li's 6 draws).
+namespace {
+// Shuffle(samp, count, dims, rng) of `count` blocks of `dims` floats that sit `bstride` floats
+// apart (montecarlo.h:183-189): count draws
+__device__ void replay_shuffle(Mt19937 &rng, float *base, int count, int dims, int64_t bstride) {
+    for (int i = 0; i < count; ++i) {
+        const int other = i + (int)(rng.next() % (uint32_t)(count - i));
+        if (other == i) continue;
+        float *a = base + (int64_t)i * bstride, *b = base + (int64_t)other * bstride;
+        for (int d = 0; d < dims; ++d) {
+            const float t = a[d];
+            a[d] = b[d];
+            b[d] = t;
+        }
+    }
+}
+// Shuffle of a light-sample array inside one camera sample's row: n elements of `dims` floats
+// at stride kReplayPerLightSample
+__device__ void replay_shuffle_elems(Mt19937 &rng, float *e0, int n, int dims) {
+    for (int j = 0; j < n; ++j) {
+        const int other = j + (int)(rng.next() % (uint32_t)(n - j));
+        if (other == j) continue;
+        float *a = e0 + j * kReplayPerLightSample, *b = e0 + other * kReplayPerLightSample;
+        for (int d = 0; d < dims; ++d) {
+            const float t = a[d];
+            a[d] = b[d];
+            b[d] = t;
+        }
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(64) void replay_render_kernel(RenderScene sc, ReplayGen g) {
+    __shared__ int stk_all[kStack * 64];
+    int *stk = stk_all + threadIdx.x;
+    const int task = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (task >= g.ntasks) return;
+    const int ew = sc.xres + 1, eh = sc.yres + 1, spp = g.spp, K = g.K;
+    int x0, x1, y0, y1;
+    replay_sub_window(task, g.ntasks, 0, ew, 0, eh, x0, x1, y0, y1);
+    Mt19937 rng{g.mt + task, g.ntasks, 624};
+    rng.seed((uint32_t)task);
+    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            float *rows = g.vals + ((int64_t)y * ew + x) * spp * K;  // the pixel's spp rows
+            // image: LDShuffleScrambled2D(1, spp)
+            {
+                const uint32_t s0 = rng.next(), s1 = rng.next();
+                for (int i = 0; i < spp; ++i) {
+                    rows[(int64_t)i * K] = van_der_corput((uint32_t)i, s0);
+                    rows[(int64_t)i * K + 1] = sobol2((uint32_t)i, s1);
+                }
+                rng.skip(spp);  // one-element blocks: Shuffle(.., 1, 2) draws once and keeps the order
+                replay_shuffle(rng, rows, spp, 2, K);
+            }
+            rng.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
+            rng.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
+            // 1D arrays: per light (component: drawn only; BSDF component: column 2)
+            for (int l = 0; l < sc.nlights; ++l) {
+                const RenderLight &L = sc.lights[l];
+                const int n = L.nsamples_round;
+                rng.skip(1 + (int64_t)spp * n + spp);
+                const uint32_t scr = rng.next();
+                float *c0 = rows + L.replay_off + 2;
+                for (int i = 0; i < spp; ++i)
+                    for (int j = 0; j < n; ++j)
+                        c0[(int64_t)i * K + j * kReplayPerLightSample] = van_der_corput((uint32_t)(i * n + j), scr);
+                for (int i = 0; i < spp; ++i) replay_shuffle_elems(rng, c0 + (int64_t)i * K, n, 1);
+                for (int i = 0; i < spp; ++i) {  // Shuffle(samples, spp, n): whole blocks
+                    const int other = i + (int)(rng.next() % (uint32_t)(spp - i));
+                    if (other == i) continue;
+                    float *a = c0 + (int64_t)i * K, *b = c0 + (int64_t)other * K;
+                    for (int j = 0; j < n; ++j) {
+                        const float t = a[j * kReplayPerLightSample];
+                        a[j * kReplayPerLightSample] = b[j * kReplayPerLightSample];
+                        b[j * kReplayPerLightSample] = t;
+                    }
+                }
+            }
+            rng.skip(2 * (1 + 2 * (int64_t)spp));  // the emission integrator's two 1D(1) arrays
+            // 2D arrays: per light, light position (columns 0, 1) then BSDF direction (3, 4)
+            for (int l = 0; l < sc.nlights; ++l) {
+                const RenderLight &L = sc.lights[l];
+                const int n = L.nsamples_round;
+                for (int arr = 0; arr < 2; ++arr) {
+                    const uint32_t s0 = rng.next(), s1 = rng.next();
+                    float *c0 = rows + L.replay_off + (arr == 0 ? 0 : 3);
+                    for (int i = 0; i < spp; ++i)
+                        for (int j = 0; j < n; ++j) {
+                            const uint32_t k = (uint32_t)(i * n + j);
+                            c0[(int64_t)i * K + j * kReplayPerLightSample] = van_der_corput(k, s0);
+                            c0[(int64_t)i * K + j * kReplayPerLightSample + 1] = sobol2(k, s1);
+                        }
+                    for (int i = 0; i < spp; ++i) replay_shuffle_elems(rng, c0 + (int64_t)i * K, n, 2);
+                    for (int i = 0; i < spp; ++i) {
+                        const int other = i + (int)(rng.next() % (uint32_t)(spp - i));
+                        if (other == i) continue;
+                        float *a = c0 + (int64_t)i * K, *b = c0 + (int64_t)other * K;
+                        for (int j = 0; j < n; ++j)
+                            for (int d = 0; d < 2; ++d) {
+                                const float t = a[j * kReplayPerLightSample + d];
+                                a[j * kReplayPerLightSample + d] = b[j * kReplayPerLightSample + d];
+                                b[j * kReplayPerLightSample + d] = t;
+                            }
+                    }
+                }
+            }
+            // the pixel's camera rays: Li (6 draws) for every ray that hits
+            if (g.li_draws > 0)
+                for (int i = 0; i < spp; ++i) {
+                    const float X = (float)x + rows[(int64_t)i * K], Y = (float)y + rows[(int64_t)i * K + 1];
+                    const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
+                    const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
+                    const Hit h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 64);
+                    if (h.tri != INT_MIN) rng.skip(g.li_draws);
+                }
+        }
+}
+
+// IrradianceTask::Run's RNG(47 k) (multipolesubsurface.cpp:81, 110-112): per point of the task's
+// slice and per light, scramble[0], scramble[1], compScramble
+__global__ __launch_bounds__(64) void replay_irradiance_kernel(int n, int nlights, int ntasks, uint32_t *mt,
+                                                               uint32_t *scr) {
+    const int task = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (task >= ntasks) return;
+    const int i0 = (int)((uint64_t)task * (uint64_t)n / (uint64_t)ntasks);
+    const int i1 = (int)((uint64_t)(task + 1) * (uint64_t)n / (uint64_t)ntasks);
+    if (i0 == i1) return;
+    Mt19937 rng{mt + task, ntasks, 624};
+    rng.seed((uint32_t)task * 47u);
+    for (int i = i0; i < i1; ++i)
+        for (int l = 0; l < nlights; ++l) {
+            uint32_t *o = scr + ((size_t)i * nlights + l) * 2;
+            o[0] = rng.next();
+            o[1] = rng.next();
+            rng.skip(1);  // compScramble (a LightSample's component: one shape per light here)
+        }
 }
 
 }  // namespace mpss

@@ -156,6 +156,7 @@ void Context::upload_scene() {
     }
     d_meshes_.upload(rm.data(), rm.size());
     std::vector<RenderLight> rl;
+    int replay_off = kReplayImage;
     d_envmaps_.clear();
     // every light's map pointers address valid memory (a 1x1 zero map for area lights), so no
     // load the compiler hoists out of a kind test can fault
@@ -207,9 +208,13 @@ void Context::upload_scene() {
         }
         r.nsamples_pow2 = round_up_pow2(l.nsamples);
         r.nsamples_round = round_up_pow2(l.nsamples);
+        r.replay_off = replay_off;
+        replay_off += kReplayPerLightSample * r.nsamples_round;
         rl.push_back(r);
     }
     d_lights_.upload(rl.data(), rl.size());
+    replay_k_ = replay_off;
+    replay_spp_ = 0;  // the replay table (if any) belongs to the old scene
     std::vector<RenderMaterial> rmat;
     if (!d_lut_.ptr) d_lut_.upload(ewa_weight_lut(), kEwaLut);
     for (auto &t : textures_)
@@ -346,9 +351,20 @@ void Context::preprocess(uint32_t seed) {
         irradiance_.resize((size_t)n * NB);
         for (int i = 0; i < n; ++i) memcpy(&irradiance_[(size_t)i * NB], s, sizeof(s));
     } else {
+        RenderScene sci = sc;
+        DevBuf<uint32_t> scr, mt;
+        if (cfg_.sampler == MPSS_SAMPLER_REFERENCE && !scene_.lights.empty()) {  // IrradianceTask streams
+            const int T = replay_irradiance_tasks(n, std::max(1, cfg_.replay_cores));
+            scr.alloc((size_t)n * scene_.lights.size() * 2);
+            mt.alloc((size_t)624 * T);
+            hipLaunchKernelGGL(replay_irradiance_kernel, dim3((T + 63) / 64), dim3(64), 0, 0, n,
+                               (int)scene_.lights.size(), T, mt.ptr, scr.ptr);
+            MPSS_HIP(hipGetLastError());
+            sci.irr_scr = scr.ptr;
+        }
         hipEvent_t ev{};
         time_begin(cfg_.kernel_timing != 0, 0, ev);
-        hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sc, dp.ptr, dn.ptr, de.ptr,
+        hipLaunchKernelGGL(irradiance_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, sci, dp.ptr, dn.ptr, de.ptr,
                            dm.ptr, duv.ptr, n, seed, dE.ptr);
         MPSS_HIP(hipGetLastError());
         time_end(cfg_.kernel_timing != 0, 0, ev, 0, timed_);
@@ -470,6 +486,40 @@ void Context::find_poisson_points(uint32_t seed) {
 // list) -> ONE sharded Mo() gather per BSSRDF material over the batch's hits -> film kernel per
 // piece. Calls on different streams may overlap: each takes its own workspace (RenderWorkspace),
 // and the scene, materials and octree are only read after the context lock is released.
+// The reference sampler's values over the whole sample extent at `spp` (replay_render_kernel),
+// rebuilt when spp or the scene changes. mu_ held; synchronous, so every stream sees the table.
+void Context::ensure_replay_table(int spp) {
+    if (replay_spp_ == spp && replay_vals_.ptr) return;
+    const int W = scene_.camera.xres, H = scene_.camera.yres;
+    const int T = replay_render_tasks(W, H, std::max(1, cfg_.replay_cores));
+    MPSS_HIP(hipDeviceSynchronize());  // no render may still read the old table
+    replay_vals_.alloc((size_t)(W + 1) * (H + 1) * spp * replay_k_);
+    DevBuf<uint32_t> mt;
+    mt.alloc((size_t)624 * T);
+    RenderScene sc = render_scene();
+    ReplayGen g{T, spp, replay_k_, (cfg_.max_depth > 0 && !cfg_.show_irradiance_points) ? kReplayLiDraws : 0, mt.ptr,
+                replay_vals_.ptr};
+    hipLaunchKernelGGL(replay_render_kernel, dim3((T + 63) / 64), dim3(64), 0, 0, sc, g);
+    MPSS_HIP(hipGetLastError());
+    MPSS_HIP(hipDeviceSynchronize());
+    replay_spp_ = spp;
+}
+
+void Context::replay_samples(int spp, float *out, uint64_t *n_floats, int *k) {
+    activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (cfg_.sampler != MPSS_SAMPLER_REFERENCE) throw Error(MPSS_ERR_INVALID, "replay_samples: the context uses the hash sampler");
+    if (scene_dirty_) upload_scene();
+    const int W = scene_.camera.xres, H = scene_.camera.yres;
+    if (W <= 0) throw Error(MPSS_ERR_INVALID, "replay_samples: no camera");
+    spp = round_up_pow2(spp);
+    *k = replay_k_;
+    *n_floats = (uint64_t)(W + 1) * (H + 1) * spp * replay_k_;
+    if (!out) return;
+    ensure_replay_table(spp);
+    MPSS_HIP(hipMemcpy(out, replay_vals_.ptr, sizeof(float) * *n_floats, hipMemcpyDeviceToHost));
+}
+
 void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs,
                            hipStream_t stream) {
     activate();
@@ -478,6 +528,12 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "render_tile: no camera");
     if (spp < 1 || spp > 65535) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be in [1, 65535]");
+    const bool replay = cfg_.sampler == MPSS_SAMPLER_REFERENCE;
+    if (replay) {
+        spp = round_up_pow2(spp);  // LDSampler rounds pixelsamples up (lowdiscrepancy.cpp:45-49)
+        if (spp > 32768) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be at most 32768 for the replay sampler");
+        ensure_replay_table(spp);
+    }
     for (int i = 0; i < n; ++i) {
         const int32_t *r = rects + 4 * i;
         if (r[0] < 0 || r[2] < 0 || r[1] > W || r[3] > H || r[0] >= r[1] || r[2] >= r[3])
@@ -497,6 +553,12 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             if (!materials_[i]->dipole) sss.push_back(SssMat{(int)i, materials_[i].get(), &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
     sc.have_octree = sss.empty() ? 0 : 1;
+    if (replay) {
+        sc.replay = replay_vals_.ptr;
+        sc.replay_k = replay_k_;
+        sc.replay_w = W + 1;
+        sc.replay_spp = spp;
+    }
     const bool timing = cfg_.kernel_timing != 0, counting = cfg_.count_traversal != 0;
     if (counting && !d_counts_.ptr) {
         d_counts_.alloc(kStatStride * kGroups);

@@ -41,7 +41,10 @@ class Config(C.Structure):
                 ("min_sample_distance", C.c_float), ("mix", C.c_float), ("show_irradiance_points", C.c_int),
                 ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
-                ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int)]
+                ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int), ("sampler", C.c_int),
+                ("replay_cores", C.c_int)]
+
+SAMPLER_HASH, SAMPLER_REFERENCE = 0, 1
 
 
 class RenderStats(C.Structure):
@@ -102,6 +105,7 @@ _sig("mpss_set_camera", C.c_int, [vp, f32p, f32p, C.c_int, C.c_int])
 _sig("mpss_set_surface_points", C.c_int, [vp, u32, vp])
 _sig("mpss_get_surface_points", C.c_int, [vp, vp, u32p])
 _sig("mpss_get_irradiance", C.c_int, [vp, vp, u32p])
+_sig("mpss_replay_samples", C.c_int, [vp, C.c_int, vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int)])
 _sig("mpss_load_pointsfile", C.c_int, [vp, C.c_char_p])
 _sig("mpss_save_pointsfile", C.c_int, [vp, C.c_char_p])
 _sig("mpss_preprocess", C.c_int, [vp, u32])
@@ -444,6 +448,14 @@ class Context:
         check(_lib.mpss_mc_profile(self.h, lay, len(lay), mfp_range, nsegments, nphotons, seed, r.ctypes.data,
                                    t.ctypes.data, C.byref(tr), C.byref(tt), C.byref(ev), stream))
         return dict(reflectance=r, transmittance=t, total_r=tr.value, total_t=tt.value, events=ev.value)
+
+    def replay_samples(self, spp, xres, yres):
+        """The reference sampler's values over the sample extent: (yres+1, xres+1, spp', K) float32."""
+        n, k = C.c_uint64(), C.c_int()
+        check(_lib.mpss_replay_samples(self.h, spp, None, C.byref(n), C.byref(k)))
+        out = np.zeros(n.value, np.float32)
+        check(_lib.mpss_replay_samples(self.h, spp, out.ctypes.data, C.byref(n), C.byref(k)))
+        return out.reshape(yres + 1, xres + 1, -1, k.value)
 
     def irradiance(self):
         n = C.c_uint32()

@@ -50,6 +50,11 @@ def _lib():
     L.o_imagemap_lookup.restype = C.c_int
     L.o_imagemap_lookup.argtypes = [C.c_int, C.c_int, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
                                     C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, f32p, f32p]
+    L.o_replay_render_table.restype = C.c_int
+    L.o_replay_render_table.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    L.o_replay_irradiance_scr.argtypes = [C.c_int, C.c_int, C.c_int, vp]
+    L.o_irradiance_replay.argtypes = [vp, C.c_int, vp, vp, C.c_int, f32p]
+    L.o_render_tile_replay.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p]
     L._render_sigs = True
     return L
 
@@ -186,6 +191,30 @@ class OracleScene:
         E = np.zeros((len(pts), NB), np.float32)
         _lib().o_irradiance(self.h, len(pts), pts.ctypes.data, seed, nthreads or os.cpu_count(), E)
         return E
+
+    # ---- the reference sampler (oracle/render.c o_replay_*)
+    def replay_table(self, spp, cores=8, li_draws=6, nthreads=None):
+        """Sample values of the whole sample extent: (yres+1, xres+1, spp, K) float32."""
+        L = _lib()
+        K = L.o_replay_render_table(self.h, spp, cores, li_draws, 1, None)
+        vals = np.zeros((self.sc.yres + 1, self.sc.xres + 1, spp, K), np.float32)
+        L.o_replay_render_table(self.h, spp, cores, li_draws, nthreads or os.cpu_count(), vals.ctypes.data)
+        return vals
+
+    def irradiance_replay(self, pts, cores=8, nthreads=None):
+        pts = np.ascontiguousarray(pts, SURFACE_POINT)
+        scr = np.zeros((len(pts), max(1, len(self.sc.lights)), 2), np.uint32)
+        _lib().o_replay_irradiance_scr(len(pts), len(self.sc.lights), cores, scr.ctypes.data)
+        E = np.zeros((len(pts), NB), np.float32)
+        _lib().o_irradiance_replay(self.h, len(pts), pts.ctypes.data, scr.ctypes.data, nthreads or os.cpu_count(), E)
+        return E
+
+    def render_tile_replay(self, spp, vals, x0, x1, y0, y1, nthreads=None):
+        vals = np.ascontiguousarray(vals, np.float32)
+        out = np.zeros(((y1 - y0) * (x1 - x0) * 4,), np.float32)
+        _lib().o_render_tile_replay(self.h, spp, vals.ctypes.data, vals.shape[-1], x0, x1, y0, y1,
+                                    nthreads or os.cpu_count(), out)
+        return out.reshape(y1 - y0, x1 - x0, 4)
 
     def set_octree(self, pts, E):
         p = np.ascontiguousarray(pts["p"], np.float32)

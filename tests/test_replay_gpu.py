@@ -1,0 +1,104 @@
+"""The reference sampler replayed on the GPU (mpss_config.sampler = MPSS_SAMPLER_REFERENCE; row a16)
+against the oracle's restatement of the same loop (oracle/render.c o_replay_*, itself checked
+against a pure-Python restatement in test_sampler_replay.py).
+
+  sample table     bit-exact: every task's MT19937 stream, LDPixelSample scrambles and shuffles,
+                   and the 6 Li draws per camera hit (the GPU's hit tests are the render kernels'
+                   own BVH traversal, bit-identical to the oracle's)
+  irradiance       IrradianceTask's RNG(47 k) scrambles: rel 1e-5, >= 99 % bit-identical (as the
+                   hash-sampler irradiance parity)
+  film             render parity tolerance (test_render_parity_gpu._check); any tiling renders
+                   the same film bit for bit, and another emulated core count another film
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_render as orr
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _scene(name, lights=None, W=40, H=32, spp=4):
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", name), xres=W, yres=H, spp=spp)
+    sc.integrator["minsampledistance"] = 0.008
+    for m in sc.materials:
+        m["desired_length"] = 64
+    if lights == "sky+area":
+        from test_render_parity_gpu import _sky_light
+        sc.lights = [sc.lights[0], _sky_light(40, [1, 1, 0], ns=2)]
+    return sc
+
+
+def _pair(mpss, sc, cores=8):
+    import torch
+    assert torch.cuda.is_available()
+    from mpss import pbrtscene
+    ctx = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=cores)
+    ctx.preprocess(seed=0)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    return torch, ctx, o
+
+
+def _render(torch, ctx, sc, rects):
+    img = np.zeros((sc.yres, sc.xres, 4), np.float32)
+    for (x0, x1, y0, y1) in rects:
+        out = torch.zeros(((y1 - y0) * (x1 - x0) * 4,), dtype=torch.float32, device="cuda")
+        ctx.render_tile(sc.spp, 0, x0, x1, y0, y1, out.data_ptr())
+        torch.cuda.synchronize()
+        img[y0:y1, x0:x1] = out.cpu().numpy().reshape(y1 - y0, x1 - x0, 4)
+    return img
+
+
+@pytest.mark.parametrize("name,lights,cores", [("skin.pbrt", None, 8), ("skin.pbrt", "sky+area", 8),
+                                               ("tissue.pbrt", None, 2)])
+def test_replay_table_bit_exact(mpss, oracle, name, lights, cores):
+    sc = _scene(name, lights)
+    torch, ctx, o = _pair(mpss, sc, cores)
+    got = ctx.replay_samples(sc.spp, sc.xres, sc.yres)
+    ref = o.replay_table(sc.spp, cores=cores, li_draws=6)
+    assert got.shape == ref.shape
+    bad = np.argwhere(np.any(got != ref, axis=(2, 3)))
+    assert len(bad) == 0, "first differing pixels (y, x): %s" % bad[:5].tolist()
+    ctx.close()
+
+
+@pytest.mark.parametrize("name,lights", [("skin.pbrt", None), ("skin.pbrt", "sky+area")])
+def test_replay_irradiance_and_image(mpss, oracle, name, lights):
+    from test_render_parity_gpu import _check
+    sc = _scene(name, lights)
+    torch, ctx, o = _pair(mpss, sc)
+    pts = ctx.surface_points()
+    E = o.irradiance_replay(pts, cores=8)
+    got_E = ctx.irradiance()
+    np.testing.assert_allclose(got_E, E, rtol=1e-5, atol=1e-6 * float(E.max()))
+    assert (got_E == E).mean() >= 0.99
+    o.set_octree(pts, E)
+    vals = o.replay_table(sc.spp, cores=8, li_draws=6)
+    ref = o.render_tile_replay(sc.spp, vals, 0, sc.xres, 0, sc.yres)
+    full = _render(torch, ctx, sc, [(0, sc.xres, 0, sc.yres)])
+    _check(full, ref)
+    tiles = [(x, min(x + 13, sc.xres), y, min(y + 11, sc.yres)) for y in range(0, sc.yres, 11)
+             for x in range(0, sc.xres, 13)]
+    assert np.array_equal(_render(torch, ctx, sc, tiles), full)
+    ctx.close()
+
+
+def test_replay_depends_on_core_count_and_not_on_seed(mpss):
+    import torch
+    from mpss import pbrtscene
+    sc = _scene("skin.pbrt")
+    imgs = []
+    for cores in (8, 8, 16):
+        ctx = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=cores)
+        ctx.preprocess(seed=len(imgs))  # seeds are ignored by the replay sampler
+        out = torch.zeros((sc.yres * sc.xres * 4,), dtype=torch.float32, device="cuda")
+        ctx.render_tile(sc.spp, 77 * len(imgs), 0, sc.xres, 0, sc.yres, out.data_ptr())
+        torch.cuda.synchronize()
+        imgs.append(out.cpu().numpy())
+        ctx.close()
+    assert np.array_equal(imgs[0], imgs[1])
+    assert not np.array_equal(imgs[0], imgs[2])
