@@ -82,6 +82,8 @@ def parse(argv=None):
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None, help="tile size (default 128 on one GPU, 64 on several)")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--batch-log2", type=int, default=None,
+                    help="camera samples per render batch, log2 (mpss_config.max_batch_samples; default 2^24)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 weak-scaling figure at N > 1")
@@ -129,7 +131,8 @@ def build_scene(a, label_cfg, local):
         pts = pbrtscene.mesh_points(sc)
         sc.meshes = [pbrtscene.subdivide_mesh(me, subdiv) for me in sc.meshes]
     t0 = time.perf_counter()
-    ctx = pbrtscene.build_context(sc, device=local)
+    kw = {} if a.batch_log2 is None else {"max_batch_samples": 1 << a.batch_log2}
+    ctx = pbrtscene.build_context(sc, device=local, **kw)
     t_mat = time.perf_counter() - t0
     if pts is not None:
         ctx.set_surface_points(pts)

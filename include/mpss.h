@@ -69,9 +69,10 @@ typedef struct {
     int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
     int profile_on_host;       /* 1: build LayeredSkin profiles and rho_hd tables on the host CPU
                                   (threads); 0 (default): on the GPU (profile_gpu.hip, rho_gpu.hip) */
-    int64_t max_batch_samples; /* camera samples per render batch; the workspace is sized for the
-                                  worst case (every sample a hit): ~280 B/sample, 4.7 GB at the
-                                  default 1 << 24 */
+    int64_t max_batch_samples; /* camera samples per render batch (default 1 << 26: a whole C2 frame
+                                  in two batches, one Mo() launch each); the workspace grows to the
+                                  largest batch rendered, sized for the worst case (every sample a
+                                  hit): ~280 B/sample, 18.8 GB for a full 2^26 batch of the 288 GB */
     int use_poisson_point_finder; /* "usepoissonpointfinder" = false: SurfacePoints by random-walk
                                   dart throwing (FindPoissonPointDistribution) instead of tessellation */
     int sampler;               /* MPSS_SAMPLER_HASH (default): counter-hash scrambled (0,2) sequences, a

@@ -142,13 +142,16 @@ struct BandLane {
 // global_load_dwordx2), NEAR 2: one flat load whose per-lane address is in LDS or in the table.
 // The L2 request rate is what bounds the gather (profiles/r02b_pmc.json), and only lanes outside
 // the near field make requests.
-template <bool POINT, bool COUNT, int KLDS, int NEAR>
-__device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ table, const BandLane &b, float d2,
-                                                   const float e[4], float w, f2v acc[2], int hist[4]) {
+// The fetch half: f per band and the four pair loads (issued, not consumed).
+template <bool COUNT, int KLDS, int NEAR>
+__device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, const BandLane &b, float d2, float f[4],
+                                              RdPair v[4], int hist[4]) {
     const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
     const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
-    const float f[4] = {f01.x, f01.y, f23.x, f23.y};
-    RdPair v[4];
+    f[0] = f01.x;
+    f[1] = f01.y;
+    f[2] = f23.x;
+    f[3] = f23.y;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t s = (uint32_t)f[j];  // saturating convert: f >= 2^32 -> 0xffffffff >= lm1
@@ -156,6 +159,21 @@ __device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ tab
         if (KLDS > 0 && NEAR == 2) {
             const float *src = s < b.klim ? b.lt + j * (KLDS + 2) + s : table + idx;
             v[j] = *reinterpret_cast<const RdPair *>(src);
+        } else if (KLDS > 0 && NEAR == 4) {
+            // LDS and L2 loads into separate registers, then a select: the two masked loads do not
+            // write the same VGPRs, so neither waits for the other (NEAR 1 serializes on that WAW)
+            const bool near = s < b.klim;
+            RdPair g{0.f, 0.f}, l{0.f, 0.f};
+            if (!near) g = *reinterpret_cast<const RdPair *>(table + idx);
+            if (near) {
+                const lds_float *row = (const lds_float *)b.lt + j * (KLDS + 2) + s;
+                l.a = row[0];
+                l.b = row[1];
+            }
+            // exactly one of g, l is the (zero-initialized) other path's: the sum is the loaded pair
+            // (table entries are never -0), and it needs both registers live, so they stay apart
+            v[j].a = g.a + l.a;
+            v[j].b = g.b + l.b;
         } else if (KLDS > 0) {
             if (s < b.klim) {
                 const lds_float *row = (const lds_float *)b.lt + j * (KLDS + 2) + s;
@@ -177,6 +195,12 @@ __device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ tab
             hist[3] += s < 16384u;
         }
     }
+}
+
+// The combine half: lerp, the Mo() products and the running sums (one point or node).
+template <bool POINT>
+__device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
+                                                f2v acc[2]) {
     float rd[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -190,6 +214,15 @@ __device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ tab
         if (POINT) val = val * f2v{w, w};
         acc[h] += val;
     }
+}
+
+template <bool POINT, bool COUNT, int KLDS, int NEAR>
+__device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ table, const BandLane &b, float d2,
+                                                   const float e[4], float w, f2v acc[2], int hist[4]) {
+    float f[4];
+    RdPair v[4];
+    band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2, f, v, hist);
+    band_rd_combine<POINT>(f, v, e, w, acc);
 }
 
 // sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d)
@@ -207,7 +240,10 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 
 // COUNT: k_nodes / k_pts = this lane's node / point visits; w_nodes / w_pts = the wave's node-loop
 // and point-loop iterations (uniform).
-template <bool COUNT, int KLDS, int NEAR>
+// PAIR: a leaf's points two at a time -- both points' eight pair loads issued before either's
+// terms are formed (the same terms, summed in the same order), so a wave waits out one L2 round
+// trip per two points.
+template <bool COUNT, int KLDS, int NEAR, bool PAIR>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
                                                  int hist[4], const float *lt) {
@@ -269,7 +305,27 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 f2v lacc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
                 const int live = (int)h.pad;
                 if (COUNT) w_pts += live;
-                for (int i = 0; i < live; ++i) {
+                int i0 = 0;
+                if (PAIR)
+                    for (; i0 + 1 < live; i0 += 2) {
+                        const int ka = h.leaf_first + i0, kb = ka + 1;
+                        const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];
+                        const float4 ea = e_g[ka], eb = e_g[kb];
+                        if (!open) continue;
+                        if (COUNT) k_pts += 2;
+                        const float ax = px - pa.x, ay = py - pa.y, az = pz - pa.z;
+                        const float bx2 = px - pb.x, by2 = py - pb.y, bz2 = pz - pb.z;
+                        const float d2a = ax * ax + ay * ay + az * az;
+                        const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
+                        float fa[4], fb[4];
+                        RdPair va[4], vb[4];
+                        band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2a, fa, va, hist);
+                        band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2b, fb, vb, hist);
+                        const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
+                        band_rd_combine<true>(fa, va, e0, pa.w, lacc);
+                        band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
+                    }
+                for (int i = i0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
                     const float4 ph = pt_hdr[kp];
                     if (!open) continue;

@@ -258,7 +258,7 @@ __device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, 
     return true;
 }
 
-template <bool COUNT, int BS, int KLDS, int NEAR>
+template <bool COUNT, int BS, int KLDS, int NEAR, bool PAIR>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_kernel(BandArgs a) {
     __shared__ unsigned long long keys[BS];
     __shared__ int chunk_s;
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         if (live) band_query(a, q, px, py, pz);
         float acc[4];
         int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, NEAR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        mo_band_traverse<COUNT, KLDS, NEAR, PAIR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
         if (live) {
             if (a.out4) {
                 a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -336,23 +336,28 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 }
 
 // Gather variant (tuning knobs; default 1024-query chunks, a 4096-entry near field read by
-// flat loads): MPSS_MO_BS = 1024 | 512, MPSS_MO_K = LDS entries per band (0, 2048, 4096, 9216),
-// MPSS_MO_NEAR = 1 (masked ds/global loads) | 2 (flat loads) | 3 (no near field, no request past
-// the profile end), MPSS_MO_SORT = 0 (no Morton sort). Measured on C2 (profiles/r02_variants.txt):
-// flat 4096 120 ms/frame, masked 4096 121, no near field 127, 512-query chunks 124-126, the
-// 9216-entry near field (one workgroup per CU) 140, no sort 128 (lane efficiency 0.47 vs 0.60).
+// flat loads, a leaf's points two at a time): MPSS_MO_BS = 1024 | 512, MPSS_MO_K = LDS entries
+// per band (0, 2048, 4096, 9216), MPSS_MO_NEAR = 1 (masked ds/global loads into the same VGPRs:
+// every pair waits out the other) | 2 (flat loads) | 3 (no near field, no request past the
+// profile end) | 4 (masked ds/global loads into separate VGPRs), MPSS_MO_PAIR = 0 | 1,
+// MPSS_MO_SORT = 0 (no Morton sort). Measured on C2 (profiles/r02_variants.txt): flat 4096
+// 120 ms/frame, masked 4096 121, no near field 127, 512-query chunks 124-126, the 9216-entry near
+// field (one workgroup per CU) 140, no sort 128 (lane efficiency 0.47 vs 0.60); round 2e
+// (profiles/r02j_variants.txt, Msamples/s): flat 4096 544, + point pairs 550, + 2^26-sample
+// batches 568; no near field with pairs 467; separate-VGPR masked loads 542; 9216 with pairs 479.
 struct BandVariant {
-    int bs, k, near;
+    int bs, k, near, pair;
 };
 BandVariant band_variant() {
-    BandVariant v{1024, 4096, 2};
+    BandVariant v{1024, 4096, 2, 1};
     if (const char *e = getenv("MPSS_MO_BS")) v.bs = atoi(e);
     if (const char *e = getenv("MPSS_MO_K")) v.k = atoi(e);
     if (const char *e = getenv("MPSS_MO_NEAR")) v.near = atoi(e);
+    if (const char *e = getenv("MPSS_MO_PAIR")) v.pair = atoi(e);
     return v;
 }
 
-template <int BS, int KLDS, int NEAR>
+template <int BS, int KLDS, int NEAR, bool PAIR = false>
 void launch_band_v(const BandArgs &a, int nq_max, bool count, hipStream_t stream) {
     // persistent grid: enough resident workgroups per XCD (32 CUs) to fill it; late ones find no work
     const int chunks = (nq_max + BS - 1) / BS;
@@ -361,9 +366,9 @@ void launch_band_v(const BandArgs &a, int nq_max, bool count, hipStream_t stream
     if (per_group <= 0) return;
     const dim3 grid((unsigned)(per_group * kGroups));
     if (count)
-        hipLaunchKernelGGL((mo_band_kernel<true, BS, KLDS, NEAR>), grid, dim3(BS), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_kernel<true, BS, KLDS, NEAR, PAIR>), grid, dim3(BS), 0, stream, a);
     else
-        hipLaunchKernelGGL((mo_band_kernel<false, BS, KLDS, NEAR>), grid, dim3(BS), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_kernel<false, BS, KLDS, NEAR, PAIR>), grid, dim3(BS), 0, stream, a);
 }
 
 void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipStream_t stream) {
@@ -377,7 +382,17 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
     const BandVariant v = band_variant();
     const char *so = getenv("MPSS_MO_SORT");
     a.sort = so ? atoi(so) : 1;
-    if (v.bs == 1024 && v.k == 0 && v.near == 3)
+    if (v.pair && v.k == 0)
+        launch_band_v<1024, 0, 0, true>(a, nq_max, count, stream);
+    else if (v.pair && v.k == 9216)
+        launch_band_v<1024, 9216, 2, true>(a, nq_max, count, stream);
+    else if (v.pair && v.near == 4)
+        launch_band_v<1024, 4096, 4, true>(a, nq_max, count, stream);
+    else if (v.near == 4)
+        launch_band_v<1024, 4096, 4, false>(a, nq_max, count, stream);
+    else if (v.pair)
+        launch_band_v<1024, 4096, 2, true>(a, nq_max, count, stream);
+    else if (v.bs == 1024 && v.k == 0 && v.near == 3)
         launch_band_v<1024, 0, 3>(a, nq_max, count, stream);
     else if (v.bs == 1024 && v.k == 0)
         launch_band_v<1024, 0, 0>(a, nq_max, count, stream);

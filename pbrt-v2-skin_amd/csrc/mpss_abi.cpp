@@ -61,7 +61,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->kernel_timing = 0;
     c->count_traversal = 0;
     c->profile_on_host = 0;
-    c->max_batch_samples = (int64_t)1 << 24;
+    c->max_batch_samples = (int64_t)1 << 26;
     c->use_poisson_point_finder = 0;
     c->sampler = MPSS_SAMPLER_HASH;
     c->replay_cores = 8;

@@ -49,7 +49,7 @@ def test_kissfft_real2d_roundtrip(oracle):
 
 
 def _test_cpp_layers():
-    # src/multipole/test/test.cpp:84-116 layer specs (mua, musp', d, eta)
+    # src/multipole/test/test.cpp:84-116 layer specs (ior, thickness d, mua, musp')
     return [(1.4, 0.025, 0.268088, 19.4879), (1.4, 2.0, 0.268088, 9.74395)]
 
 
