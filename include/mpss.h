@@ -85,6 +85,9 @@ typedef struct {
                                   rounded up to a power of two as LDSampler does */
     int replay_cores;          /* NumSystemCores() of the reference run being replayed (its task
                                   counts, samplerrenderer.cpp:207, multipolesubsurface.cpp:198) = 8 */
+    int octree_on_host;        /* 1: build the irradiance octree on the host (serial Insert in point
+                                  order, octree.cpp); 0 (default): level-synchronous build on the GPU
+                                  (octree_gpu.hip), the same tree bit for bit */
 } mpss_config;
 
 enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };
@@ -166,6 +169,12 @@ int mpss_set_irradiance_points(mpss_ctx *ctx, uint32_t n, const float *p, const 
                                const float *area);
 /* Octree statistics: node count, max depth, point count. */
 int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint32_t *n_points);
+/* The context's device octree as the gather reads it (any pointer may be null): nodes n_nodes x 64 B
+ * (pre-order NodeHdr records: centroid, sumArea, box, skip, leaf range, depth, flags, live point
+ * count), node_et n_nodes x 32 floats (30 bands + 2 zero pads), pt_hdr n_points x 4 floats {p, area;
+ * sign bit: black E}, pt_e n_points x 32 floats, pt_index n_points original point indices (each
+ * leaf's non-black points first). Sizes from mpss_octree_info. Synchronous. */
+int mpss_octree_export(mpss_ctx *ctx, void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index);
 
 /* Mo for q shading points (p_dev: q*3 floats) with material's Rd profile; mo_dev: q*30 floats.
  * counters_dev (nullable): q*4 int32 {nodes entered, leaf points evaluated} by the reference

@@ -298,11 +298,44 @@ void Context::set_irradiance_points(int n, const float *p, const float *nrm, con
 
 // SubsurfaceOctreeNode::Insert / InitHierarchy over the points, the device copy and every
 // material's band layout (mu_ held).
-void Context::build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area) {
-    build_octree(n, p, nrm, E, area, host_octree_);
-    dev_octree_.upload(host_octree_);
+void Context::build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area,
+                                  const float *dp, const float *dn, const float *dE) {
+    have_octree_ = false;
+    if (cfg_.octree_on_host) {
+        FlatOctree host;
+        build_octree(n, p, nrm, E, area, host);
+        dev_octree_.upload(host);
+    } else {
+        if (n <= 0) throw Error(-1, "build_octree: no irradiance points");
+        float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = 0; i < n; ++i)  // Union(BBox, Point), core/geometry.cpp:38-47
+            for (int k = 0; k < 3; ++k) {
+                const float v = p[3 * (size_t)i + k];
+                bmin[k] = (v < bmin[k]) ? v : bmin[k];
+                bmax[k] = (bmax[k] < v) ? v : bmax[k];
+            }
+        DevBuf<float> up, un, uE, uA;
+        if (!dp) up.upload(p, 3 * (size_t)n);
+        if (!dn) un.upload(nrm, 3 * (size_t)n);
+        if (!dE) uE.upload(E, (size_t)n * NB);
+        uA.upload(area, n);
+        build_octree_device(n, dp ? dp : up.ptr, dn ? dn : un.ptr, dE ? dE : uE.ptr, uA.ptr, bmin, bmax, dev_octree_);
+    }
     have_octree_ = true;
     ensure_layouts();
+}
+
+void Context::export_octree(void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index) {
+    activate();
+    std::lock_guard<std::mutex> g(mu_);
+    if (!have_octree_) throw Error(MPSS_ERR_INVALID, "no irradiance points: call mpss_set_irradiance_points first");
+    const DeviceOctree &t = dev_octree_;
+    MPSS_HIP(hipDeviceSynchronize());
+    if (nodes) MPSS_HIP(hipMemcpy(nodes, t.nodes.ptr, sizeof(NodeHdr) * t.n_nodes, hipMemcpyDeviceToHost));
+    if (node_et) MPSS_HIP(hipMemcpy(node_et, t.node_et.ptr, sizeof(float) * ROW * t.n_nodes, hipMemcpyDeviceToHost));
+    if (pt_hdr) MPSS_HIP(hipMemcpy(pt_hdr, t.pt_hdr.ptr, sizeof(float4) * t.n_points, hipMemcpyDeviceToHost));
+    if (pt_e) MPSS_HIP(hipMemcpy(pt_e, t.pt_e.ptr, sizeof(float) * ROW * t.n_points, hipMemcpyDeviceToHost));
+    if (pt_index) MPSS_HIP(hipMemcpy(pt_index, t.pt_index.ptr, sizeof(int) * t.n_points, hipMemcpyDeviceToHost));
 }
 
 const DeviceOctree &Context::octree() const {

@@ -86,6 +86,7 @@ public:
     const Material &material(uint32_t id) const;
     void set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area);
     const DeviceOctree &octree() const;
+    void export_octree(void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index);
     uint32_t add_imagemap(const mpss_imagemap &m);
     void set_material_textures(uint32_t material, int albedo, int bump);
     std::vector<const TexView *> host_bump_views() const;
@@ -154,7 +155,10 @@ private:
     void release_ws(RenderWorkspace *ws, hipStream_t stream);
     // every BSSRDF material's band layout exists on the device octree (mu_ held)
     void ensure_layouts();
-    void build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area);
+    // p, nrm, E, area: host arrays; dp / dn / dE (nullable): the same on the device, when the caller
+    // has them there already (Preprocess)
+    void build_octree_locked(int n, const float *p, const float *nrm, const float *E, const float *area,
+                             const float *dp = nullptr, const float *dn = nullptr, const float *dE = nullptr);
     // serializes everything that changes the context (scene, materials, octree, stats) and the
     // workspace pool; launches happen outside it
     mutable std::mutex mu_;
@@ -171,7 +175,7 @@ private:
     mpss_config cfg_;
     float max_error_, min_dist_;
     std::vector<std::unique_ptr<Material>> materials_;
-    FlatOctree host_octree_;
+
     DeviceOctree dev_octree_;
     bool have_octree_ = false;
 };

@@ -21,6 +21,7 @@ struct DeviceOctree {
     DevBuf<float> node_et;
     DevBuf<float4> pt_hdr;
     DevBuf<float> pt_e;
+    DevBuf<int> pt_index;  // original point index of every point slot
     int n_nodes = 0, n_points = 0, max_depth = 0;
     float bmin[3] = {0.f, 0.f, 0.f}, bmax[3] = {0.f, 0.f, 0.f};  // root bounds (query sort keys)
     // one group-major layout per distinct band grouping in use; built eagerly and synchronously
@@ -31,6 +32,12 @@ struct DeviceOctree {
     // builds the layout if it is missing (synchronizes the device); the caller serializes calls
     const BandLayout &ensure_layout(const BandGroups &g);
 };
+
+// SubsurfaceOctreeNode::Insert + InitHierarchy on the device (octree_gpu.hip): the tree of the host
+// build (octree.cpp) + DeviceOctree::upload, bit for bit. P, N: n x 3, E: n x NB, A: n device floats;
+// bmin / bmax: the points' bounds (Union of the points in index order). Synchronous.
+void build_octree_device(int n, const float *P, const float *N, const float *E, const float *A, const float bmin[3],
+                         const float bmax[3], DeviceOctree &t);
 
 struct DeviceProfile {
     DevBuf<float> table;  // [NB][L] channel-major + 2 trailing zeros

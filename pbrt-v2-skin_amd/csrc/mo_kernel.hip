@@ -473,6 +473,7 @@ void launch_exact(const MoArgs &a, int max_depth, bool count, hipStream_t s) {
 void DeviceOctree::upload(const FlatOctree &t) {
     std::vector<NodeHdr> hdr = t.hdr;
     std::vector<float> ph(t.pt_hdr.size()), pe(t.pt_e.size());
+    std::vector<int> pidx(t.pt_index.size());
     for (NodeHdr &h : hdr) {
         h.pad = 0;
         if (h.leaf_first < 0) continue;
@@ -484,6 +485,7 @@ void DeviceOctree::upload(const FlatOctree &t) {
                 if (blk != (pass == 1)) continue;
                 memcpy(&ph[4 * (size_t)o], &t.pt_hdr[4 * k], 4 * sizeof(float));
                 memcpy(&pe[(size_t)o * ROW], &t.pt_e[k * ROW], ROW * sizeof(float));
+                pidx[o] = t.pt_index[k];
                 ++o;
                 if (pass == 0) ++h.pad;
             }
@@ -493,6 +495,7 @@ void DeviceOctree::upload(const FlatOctree &t) {
     node_et.upload(t.node_et.data(), t.node_et.size());
     pt_hdr.upload(reinterpret_cast<const float4 *>(ph.data()), ph.size() / 4);
     pt_e.upload(pe.data(), pe.size());
+    pt_index.upload(pidx.data(), pidx.size());
     n_nodes = (int)t.hdr.size();
     n_points = (int)t.pt_index.size();
     max_depth = t.max_depth;

@@ -42,9 +42,10 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 5; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 6; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
-                                          // 5: reference-sampler replay, dipole materials
+                                          // 5: reference-sampler replay, dipole materials;
+                                          // 6: GPU octree build (octree_on_host), mpss_octree_export
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -65,6 +66,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->use_poisson_point_finder = 0;
     c->sampler = MPSS_SAMPLER_HASH;
     c->replay_cores = 8;
+    c->octree_on_host = 0;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -179,6 +181,13 @@ int mpss_octree_info(mpss_ctx *c, uint32_t *nn, uint32_t *md, uint32_t *np) {
         if (nn) *nn = (uint32_t)t.n_nodes;
         if (md) *md = (uint32_t)t.max_depth;
         if (np) *np = (uint32_t)t.n_points;
+    });
+}
+
+int mpss_octree_export(mpss_ctx *c, void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index) {
+    return guarded([&] {
+        require(c, "mpss_octree_export: null ctx");
+        reinterpret_cast<Context *>(c)->export_octree(nodes, node_et, pt_hdr, pt_e, pt_index);
     });
 }
 

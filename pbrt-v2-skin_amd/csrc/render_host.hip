@@ -373,7 +373,9 @@ void Context::preprocess(uint32_t seed) {
     }
     std::vector<float> area(n);
     for (int i = 0; i < n; ++i) area[i] = points_[i].area;
-    build_octree_locked(n, p.data(), nr.data(), irradiance_.data(), area.data());
+    const bool e_on_device = !cfg_.show_irradiance_points;  // dE holds the irradiance kernel's output
+    build_octree_locked(n, p.data(), nr.data(), irradiance_.data(), area.data(), dp.ptr, dn.ptr,
+                        e_on_device ? dE.ptr : nullptr);
 }
 
 // FindPoissonPointDistribution -> SurfacePointsRenderer::Render (renderers/surfacepoints.cpp:115-150)

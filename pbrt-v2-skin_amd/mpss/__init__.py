@@ -42,7 +42,7 @@ class Config(C.Structure):
                 ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
                 ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int), ("sampler", C.c_int),
-                ("replay_cores", C.c_int)]
+                ("replay_cores", C.c_int), ("octree_on_host", C.c_int)]
 
 SAMPLER_HASH, SAMPLER_REFERENCE = 0, 1
 
@@ -96,6 +96,7 @@ _sig("mpss_host_dipole_rd", C.c_int, [f32p, f32p, C.c_float, u32, vp, vp, vp])
 _sig("mpss_get_material_tables", C.c_int, [vp, u32, vp, u32p, vp, vp, u32p, vp])
 _sig("mpss_set_irradiance_points", C.c_int, [vp, u32, f32p, f32p, f32p, f32p])
 _sig("mpss_octree_info", C.c_int, [vp, u32p, u32p, u32p])
+_sig("mpss_octree_export", C.c_int, [vp, vp, vp, vp, vp, vp])
 _sig("mpss_mo_batch", C.c_int, [vp, u32, u32, vp, vp, vp, vp])
 _sig("mpss_add_mesh", C.c_int, [vp, u32, f32p, vp, vp, vp, u32, C.POINTER(C.c_int32), f32p, f32p, C.c_int, u32])
 _sig("mpss_add_sphere_light", C.c_int, [vp, f32p, C.c_float, f32p, C.c_int])
@@ -373,6 +374,18 @@ class Context:
         a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
         check(_lib.mpss_octree_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return dict(n_nodes=a.value, max_depth=b.value, n_points=c.value)
+
+    def octree_export(self):
+        """The device octree as the gather reads it (mpss_octree_export): nodes as raw 64-B records
+        (np.void), node_et [N, 32], pt_hdr [M, 4], pt_e [M, 32], pt_index [M]."""
+        info = self.octree_info()
+        N, M = info["n_nodes"], info["n_points"]
+        d = dict(nodes=np.zeros((N, 16), np.uint32), node_et=np.zeros((N, 32), np.float32),
+                 pt_hdr=np.zeros((M, 4), np.float32), pt_e=np.zeros((M, 32), np.float32),
+                 pt_index=np.zeros(M, np.int32))
+        check(_lib.mpss_octree_export(self.h, *[d[k].ctypes.data_as(vp) for k in
+                                                ("nodes", "node_et", "pt_hdr", "pt_e", "pt_index")]))
+        return d
 
     def mo_batch(self, mid, q, p_dev, mo_dev, counters_dev=None, stream=None):
         check(_lib.mpss_mo_batch(self.h, mid, q, p_dev, mo_dev, counters_dev, stream))
