@@ -116,6 +116,11 @@ typedef struct {
                              (ComputeMonteCarloProfile, multipole.cpp:298-368) on this context's GPU,
                              and Li uses Ft = 1 (multipolesubsurface.cpp:283-286) */
     uint64_t photons;     /* "photons" = 10000000 (per band) */
+    int rgb_profile;      /* "rgbprofile" = false: ComputeRGBMultipoleProfile (multipole.cpp:408-451) --
+                             the layers' 30-band mua / musp reduced to RGB (ToRGBSpectrum), three
+                             profiles, Rd(d^2) = FromRGB(reflectance) of the three lookups
+                             (multipole.cpp:85-107); the exported table then holds the R, G, B
+                             profiles in rows c % 3. Mo() runs the reference-order gather */
 } mpss_layeredskin;
 
 void mpss_layeredskin_defaults(mpss_layeredskin *m);

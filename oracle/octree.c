@@ -168,6 +168,7 @@ typedef struct {
     float max_error;
     long nodes, points;
     const o_diffusion *dip; /* non-NULL: DiffusionReflectance instead of the profile table */
+    int rgb;                /* rgbprofile: tab rows 0..2 are the R, G, B profiles */
 } mo_ctx;
 
 /* ---- DiffusionReflectance (diffusionutil.h:38-83) ---- */
@@ -234,6 +235,14 @@ static void rd_eval(const mo_ctx *m, float d2, float out[O_NB]) {
         o_diffusion_eval(m->dip, d2, out);
         return;
     }
+    if (m->rgb) {
+        /* MultipoleProfileData::reflectance with isRGBProfile (multipole.cpp:85-107):
+           Spectrum::FromRGBSpectrum(sampleRGBProfile(...)) = SampledSpectrum::FromRGB(rgb, reflectance) */
+        float rgb[3];
+        for (int k = 0; k < 3; ++k) rgb[k] = o_sample_profile(m->tab + (size_t)k * m->len, m->len, m->rcp[k], d2);
+        o_from_rgb(rgb, 0, out);
+        return;
+    }
     for (int c = 0; c < O_NB; ++c) out[c] = o_sample_profile(m->tab + (size_t)c * m->len, m->len, m->rcp[c], d2);
 }
 
@@ -288,6 +297,7 @@ typedef struct {
     int next;
     pthread_mutex_t mu;
     const o_diffusion *dip;
+    int rgb;
 } mo_job;
 
 static void *mo_worker(void *arg) {
@@ -300,7 +310,7 @@ static void *mo_worker(void *arg) {
         if (start >= j->q) break;
         int end = start + 256 < j->q ? start + 256 : j->q;
         for (int i = start; i < end; ++i) {
-            mo_ctx m = {j->t, j->tab, j->len, j->rcp, j->max_error, 0, 0, j->dip};
+            mo_ctx m = {j->t, j->tab, j->len, j->rcp, j->max_error, 0, 0, j->dip, j->rgb};
             mo_rec(&m, j->t->root, j->t->bmin, j->t->bmax, j->pts + 3 * (size_t)i, j->mo + (size_t)i * O_NB);
             if (j->nn) j->nn[i] = (int32_t)m.nodes;
             if (j->np) j->np[i] = (int32_t)m.points;
@@ -325,6 +335,15 @@ void o_mo_batch(const o_octree *t, int q, const float *pts, const float *tab, in
     memset(&j, 0, sizeof(j));
     j.t = t; j.q = q; j.pts = pts; j.tab = tab; j.rcp = rcp; j.len = len; j.max_error = max_error;
     j.mo = mo; j.nn = nn; j.np = np;
+    mo_run(&j, nthreads);
+}
+
+void o_mo_batch_rgb(const o_octree *t, int q, const float *pts, const float *tab, int len, const float rcp[3],
+                    float max_error, float *mo, int32_t *nn, int32_t *np, int nthreads) {
+    mo_job j;
+    memset(&j, 0, sizeof(j));
+    j.t = t; j.q = q; j.pts = pts; j.tab = tab; j.rcp = rcp; j.len = len; j.max_error = max_error;
+    j.mo = mo; j.nn = nn; j.np = np; j.rgb = 1;
     mo_run(&j, nthreads);
 }
 

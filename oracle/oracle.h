@@ -97,6 +97,10 @@ int o_octree_num_nodes(const o_octree *t);
 void o_mo_batch(const o_octree *t, int q, const float *pts /*q*3*/, const float *rd_table, int len,
                 const float rcp[O_NB], float max_error, float *mo /*q*O_NB*/, int32_t *n_nodes,
                 int32_t *n_points, int nthreads);
+/* Mo with an rgbprofile material: rd_table rows 0..2 = R, G, B profiles [3][len], rcp[3];
+   Rd = SampledSpectrum::FromRGB(reflectance) of the three lookups (multipole.cpp:85-107) */
+void o_mo_batch_rgb(const o_octree *t, int q, const float *pts, const float *rd_table, int len, const float rcp[3],
+                    float max_error, float *mo, int32_t *n_nodes, int32_t *n_points, int nthreads);
 /* DiffusionReflectance (diffusionutil.h:38-83): the single-dipole Rd functor */
 typedef struct {
     float zpos[O_NB], zneg[O_NB], sigmap_t[O_NB], sigma_tr[O_NB], alphap[O_NB];
@@ -184,6 +188,8 @@ void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, con
 void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw);
 void o_scene_free(o_scene *s);
 /* LayeredSkin "albedo" (which = 0, a spectrum imagemap) or "bumpmap" (which = 1, a float imagemap) */
+/* rgbprofile material: its rd table's rows 0..2 are the R, G, B profiles (o_mo_batch_rgb) */
+int o_scene_set_material_rgb(o_scene *s, int material, int rgb);
 int o_scene_set_material_texture(o_scene *s, int material, int which, int W, int H, const float *texels,
                                  float shift, float scale, float gamma, int wrap, int trilinear, float max_aniso,
                                  float su, float sv, float du, float dv);

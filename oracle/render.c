@@ -151,6 +151,7 @@ typedef struct {
     float *rd;
     int L;
     float rcp[O_NB];
+    int rgb; /* rgbprofile: rd rows 0..2 = R, G, B (multipole.cpp:85-107) */
 } o_mat;
 
 typedef struct { float bmin[3], bmax[3]; int left, right, first, count; } o_bnode;
@@ -215,6 +216,12 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T, const float
     m->rd = dupf(rd, (size_t)O_NB * L);
     m->L = L;
     return s->nmats++;
+}
+
+int o_scene_set_material_rgb(o_scene *s, int material, int rgb) {
+    if (material < 0 || material >= s->nmats) return -1;
+    s->mats[material].rgb = rgb;
+    return 0;
 }
 
 int o_scene_set_material_texture(o_scene *s, int material, int which, int W, int H, const float *texels,
@@ -1339,7 +1346,10 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
     /* Mo() term (multipolesubsurface.cpp:268-290) */
     if (s->octree) {
         float q[3] = {fr.p.x, fr.p.y, fr.p.z}, mo[O_NB];
-        o_mo_batch(s->octree, 1, q, mat->rd, mat->L, mat->rcp, s->max_error, mo, NULL, NULL, 1);
+        if (mat->rgb)
+            o_mo_batch_rgb(s->octree, 1, q, mat->rd, mat->L, mat->rcp, s->max_error, mo, NULL, NULL, 1);
+        else
+            o_mo_batch(s->octree, 1, q, mat->rd, mat->L, mat->rcp, s->max_error, mo, NULL, NULL, 1);
         float ct = absdot(wo, fr.nn);
         ct = ct < 1.f ? ct : 1.f;
         float Ft = mat->is_mc ? 1.f : 1.f - rho_at(mat, ct);

@@ -1,5 +1,6 @@
 // context.cpp -- Context implementation (material preparation, octree upload).
 #include "context.h"
+#include "spectral.h"
 
 #include <cstring>
 
@@ -64,7 +65,7 @@ void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) {
 void Context::ensure_layouts() {
     if (!have_octree_) return;
     for (const auto &m : materials_)
-        if (!m->dipole) dev_octree_.ensure_layout(m->dev_profile.groups);
+        if (!m->dipole && !m->rgb) dev_octree_.ensure_layout(m->dev_profile.groups);
 }
 
 // SubsurfaceOctreeNode::Mo for a batch of points (mpss_mo_batch). The octree, profile and band
@@ -85,6 +86,8 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         mode = cfg_.exact_mo;
         if (m->dipole) {
             mode = -1;  // closed-form functor: the reference-order gather (dipole.h)
+        } else if (m->rgb) {
+            mode = -2;  // FromRGB of three lookups: the reference-order gather
         } else if (mode == 0) {
             layout = &dev_octree_.ensure_layout(m->dev_profile.groups);
             ws = acquire_ws();
@@ -92,6 +95,11 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
     }
     if (mode == -1) {
         launch_mo_dipole(dev_octree_, m->dev_dipole.ptr, max_error_, q, p_dev, out_dev, NB, counters_dev, stream);
+        return;
+    }
+    if (mode == -2) {
+        launch_mo_rgb(dev_octree_, m->dev_rgb.ptr, m->dev_rgb_rcp.ptr, m->rgb_rcp, m->profile.length, max_error_, q,
+                      p_dev, nullptr, nullptr, nullptr, 0, out_dev, NB, counters_dev, stream);
         return;
     }
     if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
@@ -131,7 +139,22 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     sp.double_ref_sslf = m.double_ref_sslf != 0;
     LayerParams lp;
     skin_layer_params(sp, lp);
-    if (m.use_monte_carlo)
+    if (m.rgb_profile) {
+        // ComputeRGBMultipoleProfile (multipole.cpp:408-451, layeredskin.cpp:85-86,97-99): each layer's
+        // mua / musp as ToRGBSpectrum, profile channel k from component k. Every band c is built
+        // from component c % 3, so rows 0..2 of the table are the R, G, B profiles.
+        for (int l = 0; l < 2; ++l) {
+            float ra[3], rs[3];
+            spectrum_to_rgb(lp.mua[l], ra);
+            spectrum_to_rgb(lp.musp[l], rs);
+            for (int c = 0; c < NB; ++c) {
+                lp.mua[l][c] = ra[c % 3];
+                lp.musp[l][c] = rs[c % 3];
+            }
+        }
+        mat->rgb = true;
+    }
+    if (m.use_monte_carlo && !m.rgb_profile)
         build_profile_mc(lp, m.photons, 89, mat->profile);
     else if (cfg_.profile_on_host || sp.desired_length > 1024)
         build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
@@ -149,6 +172,12 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     mat->double_ref_sslf = m.double_ref_sslf != 0;
     mat->is_monte_carlo = m.use_monte_carlo != 0;  // Ft = 1 in Li (multipolesubsurface.cpp:285)
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
+    if (mat->rgb) {
+        mat->dev_rgb.upload(mat->profile.table.data(), 3 * (size_t)mat->profile.length);
+        for (int k = 0; k < 3; ++k) mat->rgb_rcp[k] = mat->profile.rcp[k];
+        mat->dev_rgb_rcp.upload(mat->rgb_rcp, 3);
+        for (int c = 0; c < NB; ++c) mat->dev_profile.groups.pos[c] = c;  // Mo() rows in band order
+    }
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));
     scene_dirty_ = true;

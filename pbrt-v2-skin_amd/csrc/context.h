@@ -31,6 +31,11 @@ struct Material {
     DeviceProfile dev_profile;
     DevBuf<float> dev_rho;  // [n_rho]
     int albedo_tex = -1, bump_tex = -1;  // ImageTexture ids ("texture albedo" / "texture bumpmap")
+    // rgbprofile (ComputeRGBMultipoleProfile): Rd = FromRGB of three tables, Mo() in the
+    // reference-order gather; dev_rgb [3][L] (rows 0..2 of profile.table), rgb_rcp their rcp
+    bool rgb = false;
+    DevBuf<float> dev_rgb, dev_rgb_rcp;
+    float rgb_rcp[3] = {0.f, 0.f, 0.f};
     // a DiffusionReflectance functor instead of a profile (mpss_add_dipole_material): Mo only
     bool dipole = false;
     DipoleRd dip{};

@@ -64,6 +64,14 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
 void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
                       float *out, int out_stride, int32_t *counters, hipStream_t stream);
 
+// Mo with an rgbprofile material (multipole.cpp:85-107): table3 [3][L] R, G, B profiles (device),
+// rcp3 their rcpDsqSpacing (device and host copies), in the reference summation order. Queries
+// either queries (q x 3) or the render path's queries4 / count_dev / hit_s + mat (see
+// launch_mo_band); out[i * out_stride + c].
+void launch_mo_rgb(const DeviceOctree &t, const float *table3, const float *rcp3_dev, const float rcp3[3], int L,
+                   float max_error, int nq, const float *queries, const float4 *queries4, const int *count_dev,
+                   const uint32_t *hit_s, int mat, float *out, int out_stride, int32_t *counters, hipStream_t stream);
+
 // Traversal statistics of the sharded gather (count variant): per group g, counts[kStatStride*g + k]
 // for k = 0 node visits, 1 point visits (summed over queries), 2 wave node iterations, 3 wave
 // point iterations (summed over waves; 64 x these / the visits = 1 / lane efficiency), 4 table

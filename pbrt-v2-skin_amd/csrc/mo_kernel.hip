@@ -25,6 +25,7 @@
 // pruned traversal's visits (SURVEY.md 8d counters).
 #include "dipole.h"
 #include "mo_kernel.h"
+#include "spectral.h"
 #include "mo_packet.h"
 
 #include <cstring>
@@ -47,14 +48,66 @@ struct MoArgs {
     int L, n_nodes, nq, out_stride;
     float max_error, prune_f;           // prune when d2box * rcp_min >= prune_f
     float rcp_min;
-    const float *__restrict__ dipole;   // DIP: [4][NB] zpos, zneg, sigma_tr, k (dipole.h)
+    const float *__restrict__ dipole;   // FN_DIPOLE: [4][NB] zpos, zneg, sigma_tr, k (dipole.h)
+    // render path (instead of queries): queries4[i] = {p, w} (w < 0: no BSSRDF), i < *count, and
+    // with hit_s the material filter; out[i * out_stride + c]
+    const float4 *__restrict__ queries4;
+    const int *__restrict__ count;
+    const uint32_t *__restrict__ hit_s;
+    int mat;
 };
+
+// Rd functors of the reference-order gather: the tabulated spectral profile, the closed-form
+// single dipole (DiffusionReflectance), and the RGB profile (rgbprofile: three tables, Rd =
+// SampledSpectrum::FromRGB(reflectance) of the three lookups, multipole.cpp:85-107).
+enum { FN_TABLE = 0, FN_DIPOLE = 1, FN_RGB = 2 };
+
+// rgbRefl2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue} (spectrum.cpp, SampledSpectrum::Init)
+__constant__ float kRefl[7][NB] = {MPSS_BAND_RGBREFL2SPECTWHITE_INIT, MPSS_BAND_RGBREFL2SPECTCYAN_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTMAGENTA_INIT, MPSS_BAND_RGBREFL2SPECTYELLOW_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTRED_INIT, MPSS_BAND_RGBREFL2SPECTGREEN_INIT,
+                                   MPSS_BAND_RGBREFL2SPECTBLUE_INIT};
+
+// Band c of SampledSpectrum::FromRGB(rgb, SPECTRUM_REFLECTANCE) (spectrum.cpp:103-186): the same
+// float operations as the 30-band code (spectral.cpp spectrum_from_rgb), one band.
+__device__ __forceinline__ float from_rgb_band(float R, float G, float B, int c) {
+    enum { W = 0, CY = 1, MG = 2, YE = 3, RD = 4, GR = 5, BL = 6 };
+    float r = 0.f;
+    if (R <= G && R <= B) {
+        r += kRefl[W][c] * R;
+        if (G <= B) { r += kRefl[CY][c] * (G - R); r += kRefl[BL][c] * (B - G); }
+        else { r += kRefl[CY][c] * (B - R); r += kRefl[GR][c] * (G - B); }
+    } else if (G <= R && G <= B) {
+        r += kRefl[W][c] * G;
+        if (R <= B) { r += kRefl[MG][c] * (R - G); r += kRefl[BL][c] * (B - R); }
+        else { r += kRefl[MG][c] * (B - G); r += kRefl[RD][c] * (R - B); }
+    } else {
+        r += kRefl[W][c] * B;
+        if (R <= G) { r += kRefl[YE][c] * (R - B); r += kRefl[GR][c] * (G - R); }
+        else { r += kRefl[YE][c] * (G - B); r += kRefl[RD][c] * (R - G); }
+    }
+    const float v = r * (float).94;
+    return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
+}
 
 __device__ __forceinline__ float rd_lerp(const float *__restrict__ tb, float f) {
     const uint32_t s = (uint32_t)f;
     const float t = f - (float)s;
     const float a = tb[s], b = tb[s + 1];
     return (1.f - t) * a + t * b;
+}
+
+// MultipoleProfileData::reflectance with isRGBProfile (multipole.cpp:85-107): sampleProfile of
+// the R, G, B tables, then band c of Spectrum::FromRGBSpectrum
+__device__ __forceinline__ float rgb_rd(const float *__restrict__ table, int L, const float rcp3[3], float lm1, float d2,
+                                        int c) {
+    float v[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float f = d2 * rcp3[k];
+        v[k] = f < lm1 ? rd_lerp(table + (size_t)k * L, f) : 0.f;
+    }
+    return from_rgb_band(v[0], v[1], v[2], c);
 }
 
 __device__ __forceinline__ float box_d2(float px, float py, float pz, const NodeHdr &h) {
@@ -64,25 +117,40 @@ __device__ __forceinline__ float box_d2(float px, float py, float pz, const Node
     return bx * bx + by * by + bz * bz;
 }
 
-// DIP: the Rd functor is the closed-form single dipole (DiffusionReflectance, dipole.h) instead
-// of the tabulated profile; it never returns an exact 0 past a range, so nothing is pruned.
-template <int MAXD, bool COUNT, bool DIP>
+// FN_DIPOLE: the Rd functor is the closed-form single dipole (DiffusionReflectance, dipole.h)
+// instead of the tabulated profile; it never returns an exact 0 past a range, so nothing is
+// pruned. FN_RGB: a.table holds the R, G, B profiles ([3][L]) and a.rcp their rcpDsqSpacing; the
+// three lookups are wave-uniform per half-wave, each lane converts them to its band.
+template <int MAXD, bool COUNT, int FN>
 __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
+    constexpr bool DIP = FN == FN_DIPOLE;
     __shared__ float S[4][MAXD + 1][64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int c = lane & 31;
     const int q = ((int)blockIdx.x * 4 + wave) * 2 + (lane >> 5);
-    const bool active = q < a.nq;
+    bool active = q < a.nq;
     float(*St)[64] = S[wave];
 
     float px = 0.f, py = 0.f, pz = 0.f;
-    if (active) {
+    if (a.queries4) {  // render path: the compacted hit list (count on the device) and its filter
+        if (active) active = q < *a.count;
+        if (active) {
+            const float4 v = a.queries4[q];
+            px = v.x;
+            py = v.y;
+            pz = v.z;
+            active = v.w >= 0.f && (!a.hit_s || (int)((a.hit_s[q] >> 16) & 0xffu) == a.mat);
+        }
+    } else if (active) {
         px = a.queries[3 * (size_t)q];
         py = a.queries[3 * (size_t)q + 1];
         pz = a.queries[3 * (size_t)q + 2];
     }
-    const float rcp = (!DIP && c < NB) ? a.rcp[c] : INFINITY;
+    const float rcp = (FN == FN_TABLE && c < NB) ? a.rcp[c] : INFINITY;
+    float rcp3[3] = {0.f, 0.f, 0.f};
+    if (FN == FN_RGB)
+        for (int k = 0; k < 3; ++k) rcp3[k] = a.rcp[k];
     const float lm1 = (float)(a.L - 1);
     const float *__restrict__ tb = a.table + (size_t)(c < NB ? c : 0) * a.L;
     float dzp = 0.f, dzn = 0.f, dtr = 0.f, dk = 0.f;
@@ -128,6 +196,8 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
             if (dw < a.max_error && !inside) {
                 if (DIP) {
                     St[d][lane] += dipole_band(dzp, dzn, dtr, dk, d2) * a.node_et[(size_t)node * ROW + c];
+                } else if (FN == FN_RGB) {
+                    St[d][lane] += rgb_rd(a.table, a.L, rcp3, lm1, d2, c < NB ? c : 0) * a.node_et[(size_t)node * ROW + c];
                 } else {
                     const float f = d2 * rcp;
                     if (f < lm1) St[d][lane] += rd_lerp(tb, f) * a.node_et[(size_t)node * ROW + c];
@@ -145,6 +215,11 @@ __global__ __launch_bounds__(256) void mo_gather_kernel(MoArgs a) {
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
                     if (DIP) {
                         acc += dipole_band(dzp, dzn, dtr, dk, ex * ex + ey * ey + ez * ez) *
+                               a.pt_e[(size_t)k * ROW + c] * ph.w;
+                        continue;
+                    }
+                    if (FN == FN_RGB) {
+                        acc += rgb_rd(a.table, a.L, rcp3, lm1, ex * ex + ey * ey + ez * ez, c < NB ? c : 0) *
                                a.pt_e[(size_t)k * ROW + c] * ph.w;
                         continue;
                     }
@@ -441,25 +516,25 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     return bt;
 }
 
-template <int MAXD, bool DIP>
+template <int MAXD, int FN>
 void launch_t(const MoArgs &a, bool count, hipStream_t s) {
     const int waves = (a.nq + 1) / 2;
     const int blocks = (waves + 3) / 4;
     if (blocks == 0) return;
     if (count)
-        hipLaunchKernelGGL((mo_gather_kernel<MAXD, true, DIP>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, true, FN>), dim3(blocks), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((mo_gather_kernel<MAXD, false, DIP>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((mo_gather_kernel<MAXD, false, FN>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-template <bool DIP>
+template <int FN>
 void launch_exact(const MoArgs &a, int max_depth, bool count, hipStream_t s) {
     if (max_depth < 16)
-        launch_t<16, DIP>(a, count, s);
+        launch_t<16, FN>(a, count, s);
     else if (max_depth < 32)
-        launch_t<32, DIP>(a, count, s);
+        launch_t<32, FN>(a, count, s);
     else if (max_depth < 64)
-        launch_t<64, DIP>(a, count, s);
+        launch_t<64, FN>(a, count, s);
     else
         throw Error(-2, "octree deeper than 63 levels is not supported by the gather kernel");
     MPSS_HIP(hipGetLastError());
@@ -582,7 +657,7 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
         launch_band(b, nq, t, count, stream);
         return;
     }
-    MoArgs a;
+    MoArgs a{};  // value-initialized: unused fields (render-path queries, functor tables) are null
     a.nodes = t.nodes.ptr;
     a.node_et = t.node_et.ptr;
     a.pt_hdr = t.pt_hdr.ptr;
@@ -609,7 +684,7 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
         return;
     }
     a.dipole = nullptr;
-    launch_exact<false>(a, t.max_depth, count, stream);
+    launch_exact<FN_TABLE>(a, t.max_depth, count, stream);
 }
 
 void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
@@ -632,7 +707,40 @@ void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_
     a.rcp_min = 0.f;
     a.prune_f = INFINITY;
     a.dipole = dipole_dev;
-    launch_exact<true>(a, t.max_depth, counters != nullptr, stream);
+    launch_exact<FN_DIPOLE>(a, t.max_depth, counters != nullptr, stream);
+}
+
+void launch_mo_rgb(const DeviceOctree &t, const float *table3, const float *rcp3_dev, const float rcp3[3], int L,
+                   float max_error, int nq, const float *queries, const float4 *queries4, const int *count_dev,
+                   const uint32_t *hit_s, int mat, float *out, int out_stride, int32_t *counters, hipStream_t stream) {
+    if (nq <= 0) return;
+    if (t.n_nodes <= 0) throw Error(-1, "launch_mo_rgb: octree is empty");
+    if (L < 2) throw Error(-1, "launch_mo_rgb: profile table has fewer than 2 entries");
+    MoArgs a{};
+    a.nodes = t.nodes.ptr;
+    a.node_et = t.node_et.ptr;
+    a.pt_hdr = t.pt_hdr.ptr;
+    a.pt_e = t.pt_e.ptr;
+    a.table = table3;
+    a.rcp = rcp3_dev;
+    a.queries = queries;
+    a.queries4 = queries4;
+    a.count = count_dev;
+    a.hit_s = hit_s;
+    a.mat = mat;
+    a.out = out;
+    a.counters = counters;
+    a.L = L;
+    a.n_nodes = t.n_nodes;
+    a.nq = nq;
+    a.out_stride = out_stride;
+    a.max_error = max_error;
+    // every band is FromRGB of the three lookups: +0 once all three are past their table's end
+    float rmin = rcp3[0] < rcp3[1] ? rcp3[0] : rcp3[1];
+    rmin = rcp3[2] < rmin ? rcp3[2] : rmin;
+    a.rcp_min = rmin > 0.f ? rmin : 0.f;
+    a.prune_f = (a.rcp_min > 0.f) ? (float)(L - 1) * 1.0001f : INFINITY;
+    launch_exact<FN_RGB>(a, t.max_depth, counters != nullptr, stream);
 }
 
 }  // namespace mpss

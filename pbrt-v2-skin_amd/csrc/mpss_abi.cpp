@@ -100,6 +100,7 @@ void mpss_layeredskin_defaults(mpss_layeredskin *m) {
     m->double_ref_sslf = 0;
     m->use_monte_carlo = 0;
     m->photons = 10000000ull;
+    m->rgb_profile = 0;
 }
 
 int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {

@@ -552,7 +552,10 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     std::vector<SssMat> sss;
     if (have_octree_)
         for (size_t i = 0; i < materials_.size(); ++i)
-            if (!materials_[i]->dipole) sss.push_back(SssMat{(int)i, materials_[i].get(), &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
+            if (!materials_[i]->dipole)
+                sss.push_back(SssMat{(int)i, materials_[i].get(),
+                                     materials_[i]->rgb ? nullptr
+                                                        : &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
     sc.have_octree = sss.empty() ? 0 : 1;
     if (replay) {
@@ -707,10 +710,17 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             }
             if (!sss.empty()) {
                 time_begin(timing, stream, ev);
-                for (const SssMat &s : sss)
-                    launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)total, ws->q.ptr,
-                                   ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
-                                   ws->work.ptr, stream);
+                for (const SssMat &s : sss) {
+                    if (s.m->rgb)  // Mo() rows in band order (the material's pos is the identity)
+                        launch_mo_rgb(dev_octree_, s.m->dev_rgb.ptr, s.m->dev_rgb_rcp.ptr, s.m->rgb_rcp,
+                                      s.m->profile.length, max_error, (int)total, nullptr, ws->q.ptr, ws->count.ptr,
+                                      sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, (float *)ws->mo.ptr, 4 * kGroups,
+                                      nullptr, stream);
+                    else
+                        launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)total, ws->q.ptr,
+                                       ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
+                                       ws->work.ptr, stream);
+                }
                 time_end(timing, stream, ev, 2, timed);
             }
             off = 0;

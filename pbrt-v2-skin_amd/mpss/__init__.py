@@ -65,7 +65,8 @@ class LayeredSkin(C.Structure):
                 ("b_derm", C.c_float), ("layer_thickness_nm", C.c_float * 2), ("layer_ior", C.c_float * 2),
                 ("albedo", C.c_float * NB), ("Kr", C.c_float * NB), ("Kt", C.c_float * NB),
                 ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
-                ("double_ref_sslf", C.c_int), ("use_monte_carlo", C.c_int), ("photons", C.c_uint64)]
+                ("double_ref_sslf", C.c_int), ("use_monte_carlo", C.c_int), ("photons", C.c_uint64),
+                ("rgb_profile", C.c_int)]
 
 
 class Imagemap(C.Structure):

@@ -354,7 +354,7 @@ def _skin_params(ps, textures):
     if "photons" in ps:  # a string parameter parsed with _strtoui64 (layeredskin.cpp:251-252)
         p["photons"] = int(str(ps.one("photons")))
     for k, dst in (("lerponthinslab", "lerp_on_thin_slab"), ("doublerefsslf", "double_ref_sslf"),
-                   ("usemontecarlo", "use_monte_carlo")):
+                   ("usemontecarlo", "use_monte_carlo"), ("rgbprofile", "rgb_profile")):
         if k in ps:
             v = ps.one(k)
             p[dst] = int(v in (True, "true", 1))

@@ -46,6 +46,7 @@ def lib():
     L.o_average_spectrum_samples.restype = C.c_float
     L.o_average_spectrum_samples.argtypes = [f32p, f32p, C.c_int, C.c_float, C.c_float]
     L.o_from_rgb.argtypes = [f32p, C.c_int, f32p]
+    L.o_to_rgb.argtypes = [f32p, f32p]
     L.o_y.restype = C.c_float
     L.o_y.argtypes = [f32p]
     L.o_to_xyz.argtypes = [f32p, f32p]
@@ -75,6 +76,8 @@ def lib():
     L.o_octree_num_nodes.argtypes = [C.c_void_p]
     L.o_mo_batch.argtypes = [C.c_void_p, C.c_int, f32p, f32p, C.c_int, f32p, C.c_float, f32p,
                              C.c_void_p, C.c_void_p, C.c_int]
+    L.o_mo_batch_rgb.argtypes = [C.c_void_p, C.c_int, f32p, f32p, C.c_int, f32p, C.c_float, f32p,
+                                 C.c_void_p, C.c_void_p, C.c_int]
     L.o_diffusion_init.argtypes = [f32p, f32p, C.c_float, C.c_void_p]
     L.o_diffusion_eval.argtypes = [C.c_void_p, C.c_float, f32p]
     L.o_diffusion_total.argtypes = [C.c_void_p, f32p]
@@ -89,6 +92,13 @@ def lib():
 
 def nthreads():
     return max(1, min(os.cpu_count() or 1, 16))
+
+
+def to_rgb(s):
+    """SampledSpectrum::ToRGB (ToXYZ + XYZToRGB, spectrum.h:51-55, 374-398)."""
+    out = np.zeros(3, np.float32)
+    lib().o_to_rgb(np.ascontiguousarray(s, np.float32), out)
+    return out
 
 
 def from_rgb(rgb, illuminant=False):
@@ -205,6 +215,16 @@ class Octree:
                          max_error, out, nn.ctypes.data if counters else None,
                          npt.ctypes.data if counters else None, nthreads())
         return (out, nn, npt) if counters else out
+
+    def mo_rgb(self, q, table, rcp, max_error):
+        """Mo with an rgbprofile material: table rows 0..2 = the R, G, B profiles, rcp[:3]."""
+        q = np.ascontiguousarray(q, np.float32)
+        table = np.ascontiguousarray(table[:3], np.float32)
+        out = np.zeros((len(q), NB), np.float32)
+        lib().o_mo_batch_rgb(self.handle, len(q), q, table, table.shape[1],
+                             np.ascontiguousarray(np.asarray(rcp, np.float32)[:3]), max_error, out, None, None,
+                             nthreads())
+        return out
 
     def mo_diffusion(self, q, dip, max_error, counters=False):
         q = np.ascontiguousarray(q, np.float32)

@@ -28,6 +28,8 @@ def _lib():
     L.o_scene_add_material.restype = C.c_int
     L.o_scene_add_material.argtypes = [vp, f32p, f32p, f32p, C.c_float, C.c_float, C.c_float, C.c_int, f32p,
                                        C.c_int, C.c_int, f32p, C.c_int, f32p]
+    L.o_scene_set_material_rgb.restype = C.c_int
+    L.o_scene_set_material_rgb.argtypes = [vp, C.c_int, C.c_int]
     L.o_scene_add_mesh.restype = C.c_int
     L.o_scene_add_mesh.argtypes = [vp, C.c_int, f32p, vp, vp, vp, C.c_int, oracle_lib.i32p, f32p, f32p, C.c_int,
                                    C.c_int]
@@ -130,6 +132,8 @@ class OracleScene:
             L.o_scene_add_material(self.h, Kr, Kt, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
                                    int(skin.double_ref_sslf), rho, len(rho), int(skin.use_monte_carlo),
                                    np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
+            if skin.rgb_profile:
+                assert L.o_scene_set_material_rgb(self.h, mid, 1) == 0
             for which, key in ((0, "albedo_tex"), (1, "bump_tex")):
                 if m.get(key) is not None:
                     W, H, ptr, arr, rest = _tex_args(m[key])
