@@ -91,6 +91,27 @@ struct TileBatch {
     int64_t nsamples;  // ew * eh * spp
 };
 
+// Up to kMaxPieces tile pieces of one batch in ONE launch of primary_kernel / film_kernel (a
+// launch per piece left most of the chip idle: a 128 x 128 tile's film pass is 64 workgroups).
+// Piece k owns blocks [block0[k], block0[k + 1]); its camera samples start at record off[k] of
+// the batch; out[k] / out_stride[k]: its film rectangle (film_kernel).
+constexpr int kMaxPieces = 16;
+struct PieceList {
+    int n;
+    int block0[kMaxPieces + 1];
+    int out_stride[kMaxPieces];
+    int64_t off[kMaxPieces];
+    float *out[kMaxPieces];
+    TileBatch tb[kMaxPieces];
+};
+
+// The piece of this block (wave-uniform: kernel-argument reads, <= kMaxPieces steps).
+__device__ __forceinline__ int piece_of(const PieceList &pl, int block) {
+    int k = 0;
+    while (k + 1 < pl.n && block >= pl.block0[k + 1]) ++k;
+    return k;
+}
+
 enum : uint32_t {
     REC_LIVE = 1u,
     REC_SURF = 2u,  // hit a mesh: Ld valid
@@ -135,7 +156,7 @@ __global__ void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, const float *sp_uv, int n, uint32_t seed, float *E_out);
 
-__global__ void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec);
+__global__ void primary_kernel(RenderScene sc, PieceList pl, SampleRecs rec0);
 struct DirectTerms;
 // inf_st (null without infinite lights): per lane, the radiance-map lookup coordinates (s, t)
 // of the light-sampled and the BSDF-sampled direction of an infinite light's EstimateDirect
@@ -155,6 +176,6 @@ __global__ void assemble_kernel(RenderScene sc, SampleRecs rec, int max_hits);
 // cls[i] = 0 miss or light, 1 mesh surface, 2 BSSRDF surface (render_host.hip tile_costs).
 __global__ void probe_kernel(RenderScene sc, int x0, int x1, int y0, int y1, uint8_t *cls);
 __global__ void sky_kernel(RenderScene sc, SampleRecs rec, int max_hits);
-__global__ void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec, float *out, int out_stride_px);
+__global__ void film_kernel(RenderScene sc, PieceList pl, SampleRecs rec0);
 
 }  // namespace mpss

@@ -550,10 +550,15 @@ __device__ __forceinline__ void image_sample(const RenderScene &sc, uint32_t see
 // SamplerRendererTask::Run's per-sample head: image sample -> PerspectiveCamera::GenerateRay ->
 // Scene::Intersect. Surface hits are compacted (one atomic per wave, sample order kept inside
 // the wave) so the shading kernel runs on full waves; a miss or an area-light hit ends here.
-__global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, TileBatch tb, SampleRecs rec) {
+__global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList pl, SampleRecs rec) {
     __shared__ int stk_all[kStack * 256];
     int *stk = stk_all + threadIdx.x;
-    const int64_t sid0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = piece_of(pl, (int)blockIdx.x);
+    const TileBatch &tb = pl.tb[k];
+    rec.flags += pl.off[k];
+    rec.slot += pl.off[k];
+    rec.spill += pl.off[k] / tb.spp;
+    const int64_t sid0 = (int64_t)((int)blockIdx.x - pl.block0[k]) * blockDim.x + threadIdx.x;
     const bool in_range = sid0 < tb.nsamples;
     const int64_t sid = in_range ? sid0 : tb.nsamples - 1;
     const int s = (int)(sid % tb.spp);
@@ -947,10 +952,67 @@ template __global__ void direct_combine_kernel<true>(RenderScene, SampleRecs, in
 // multipolesubsurface.cpp:253-303): L = 0 + Le; L += ((INV_PI * Ft) * Mo * Pow(albedo, 1 - mix))
 // .Clamp(0); L += Ld -- then the SamplerRenderer sample filter (NaN / y < -1e-5 / inf -> 0,
 // samplerrenderer.cpp:119-133) and Spectrum::ToXYZ in band order. One lane per slot.
+// The common wave: every lane an SSS hit of one untextured material. The material is then
+// wave-uniform (its tables are scalar loads), the lane's Ld row and the band-ordered Mo() values
+// are all issued up front, and the 30-band loop is unrolled -- the same float operations, in the
+// same order, as the general path below.
+__device__ __forceinline__ void assemble_uniform(const RenderScene &sc, const SampleRecs &rec, int slot, int mid) {
+    const RenderMaterial &mat = sc.materials[mid];
+    const float4 q = rec.hit_q[slot];
+    const float Ft = mat.is_mc ? 1.f : 1.f - rho_lookup(mat.rho, mat.n_rho, q.w);
+    const float kss = kInvPiF * Ft;
+    const float *mo = reinterpret_cast<const float *>(rec.mo4 + (size_t)slot * kGroups);
+    const float4 *ld4 = reinterpret_cast<const float4 *>(rec.ld + (size_t)slot * ROW);
+    float ld[32], m[NB];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float4 v = ld4[k];
+        ld[4 * k] = v.x;
+        ld[4 * k + 1] = v.y;
+        ld[4 * k + 2] = v.z;
+        ld[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c) m[c] = mo[mat.band_pos[c]];
+    float X = 0.f, Y = 0.f, Z = 0.f;
+    bool nan = false;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        float L = 0.f;
+        float t = (kss * m[c]) * mat.alb_1mmix[c];
+        t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
+        L += t;
+        L += ld[c];
+        nan = nan || (L != L);
+        X += kCieX[c] * L;
+        Y += kCieY[c] * L;
+        Z += kCieZ[c] * L;
+    }
+    const float scale = (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
+    const float y = Y * (float)(700 - 400) / (float)(MPSS_CIE_Y_INTEGRAL * NB);
+    X *= scale;
+    Y *= scale;
+    Z *= scale;
+    if (nan || y < -1e-5f || __builtin_isinf(y)) X = Y = Z = 0.f;
+    rec.xyz[slot] = make_float4(X, Y, Z, 0.f);
+}
+
 __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRecs rec, int max_hits) {
     const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int nhits = *rec.hit_count;
-    if (slot >= nhits || slot >= max_hits) return;
+    const bool in = slot < nhits && slot < max_hits;
+    {
+        const uint32_t hs0 = in ? rec.hit_s[slot] : 0u;
+        const int mid = (int)((hs0 >> REC_MAT_SHIFT) & 0xffu);
+        const int mid0 = __builtin_amdgcn_readfirstlane(mid);
+        // SSS hit (bit 31, not a light) of material mid0, without an albedo texture
+        const bool fast = in && (hs0 >> 31) && mid == mid0;
+        if (__builtin_amdgcn_ballot_w64(in && !fast) == 0 && !sc.materials[mid0].has_alb_tex) {
+            if (in) assemble_uniform(sc, rec, slot, mid0);
+            return;
+        }
+    }
+    if (!in) return;
     const uint32_t hs = rec.hit_s[slot];
     const float *le = nullptr, *mo = nullptr, *ld = nullptr;
     const RenderMaterial *mat = nullptr;
@@ -1044,9 +1106,15 @@ __global__ __launch_bounds__(256) void sky_kernel(RenderScene sc, SampleRecs rec
     rec.xyz[slot] = make_float4(X, Y, Z, 0.f);
 }
 
-__global__ __launch_bounds__(256) void film_kernel(RenderScene sc, TileBatch tb, SampleRecs rec,
-                                                   float *__restrict__ out, int out_stride_px) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void film_kernel(RenderScene sc, PieceList pl, SampleRecs rec) {
+    const int k = piece_of(pl, (int)blockIdx.x);
+    const TileBatch &tb = pl.tb[k];
+    rec.flags += pl.off[k];
+    rec.slot += pl.off[k];
+    rec.spill += pl.off[k] / tb.spp;
+    float *__restrict__ out = pl.out[k];
+    const int out_stride_px = pl.out_stride[k];
+    const int i = ((int)blockIdx.x - pl.block0[k]) * blockDim.x + threadIdx.x;
     const int tw = tb.x1 - tb.x0, th = tb.y1 - tb.y0;
     if (i >= tw * th) return;
     const int px = tb.x0 + i % tw, py = tb.y0 + i / tw;

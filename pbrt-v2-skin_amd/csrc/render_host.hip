@@ -667,15 +667,37 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                                   ws->ha.ptr, ws->hb.ptr, ws->hs.ptr, ws->q.ptr, ws->count.ptr, ws->mo.ptr,
                                   ws->xyz.ptr, ws->alb.ptr, ws->frame.ptr};
             };
-            int64_t off = 0;
+            // the batch's pieces, kMaxPieces per launch; blocks per piece: samples (primary) or
+            // tile pixels (film) / 256
+            auto launch_pieces = [&](bool film) {
+                int64_t off = 0;
+                for (size_t k0 = pi; k0 < pe; k0 += kMaxPieces) {
+                    PieceList pl{};
+                    int blocks = 0;
+                    for (size_t k = k0; k < pe && k < k0 + kMaxPieces; ++k) {
+                        const TileBatch &tb = pieces[k].tb;
+                        const int j = pl.n++;
+                        const int tw = tb.x1 - tb.x0;
+                        const int64_t items = film ? (int64_t)tw * (tb.y1 - tb.y0) : tb.nsamples;
+                        pl.block0[j] = blocks;
+                        pl.tb[j] = tb;
+                        pl.off[j] = off;
+                        pl.out[j] = pieces[k].out;
+                        pl.out_stride[j] = tw;
+                        blocks += (int)((items + 255) / 256);
+                        off += tb.nsamples;
+                    }
+                    pl.block0[pl.n] = blocks;
+                    if (film)
+                        hipLaunchKernelGGL(film_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, sc, pl, recs(0));
+                    else
+                        hipLaunchKernelGGL(primary_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, sc, pl,
+                                           recs(0));
+                }
+            };
             hipEvent_t ev{};
             time_begin(timing, stream, ev);
-            for (size_t k = pi; k < pe; ++k) {
-                const TileBatch &tb = pieces[k].tb;
-                hipLaunchKernelGGL(primary_kernel, dim3((unsigned)((tb.nsamples + 255) / 256)), dim3(256), 0, stream,
-                                   sc, tb, recs(off));
-                off += tb.nsamples;
-            }
+            launch_pieces(false);
             time_end(timing, stream, ev, 1, timed);
             {
                 const SampleRecs rec = recs(0);
@@ -723,7 +745,6 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 }
                 time_end(timing, stream, ev, 2, timed);
             }
-            off = 0;
             time_begin(timing, stream, ev);
             {
                 const SampleRecs rec = recs(0);
@@ -733,13 +754,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                     hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
                                        rec, (int)total);
             }
-            for (size_t k = pi; k < pe; ++k) {
-                const TileBatch &tb = pieces[k].tb;
-                const int tw = tb.x1 - tb.x0, npx = tw * (tb.y1 - tb.y0);
-                hipLaunchKernelGGL(film_kernel, dim3((npx + 255) / 256), dim3(256), 0, stream, sc, tb, recs(off),
-                                   pieces[k].out, tw);
-                off += tb.nsamples;
-            }
+            launch_pieces(true);
             time_end(timing, stream, ev, 3, timed);
             MPSS_HIP(hipGetLastError());
             n_samples += total;
