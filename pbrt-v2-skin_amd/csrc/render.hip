@@ -801,7 +801,21 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                 lightPdf = L.kind ? infinite_pdf(L, wi) : sphere_pdf(L.s, fr.p, wi);
                 if (lightPdf != 0.f) {
                     const float w = power_heuristic(bsdfPdf, lightPdf);
-                    const Hit hl = trace_closest(sc, fr.p, wi, reps, INFINITY, stk, 256);
+                    // An area light is hit only if the ray meets its sphere at all: the sphere test
+                    // with maxt = inf accepts every hit that the traversal's (smaller maxt) accepts,
+                    // so a miss here is a miss there and the trace is skipped. A hit at tl bounds the
+                    // traversal: the closest primitive is the light iff nothing is hit before tl
+                    // (ties at tl go to the sphere in both, its test runs last).
+                    float tmax = INFINITY;
+                    bool need_trace = true;
+                    if (!L.kind) {
+                        float tl;
+                        need_trace = sphere_intersect(L.s, fr.p, wi, reps, INFINITY, tl, nullptr);
+                        tmax = tl;
+                    }
+                    Hit hl;
+                    hl.tri = INT_MIN;
+                    if (need_trace) hl = trace_closest(sc, fr.p, wi, reps, tmax, stk, 256);
                     // Li = lightIsect.Le(-wi) when the hit primitive is this light; light->Le(ray)
                     // when the ray escapes (0 for an area light)
                     bool lit;
