@@ -300,7 +300,10 @@ def main(a):
                                                        max(1, 64 * (cnt["mo_wave_node_iters"] +
                                                                     cnt["mo_wave_point_iters"])), 4),
                            "mo_lookup_near_fraction": [round(x / max(1, cnt["mo_lookups"]), 4)
-                                                       for x in cnt["mo_lookups_near"]]},
+                                                       for x in cnt["mo_lookups_near"]],
+                           "mo_wave_iters": {"node": cnt["mo_wave_node_iters"], "point": cnt["mo_wave_point_iters"]},
+                           "mo_visits": {"node": cnt["mo_nodes"], "point": cnt["mo_points"],
+                                         "lookups_in_profile": cnt["mo_lookups"]}},
                 "roofline": roofline, "cpu_baseline": cpu}
         if secondary:
             line["secondary"] = secondary

@@ -103,7 +103,8 @@ __global__ void level_nodes_kernel(int n, int base, int lvl, const int *__restri
     atomicAdd(&nd.nchild[par], 1);
 }
 
-// Each point of a split node moves to its child (the run of its head); the others are done.
+// Each point of a split node moves to its child (the run of its head); the others are done. The
+// run's last point writes the child's count (no atomics: a level-1 node holds ~n / 8 points).
 __global__ void level_assign_kernel(int n, int base, const int *__restrict__ nid, const int *__restrict__ head,
                                     const int *__restrict__ idx, Nodes nd, int *__restrict__ nid_out) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -112,7 +113,8 @@ __global__ void level_assign_kernel(int n, int base, const int *__restrict__ nid
     int o = -1;
     if (g >= 0 && nd.count[g] > 8) {
         o = base + idx[i] + head[i] - 1;  // inclusive scan - 1: this point's run
-        atomicAdd(&nd.count[o], 1);
+        const bool tail = i + 1 == nd.start[g] + nd.count[g] || head[i + 1];
+        if (tail) nd.count[o] = i + 1 - nd.start[o];
     }
     nid_out[i] = o;
 }
@@ -342,7 +344,6 @@ void build_octree_device(int n, const float *P, const float *N, const float *E, 
         if (added == 0) break;  // no node of this level splits: orig[cur] is final (nothing moved)
         ns.reserve((size_t)base, (size_t)base + added);
         nd = ns.view();
-        MPSS_HIP(hipMemset(ns.count.ptr + base, 0, sizeof(int) * added));
         hipLaunchKernelGGL(level_nodes_kernel, dim3(grid_of(n)), dim3(256), 0, 0, n, base, lvl + 1, nid[cur].ptr,
                            key[1].ptr, head.ptr, idx.ptr, nd);
         hipLaunchKernelGGL(level_assign_kernel, dim3(grid_of(n)), dim3(256), 0, 0, n, base, nid[cur].ptr, head.ptr,
