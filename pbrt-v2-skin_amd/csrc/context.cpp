@@ -102,10 +102,20 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
                       p_dev, nullptr, nullptr, nullptr, 0, out_dev, NB, counters_dev, stream);
         return;
     }
+    int *perm = nullptr;
+    if (ws && wave_queue_enabled()) {
+        const int64_t need = ((int64_t)q + 1023) / 1024 * 1024;
+        if (ws->perm_n < need) {
+            if (ws->pending) MPSS_HIP(hipEventSynchronize(ws->done));
+            ws->perm.alloc((size_t)need);
+            ws->perm_n = need;
+        }
+        perm = ws->perm.ptr;
+    }
     if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
     try {
         launch_mo_gather(dev_octree_, layout, m->dev_profile, max_error_, q, p_dev, out_dev, NB, counters_dev,
-                         ws ? ws->work.ptr : nullptr, stream, mode);
+                         ws ? ws->work.ptr : nullptr, stream, mode, perm);
     } catch (...) {
         if (ws) release_ws(ws, stream);
         throw;

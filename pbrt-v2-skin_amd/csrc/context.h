@@ -68,7 +68,8 @@ std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m);
 struct RenderWorkspace {
     DevBuf<uint32_t> flags, hs, spill;
     DevBuf<int32_t> slot;
-    DevBuf<int> count, work;
+    DevBuf<int> count, work, perm;  // perm: the wave-queue gather's sorted query ids
+    int64_t perm_n = 0;
     DevBuf<float4> q, mo, ha, hb, xyz, alb, frame, st;
     DevBuf<unsigned char> terms;
     DevBuf<float> ld;

@@ -57,12 +57,17 @@ struct DeviceProfile {
 // work: kGroups ints of device scratch for mode 0 (the persistent grid's chunk counters).
 void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
                       const float *queries, float *out, int out_stride, int32_t *counters, int *work,
-                      hipStream_t stream, int mode);
+                      hipStream_t stream, int mode, int *perm = nullptr);
 
 // Mo with the closed-form single dipole (dipole.h) as Rd, in the reference summation order.
 // dipole_dev: [4][NB] device floats zpos, zneg, sigma_tr, k. Nothing is pruned.
 void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
                       float *out, int out_stride, int32_t *counters, hipStream_t stream);
+
+// perm (nullable, >= nq rounded up to 1024 ints of device scratch): run the wave-queue gather
+// (mo_sort_kernel + mo_band_wave_kernel) instead of the chunk-per-workgroup kernel. Callers pass
+// it when wave_queue_enabled() (default; MPSS_MO_WAVEQ=0 turns it off).
+bool wave_queue_enabled();
 
 // Mo with an rgbprofile material (multipole.cpp:85-107): table3 [3][L] R, G, B profiles (device),
 // rcp3 their rcpDsqSpacing (device and host copies), in the reference summation order. Queries
@@ -85,6 +90,7 @@ constexpr int kStatStride = 8;
 // work: kGroups ints of device scratch (the chunk counters of the persistent grid).
 void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
                     int nq_max, const float4 *queries4, const int *count_dev, float4 *out4,
-                    const uint32_t *hit_s, int mat, unsigned long long *counts, int *work, hipStream_t stream);
+                    const uint32_t *hit_s, int mat, unsigned long long *counts, int *work, hipStream_t stream,
+                    int *perm = nullptr);
 
 }  // namespace mpss

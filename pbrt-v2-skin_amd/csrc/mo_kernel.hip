@@ -315,6 +315,7 @@ struct BandArgs {
     int *__restrict__ work;              // [kGroups] chunk counters (zeroed before the launch)
     float klo[3], kinv[3];               // Morton key quantization (octree root bounds)
     int sort;                            // 0: keep slot order (MPSS_MO_SORT=0, a tuning knob)
+    int *perm;                           // wave-queue gather: chunk-sorted query ids (-1: none)
 };
 
 __device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, float &py, float &pz) {
@@ -410,6 +411,95 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     }
 }
 
+// Wave-queue gather, step 1: each 1024-query chunk sorted by the Morton key of its live queries
+// (as mo_band_kernel does in place), written as a permutation: perm[base + i] = the i-th query
+// of the chunk in key order, -1 past the live ones. Chunks at or past the query count write nothing.
+__global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
+    __shared__ unsigned long long keys[1024];
+    const int tid = (int)threadIdx.x;
+    const int nq = a.count ? *a.count : a.nq;
+    const int base = (int)blockIdx.x * 1024;
+    if (base >= nq) return;  // uniform over the block
+    float px = 0.f, py = 0.f, pz = 0.f;
+    const bool in = base + tid < nq && band_query(a, base + tid, px, py, pz);
+    const uint32_t key = in ? (a.sort ? morton30(px, py, pz, a.klo, a.kinv) : 0u) : 0xffffffffu;
+    keys[tid] = ((unsigned long long)key << 32) | (unsigned)tid;
+    __syncthreads();
+    for (int k = 2; k <= 1024; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int ixj = tid ^ j;
+            if (ixj > tid) {
+                const unsigned long long x = keys[tid], y = keys[ixj];
+                if ((x > y) == ((tid & k) == 0)) {
+                    keys[tid] = y;
+                    keys[ixj] = x;
+                }
+            }
+            __syncthreads();
+        }
+    const unsigned long long mine = keys[tid];
+    a.perm[base + tid] = (mine >> 32) != 0xffffffffull ? base + (int)(mine & 0xffffffffull) : -1;
+}
+
+// Step 2: every wave takes 64 consecutive entries of perm at a time from its group's counter and
+// walks them to the end on its own -- no workgroup barrier between chunks, so a wave with a short
+// traversal does not wait for the slowest wave of its workgroup. Same traversal, same sums.
+template <bool COUNT, int KLDS, int NEAR, bool PAIR>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_wave_kernel(BandArgs a) {
+    __shared__ float lt[KLDS > 0 ? 4 * (KLDS + 2) : 1];
+    const int grp = (int)(blockIdx.x & (kGroups - 1));
+    const int tid = (int)threadIdx.x, lane = tid & 63;
+    const int nq = a.count ? *a.count : a.nq;
+    if (KLDS > 0) {
+        for (int i = tid; i < 4 * (KLDS + 2); i += 1024) {
+            const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
+            lt[i] = (c >= 0 && k <= KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+        }
+    }
+    __syncthreads();  // the near field is read-only from here on
+    for (;;) {
+        int u = 0;
+        if (lane == 0) u = atomicAdd(&a.work[grp], 1);
+        u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
+        const int base = u * 64;
+        if (base >= nq) break;
+        const int q = a.perm[base + lane];
+        float px = 0.f, py = 0.f, pz = 0.f;
+        const bool live = q >= 0 && band_query(a, q, px, py, pz);
+        float acc[4];
+        int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
+        mo_band_traverse<COUNT, KLDS, NEAR, PAIR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        if (live) {
+            if (a.out4) {
+                a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = a.t.groups.band[grp][j];
+                    if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
+                }
+            }
+        }
+        if (COUNT) {
+            if (a.counters && live) {
+                atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
+                atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
+            }
+            if (a.counts) {
+                if (kn) atomicAdd(&a.counts[kStatStride * grp], (unsigned long long)kn);
+                if (kp) atomicAdd(&a.counts[kStatStride * grp + 1], (unsigned long long)kp);
+                if (lane == 0) {
+                    atomicAdd(&a.counts[kStatStride * grp + 2], (unsigned long long)wn);
+                    atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
+            }
+        }
+    }
+}
+
 // Gather variant (tuning knobs; default 1024-query chunks, a 4096-entry near field read by
 // flat loads, a leaf's points two at a time): MPSS_MO_BS = 1024 | 512, MPSS_MO_K = LDS entries
 // per band (0, 2048, 4096, 9216), MPSS_MO_NEAR = 1 (masked ds/global loads into the same VGPRs:
@@ -420,6 +510,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 // field (one workgroup per CU) 140, no sort 128 (lane efficiency 0.47 vs 0.60); round 2e
 // (profiles/r02j_variants.txt, Msamples/s): flat 4096 544, + point pairs 550, + 2^26-sample
 // batches 568; no near field with pairs 467; separate-VGPR masked loads 542; 9216 with pairs 479.
+}  // namespace
+
+// Default on (C2: 48.0 vs 50.4 ms per launch, profiles/r02j_variants.txt); MPSS_MO_WAVEQ=0 runs the
+// chunk-per-workgroup kernel and its tuning knobs below.
+bool wave_queue_enabled() {
+    const char *e = getenv("MPSS_MO_WAVEQ");
+    return !e || atoi(e) != 0;
+}
+
+namespace {
+
 struct BandVariant {
     int bs, k, near, pair;
 };
@@ -457,6 +558,18 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
     const BandVariant v = band_variant();
     const char *so = getenv("MPSS_MO_SORT");
     a.sort = so ? atoi(so) : 1;
+    if (a.perm) {  // wave-queue gather (the default config: 4096-entry flat near field, point pairs)
+        const int chunks = (nq_max + 1023) / 1024;
+        hipLaunchKernelGGL(mo_sort_kernel, dim3((unsigned)chunks), dim3(1024), 0, stream, a);
+        const int per_group = chunks < 64 ? chunks : 64;
+        const dim3 grid((unsigned)(per_group * kGroups));
+        if (count)
+            hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+        else
+            hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+        MPSS_HIP(hipGetLastError());
+        return;
+    }
     if (v.pair && v.k == 0)
         launch_band_v<1024, 0, 0, true>(a, nq_max, count, stream);
     else if (v.pair && v.k == 9216)
@@ -620,7 +733,7 @@ const BandLayout &DeviceOctree::ensure_layout(const BandGroups &g) {
 
 void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
                     int nq_max, const float4 *queries4, const int *count_dev, float4 *out4, const uint32_t *hit_s,
-                    int mat, unsigned long long *counts, int *work, hipStream_t stream) {
+                    int mat, unsigned long long *counts, int *work, hipStream_t stream, int *perm) {
     if (nq_max <= 0 || t.n_nodes <= 0) return;
     BandArgs a{};
     a.t = band_tree(t, layout, p, max_error);
@@ -632,12 +745,13 @@ void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const Devic
     a.out4 = out4;
     a.counts = counts;
     a.work = work;
+    a.perm = perm;
     launch_band(a, nq_max, t, counts != nullptr, stream);
 }
 
 void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
                       const float *queries, float *out, int out_stride, int32_t *counters, int *work,
-                      hipStream_t stream, int mode) {
+                      hipStream_t stream, int mode, int *perm) {
     const bool exact = mode == 1;
     if (nq <= 0) return;
     if (t.n_nodes <= 0) throw Error(-1, "launch_mo_gather: octree is empty");
@@ -654,6 +768,7 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
         b.out_stride = out_stride;
         b.counters = counters;
         b.work = work;
+        b.perm = perm;
         launch_band(b, nq, t, count, stream);
         return;
     }
