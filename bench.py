@@ -255,7 +255,7 @@ def main(a):
     shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
-    roofline = {"kernel": "mo_band_kernel (Mo gather, spectrally sharded)", "bound": "hbm", "achieved": round(mo_gbs, 1),
+    roofline = {"kernel": "mo_sort_kernel + mo_band_wave_kernel (Mo gather, spectrally sharded, wave queue)", "bound": "hbm", "achieved": round(mo_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(mo_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
                 "dominant_kernel": dom,
@@ -351,7 +351,8 @@ def pmc_traffic(path, launch_ms):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        e = next((v for k, v in d.items() if k.startswith("void mpss::mo_band_kernel<false")), None)
+        e = next((v for k, v in d.items() if k.startswith(("void mpss::mo_band_wave_kernel<false",
+                                                             "void mpss::mo_band_kernel<false"))), None)
         if not e or "fetch_bytes_corrected_mean" not in e:
             continue
         if d.get("__meta__", {}).get("source_hash") != want:
