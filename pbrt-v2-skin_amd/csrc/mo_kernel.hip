@@ -563,10 +563,21 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
         hipLaunchKernelGGL(mo_sort_kernel, dim3((unsigned)chunks), dim3(1024), 0, stream, a);
         const int per_group = chunks < 64 ? chunks : 64;
         const dim3 grid((unsigned)(per_group * kGroups));
-        if (count)
-            hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
-        else
-            hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+        // near field: the sort's 8 KB left the workgroup, so two workgroups per CU have room for
+        // 5088 entries per band (4 x 5090 floats = 79.5 KB each) -- MPSS_MO_WK=4096 keeps the old size
+        const char *wk = getenv("MPSS_MO_WK");
+        const bool k4096 = wk && atoi(wk) == 4096;
+        if (count) {
+            if (k4096)
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+            else
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
+        } else {
+            if (k4096)
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+            else
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
+        }
         MPSS_HIP(hipGetLastError());
         return;
     }
