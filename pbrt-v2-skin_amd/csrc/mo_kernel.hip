@@ -28,6 +28,7 @@
 #include "spectral.h"
 #include "mo_packet.h"
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -561,20 +562,31 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
     if (a.perm) {  // wave-queue gather (the default config: 4096-entry flat near field, point pairs)
         const int chunks = (nq_max + 1023) / 1024;
         hipLaunchKernelGGL(mo_sort_kernel, dim3((unsigned)chunks), dim3(1024), 0, stream, a);
-        const int per_group = chunks < 64 ? chunks : 64;
+        const char *wg = getenv("MPSS_MO_WGS");  // resident workgroups per group, 2 per CU (tuning knob)
+        const int cap = wg ? std::max(1, std::min(64, atoi(wg))) : 64;
+        const int per_group = chunks < cap ? chunks : cap;
         const dim3 grid((unsigned)(per_group * kGroups));
         // near field: the sort's 8 KB left the workgroup, so two workgroups per CU have room for
         // 5088 entries per band (4 x 5090 floats = 79.5 KB each) -- MPSS_MO_WK=4096 keeps the old size
+        // near field per band: 10236 entries (default) -- one workgroup of 16 waves per CU holds the
+        // whole 160 KB LDS, 32 workgroups per group; the wave queue keeps the gather L2-bound at 4
+        // waves per SIMD (C2: 43.9 ms per launch vs 46.6 with two workgroups x 5088 entries,
+        // profiles/r02j_variants.txt). MPSS_MO_WK=5088 | 4096: two workgroups per CU.
         const char *wk = getenv("MPSS_MO_WK");
-        const bool k4096 = wk && atoi(wk) == 4096;
+        const int kw = wk ? atoi(wk) : 10236;
+        const dim3 grid1((unsigned)((chunks < 32 ? chunks : 32) * kGroups));
         if (count) {
-            if (k4096)
+            if (kw == 4096)
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+            else if (kw == 10236)
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         } else {
-            if (k4096)
+            if (kw == 4096)
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
+            else if (kw == 10236)
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         }
