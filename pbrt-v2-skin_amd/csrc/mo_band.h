@@ -125,7 +125,18 @@ struct BandLane {
     uint32_t lm1;     // L - 1: sampleProfile's range end
     uint32_t klim;    // min(KLDS, L - 1): s < klim <=> the pair (s, s + 1) is in the LDS copy
     const float *lt;  // LDS rows of KLDS + 2 floats per band slot (generic pointer)
+    // NEAR 5 (rows of KLDS + 3 floats): klim = min(KLDS, L - 2), gspan = L - 1 - klim; lanes with
+    // klim <= s < L - 1 read the table, all others LDS -- s < klim the near field, s >= L - 1
+    // (past the profile end) the zero pair at row offset KLDS + 1: one select less per band than
+    // NEAR 2's zero-index and near-field tests. tb[j]: the band's table row.
+    uint32_t gspan;
+    const float *tb[4];
 };
+// Row length (floats) of a band's LDS near field for near-field mode NEAR.
+template <int KLDS, int NEAR>
+__host__ __device__ constexpr int near_row() {
+    return NEAR == 5 ? KLDS + 3 : KLDS + 2;
+}
 
 // Rd lookups of one record for the lane's 4 bands, accumulated:
 // acc[j] += Rd_j(d2) * e[j] (* w), as sampleProfile + the Mo() product (multipole.cpp:60-73;
@@ -156,7 +167,12 @@ __device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, c
     for (int j = 0; j < 4; ++j) {
         const uint32_t s = (uint32_t)f[j];  // saturating convert: f >= 2^32 -> 0xffffffff >= lm1
         const uint32_t idx = s < b.lm1 ? b.off[j] + s : b.zero;
-        if (KLDS > 0 && NEAR == 2) {
+        if (KLDS > 0 && NEAR == 5) {
+            const bool glob = s - b.klim < b.gspan;  // unsigned: s < klim wraps past gspan
+            const uint32_t li = s < (uint32_t)(KLDS + 1) ? s : (uint32_t)(KLDS + 1);
+            const float *src = glob ? b.tb[j] + s : b.lt + j * (KLDS + 3) + li;
+            v[j] = *reinterpret_cast<const RdPair *>(src);
+        } else if (KLDS > 0 && NEAR == 2) {
             const float *src = s < b.klim ? b.lt + j * (KLDS + 2) + s : table + idx;
             v[j] = *reinterpret_cast<const RdPair *>(src);
         } else if (KLDS > 0 && NEAR == 4) {
@@ -257,6 +273,13 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     b.zero = (uint32_t)NB * (uint32_t)a.L;
     b.lm1 = (uint32_t)(a.L - 1);
     b.klim = (uint32_t)KLDS < b.lm1 ? (uint32_t)KLDS : b.lm1;
+    if (NEAR == 5) {
+        const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
+        b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
+        b.gspan = b.lm1 - b.klim;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b.tb[j] = a.table + b.off[j];
+    }
     b.lt = lt;
     const float *__restrict__ table = a.table;
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};

@@ -447,14 +447,18 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
 // traversal does not wait for the slowest wave of its workgroup. Same traversal, same sums.
 template <bool COUNT, int KLDS, int NEAR, bool PAIR>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_wave_kernel(BandArgs a) {
-    __shared__ float lt[KLDS > 0 ? 4 * (KLDS + 2) : 1];
+    constexpr int ROWF = near_row<KLDS, NEAR>();
+    __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
     const int grp = (int)(blockIdx.x & (kGroups - 1));
     const int tid = (int)threadIdx.x, lane = tid & 63;
     const int nq = a.count ? *a.count : a.nq;
     if (KLDS > 0) {
-        for (int i = tid; i < 4 * (KLDS + 2); i += 1024) {
-            const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
-            lt[i] = (c >= 0 && k <= KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+        // entries 0..kmax of each band, zeros after (NEAR 5: kmax = min(KLDS, L - 2), and the last
+        // two floats of a row are the zero pair of the lanes past the profile end)
+        const int kmax = NEAR == 5 ? (KLDS < a.t.L - 2 ? KLDS : a.t.L - 2) : (KLDS < a.t.L - 1 ? KLDS : a.t.L - 1);
+        for (int i = tid; i < 4 * ROWF; i += 1024) {
+            const int j = i / ROWF, k = i % ROWF, c = a.t.groups.band[grp][j];
+            lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
     }
     __syncthreads();  // the near field is read-only from here on
@@ -571,22 +575,27 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
         // near field per band: 10236 entries (default) -- one workgroup of 16 waves per CU holds the
         // whole 160 KB LDS, 32 workgroups per group; the wave queue keeps the gather L2-bound at 4
         // waves per SIMD (C2: 43.9 ms per launch vs 46.6 with two workgroups x 5088 entries,
-        // profiles/r02j_variants.txt). MPSS_MO_WK=5088 | 4096: two workgroups per CU.
+        // profiles/r02j_variants.txt), and past-end lanes read an LDS zero pair (NEAR 5: 42.9 vs
+        // 43.5 ms; MPSS_MO_WN2=1 keeps NEAR 2). MPSS_MO_WK=5088 | 4096: two workgroups per CU.
         const char *wk = getenv("MPSS_MO_WK");
         const int kw = wk ? atoi(wk) : 10236;
         const dim3 grid1((unsigned)((chunks < 32 ? chunks : 32) * kGroups));
         if (count) {
             if (kw == 4096)
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
-            else if (kw == 10236)
+            else if (kw == 10236 && getenv("MPSS_MO_WN2"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236)
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         } else {
             if (kw == 4096)
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
-            else if (kw == 10236)
+            else if (kw == 10236 && getenv("MPSS_MO_WN2"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236)
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         }
