@@ -213,6 +213,17 @@ __device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, c
     }
 }
 
+// A wave-uniform pointer held in VGPRs for the whole traversal (opaque to rematerialization): the
+// per-lane address select of NEAR 5 then reads the band's row base straight from registers instead
+// of re-copying it from SGPRs (v_cndmask takes one SGPR operand at most) for every lookup.
+__device__ __forceinline__ const float *in_vgprs(const float *p) {
+    const uint64_t u = (uint64_t)(uintptr_t)p;
+    uint32_t lo, hi;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "s"((uint32_t)u));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "s"((uint32_t)(u >> 32)));
+    return (const float *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 // The combine half: lerp, the Mo() products and the running sums (one point or node).
 template <bool POINT>
 __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
@@ -259,7 +270,7 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 // PAIR: a leaf's points two at a time -- both points' eight pair loads issued before either's
 // terms are formed (the same terms, summed in the same order), so a wave waits out one L2 round
 // trip per two points.
-template <bool COUNT, int KLDS, int NEAR, bool PAIR>
+template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = false>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
                                                  int hist[4], const float *lt) {
@@ -278,7 +289,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
         b.gspan = b.lm1 - b.klim;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b.tb[j] = a.table + b.off[j];
+        for (int j = 0; j < 4; ++j) b.tb[j] = VROWS ? in_vgprs(a.table + b.off[j]) : a.table + b.off[j];
     }
     b.lt = lt;
     const float *__restrict__ table = a.table;

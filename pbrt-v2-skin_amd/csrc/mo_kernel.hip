@@ -445,8 +445,16 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
 // Step 2: every wave takes 64 consecutive entries of perm at a time from its group's counter and
 // walks them to the end on its own -- no workgroup barrier between chunks, so a wave with a short
 // traversal does not wait for the slowest wave of its workgroup. Same traversal, same sums.
-template <bool COUNT, int KLDS, int NEAR, bool PAIR>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_wave_kernel(BandArgs a) {
+// Waves per SIMD the register allocation targets: 8 with two workgroups per CU; the 10236-entry near
+// field fills the LDS with one workgroup (4 waves per SIMD), so up to 128 VGPRs are free to use.
+template <int KLDS>
+constexpr int wave_kernel_wpe() {
+    return KLDS > 5088 ? 4 : 8;
+}
+
+template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = (KLDS > 5088)>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS>(), wave_kernel_wpe<KLDS>())))
+void mo_band_wave_kernel(BandArgs a) {
     constexpr int ROWF = near_row<KLDS, NEAR>();
     __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
     const int grp = (int)(blockIdx.x & (kGroups - 1));
@@ -473,7 +481,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         const bool live = q >= 0 && band_query(a, q, px, py, pz);
         float acc[4];
         int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, NEAR, PAIR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        mo_band_traverse<COUNT, KLDS, NEAR, PAIR, VROWS>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
         if (live) {
             if (a.out4) {
                 a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -585,6 +593,8 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
             else if (kw == 10236 && getenv("MPSS_MO_WN2"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
             else if (kw == 10236)
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
             else
@@ -594,6 +604,8 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
             else if (kw == 10236 && getenv("MPSS_MO_WN2"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
             else if (kw == 10236)
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
             else
