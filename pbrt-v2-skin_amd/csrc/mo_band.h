@@ -233,7 +233,10 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
     for (int j = 0; j < 4; ++j) {
         const float t = __builtin_amdgcn_fractf(f[j]);  // == f - (float)(uint)f for 0 <= f < 2^24
         const f2v p = f2v{1.f - t, t} * f2v{v[j].a, v[j].b};
-        rd[j] = p.x + p.y;  // (1 - t) * T[s] + t * T[s + 1]
+        // (1 - t) * T[s] + t * T[s + 1]: one v_add_f32 of the product pair's halves (the IEEE add the
+        // compiler would emit; written out because its SLP pass otherwise pairs the adds of two bands
+        // into a v_pk_add_f32 fed by three v_mov_b32 swizzles)
+        asm("v_add_f32 %0, %1, %2" : "=v"(rd[j]) : "v"(p.x), "v"(p.y));
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
