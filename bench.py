@@ -343,7 +343,9 @@ def pmc_traffic(path, launch_ms):
     ceiling. Only a summary whose source_hash matches the current kernel sources is used; an
     older one is named as stale and its numbers are not attached."""
     import glob
-    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True)
+    # newest round tag first: r02z < r02aa (tags grow a letter), so order by length, then name
+    cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
+                                       key=lambda f: (len(os.path.basename(f)), os.path.basename(f)), reverse=True)
     want = kernel_source_hash()
     stale = None
     for f in cands:
