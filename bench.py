@@ -180,6 +180,7 @@ def timed_steps(a, ctx, sc, tiles, items_by_rank, frames, T, rank, world, steps,
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    ctx.reset_render_stats()  # per-kernel times cover exactly the timed steps
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
