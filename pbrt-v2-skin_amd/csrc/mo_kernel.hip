@@ -452,14 +452,38 @@ constexpr int wave_kernel_wpe() {
     return KLDS > 5088 ? 4 : 8;
 }
 
-template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = (KLDS > 5088)>
+template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = (KLDS > 5088), bool STEAL = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS>(), wave_kernel_wpe<KLDS>())))
 void mo_band_wave_kernel(BandArgs a) {
     constexpr int ROWF = near_row<KLDS, NEAR>();
     __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
-    const int grp = (int)(blockIdx.x & (kGroups - 1));
+    __shared__ int next_grp;
     const int tid = (int)threadIdx.x, lane = tid & 63;
     const int nq = a.count ? *a.count : a.nq;
+    // STEAL: a workgroup whose group queue is dry moves on to the next group with units left
+    // (groups g + 1, g + 2, ... in turn), reloading its near field; the XCDs whose groups finish
+    // first then take over the tail of the slowest group.
+    const int home = (int)(blockIdx.x & (kGroups - 1));
+    for (int ph = 0; ph < (STEAL ? kGroups : 1); ++ph) {
+    int grp = home;
+    if (STEAL) {
+        if (ph > 0) {
+            __syncthreads();  // every wave is done with the previous group's near field
+            if (tid == 0) {
+                int g = -1;
+                for (int k = ph; k < kGroups && g < 0; ++k) {
+                    const int c = (home + k) & (kGroups - 1);
+                    if (__hip_atomic_load(&a.work[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 64 < nq) g = c;
+                }
+                next_grp = g;
+            }
+            __syncthreads();
+            grp = next_grp;
+            if (grp < 0) break;
+            // (the loop index stays ph; later phases search from ph onwards, so a group is tried at
+            // most once after it was found dry)
+        }
+    }
     if (KLDS > 0) {
         // entries 0..kmax of each band, zeros after (NEAR 5: kmax = min(KLDS, L - 2), and the last
         // two floats of a row are the zero pair of the lanes past the profile end)
@@ -510,6 +534,7 @@ void mo_band_wave_kernel(BandArgs a) {
                     if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
             }
         }
+    }
     }
 }
 
@@ -585,6 +610,9 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
         // waves per SIMD (C2: 43.9 ms per launch vs 46.6 with two workgroups x 5088 entries,
         // profiles/r02j_variants.txt), and past-end lanes read an LDS zero pair (NEAR 5: 42.9 vs
         // 43.5 ms; MPSS_MO_WN2=1 keeps NEAR 2). MPSS_MO_WK=5088 | 4096: two workgroups per CU.
+        // Workgroups whose group queue runs dry move on to the next group with units left (the
+        // slowest group finished ~3 ms after the others: 42.5 -> 41.2 ms per C2 frame launch,
+        // profiles/r02j_variants.txt r02bd / r02be); MPSS_MO_NOSTEAL=1 keeps each on its own group.
         const char *wk = getenv("MPSS_MO_WK");
         const int kw = wk ? atoi(wk) : 10236;
         const dim3 grid1((unsigned)((chunks < 32 ? chunks : 32) * kGroups));
@@ -606,8 +634,10 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
             else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236)
+            else if (kw == 10236 && getenv("MPSS_MO_NOSTEAL"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236)  // default: work stealing across groups (41.2 vs 42.5 ms per C2 frame launch)
+                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true, true, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<false, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         }
