@@ -40,6 +40,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # groups + 16 B x the record visits of the busiest group (position/area counted once per
 # query-record, as the reference reads them once). Re-reads the sharding adds are not counted.
 REC_HDR_BYTES = 16
+REF_RECORD_BYTES = 12 + 4 + 4 * 30  # position, area / sumArea, 30-band E / Et
 # The gather's real ceiling: L2 requests of per-lane 8-byte table gathers, measured by
 # tools/microbench/l2_gather.hip on MI355X (profiles/r02_l2_gather_ceiling.json).
 L2_GATHER_CEILING_REQ_S = 2.46e11
@@ -231,6 +232,12 @@ def main(a):
     ctx.reset_render_stats()
     tl.render_items(ctx, mine, tiles, sc.spp, seeds, out_c, T, stream)
     cnt = ctx.render_stats()
+    # the reference traversal's record visits: the same pass with the reach pruning off
+    os.environ["MPSS_MO_COUNT_NOPRUNE"] = "1"
+    ctx.reset_render_stats()
+    tl.render_items(ctx, mine, tiles, sc.spp, seeds, out_c, T, stream)
+    cnt_ref = ctx.render_stats()
+    del os.environ["MPSS_MO_COUNT_NOPRUNE"]
     del out_c
     ctx.set_instrumentation(kernel_timing=True, count_traversal=False)
     ctx.reset_render_stats()
@@ -252,13 +259,21 @@ def main(a):
     dom = max(kern, key=lambda k: kern[k][0])
     nbands = [sum(1 for c in grp if c >= 0) for grp in cnt["group_bands"]]
     gvis = [cnt["group_nodes"][g] + cnt["group_points"][g] for g in range(8)]
-    mo_bytes_step = sum(gvis[g] * 4 * nbands[g] for g in range(8)) + REC_HDR_BYTES * max(gvis)  # this rank
+    # algorithmic bytes: 136 B (position, area, 30-band E) per record the reference's
+    # Mo() recursion reads, counted by the no-pruning pass (every group walks the same records)
+    ref_visits = cnt_ref["group_nodes"][0] + cnt_ref["group_points"][0]
+    mo_bytes_step = REF_RECORD_BYTES * ref_visits  # this rank
+    # the kernel's own evaluations (after the exact-zero reach pruning), the earlier definition
+    kern_bytes_step = sum(gvis[g] * 4 * nbands[g] for g in range(8)) + REC_HDR_BYTES * max(gvis)
     shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
     roofline = {"kernel": "mo_sort_kernel + mo_band_wave_kernel (Mo gather, spectrally sharded, wave queue)", "bound": "hbm", "achieved": round(mo_gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(mo_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_launch": mo_bytes_step / launches_per_step, "avg_launch_ms": round(shade_launch_ms, 4),
+                "bytes_definition": "SURVEY 8d: 136 B x record visits of the reference Mo() traversal "
+                                    "(no reach pruning), %.4g visits per SSS sample" % (ref_visits / max(1, cnt["sss_samples"])),
+                "kernel_eval_bytes_per_launch": kern_bytes_step / launches_per_step,
                 "dominant_kernel": dom,
                 "kernel_ms_per_step": {k: round(v[0] / a.steps, 3) for k, v in kern.items()}}
     # the committed PMC summaries are of the C2 command; other configs report traffic only with --pmc-json

@@ -593,6 +593,9 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
         a.kinv[k] = ext > 0.f ? 1023.99f / ext : 0.f;
     }
     MPSS_HIP(hipMemsetAsync(a.work, 0, sizeof(int) * kGroups, stream));
+    // bench.py's reference-traversal count (SURVEY 8d algorithmic bytes): the instrumented pass with
+    // the reach pruning off visits exactly the records the reference's Mo() recursion reads
+    if (count && getenv("MPSS_MO_COUNT_NOPRUNE")) a.t.prune_f = INFINITY;
     const BandVariant v = band_variant();
     const char *so = getenv("MPSS_MO_SORT");
     a.sort = so ? atoi(so) : 1;
