@@ -160,3 +160,22 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
         ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
         assert _rel_close(fast, ref, 2e-5), npts
         assert np.array_equal(band, fast), npts
+
+
+@pytest.mark.parametrize("knob", ["MPSS_MO_SNAKE", "MPSS_MO_NOSTEAL"])
+def test_mo_grouping_and_stealing_are_bit_identical(oracle, mpss, torch_dev, skin_profile, monkeypatch, knob):
+    """The default gather deals bands into adjacent-reach groups and lets workgroups steal other
+    groups' units; snake-round groups (MPSS_MO_SNAKE) and per-XCD groups (MPSS_MO_NOSTEAL) evaluate
+    the same non-zero terms in the same order, so every sum must match bit for bit (and the oracle)."""
+    cloud = synth.ellipsoid_cloud(120000, radii=RADII, seed=23, black_frac=0.05)
+    q = synth.surface_queries(20000, radii=RADII, seed=29)
+    table, rcp = skin_profile
+    _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
+    packet, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=2)
+    monkeypatch.setenv(knob, "1")
+    _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
+    assert np.array_equal(base, alt)
+    assert np.array_equal(base, packet)  # one running sum per band, the packet kernel's order
+    ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
+    assert _rel_close(base, ref, 2e-5), np.abs(base - ref).max()
+    assert np.any(ref > 0)
