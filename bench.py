@@ -359,7 +359,8 @@ def pmc_traffic(path, launch_ms):
     ceiling. Only a summary whose source_hash matches the current kernel sources is used; an
     older one is named as stale and its numbers are not attached."""
     import glob
-    # newest round tag first: r02z < r02aa (tags grow a letter), so order by length, then name
+    # newest round tag first: r02z < r02aa (tags grow a letter), so order by length, then name.
+    # Only C2 summaries are named *_pmc.json (other configs: *_pmc_<config>.json).
     cands = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")),
                                        key=lambda f: (len(os.path.basename(f)), os.path.basename(f)), reverse=True)
     want = kernel_source_hash()
