@@ -626,8 +626,8 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipS
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
             else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236)
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
+            else if (kw == 10236)  // the instrumented pass steals too (its counts do not depend on it)
+                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true, true, true>), grid1, dim3(1024), 0, stream, a);
             else
                 hipLaunchKernelGGL((mo_band_wave_kernel<true, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
         } else {
