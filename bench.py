@@ -233,11 +233,10 @@ def main(a):
     tl.render_items(ctx, mine, tiles, sc.spp, seeds, out_c, T, stream)
     cnt = ctx.render_stats()
     # the reference traversal's record visits: the same pass with the reach pruning off
-    os.environ["MPSS_MO_COUNT_NOPRUNE"] = "1"
+    ctx.set_instrumentation(kernel_timing=False, count_traversal=2)
     ctx.reset_render_stats()
     tl.render_items(ctx, mine, tiles, sc.spp, seeds, out_c, T, stream)
     cnt_ref = ctx.render_stats()
-    del os.environ["MPSS_MO_COUNT_NOPRUNE"]
     del out_c
     ctx.set_instrumentation(kernel_timing=True, count_traversal=False)
     ctx.reset_render_stats()

@@ -66,7 +66,10 @@ typedef struct {
                                   groups pinned to XCDs); 2: packet kernel. 0 and 2 evaluate the same
                                   terms with one running sum per band and agree bit for bit */
     int kernel_timing;         /* 1: time every render kernel with HIP events (mpss_get_render_stats) */
-    int count_traversal;       /* 1: shade kernel counts octree nodes / points it reads (slower) */
+    int count_traversal;       /* 1: the Mo() gather counts the octree nodes / points it reads (slower);
+                                  2: the same with the exact-zero reach pruning off, so every band
+                                  group walks exactly the records of the reference's Mo() recursion
+                                  (SURVEY 8d algorithmic bytes; results unchanged) */
     int profile_on_host;       /* 1: build LayeredSkin profiles and rho_hd tables on the host CPU
                                   (threads); 0 (default): on the GPU (profile_gpu.hip, rho_gpu.hip) */
     int64_t max_batch_samples; /* camera samples per render batch (default 1 << 26: a whole C2 frame
@@ -88,6 +91,13 @@ typedef struct {
     int octree_on_host;        /* 1: build the irradiance octree on the host (serial Insert in point
                                   order, octree.cpp); 0 (default): level-synchronous build on the GPU
                                   (octree_gpu.hip), the same tree bit for bit */
+    /* Choices of the spectrally sharded gather (exact_mo = 0). None changes a result bit. */
+    int mo_band_dealing;       /* 0 (default): the 30 bands dealt into 8 groups of adjacent profile
+                                  reach; 1: snake rounds (every group one of the 8 longest reaches) */
+    int mo_work_stealing;      /* 1 (default): a workgroup whose band group runs dry moves on to the
+                                  next group with work left; 0: each stays on its own group (XCD) */
+    int mo_near_field;         /* profile entries per band kept in LDS: 10236 (default; one workgroup
+                                  per CU holds the whole 160 KB) or 5088 (two workgroups per CU) */
 } mpss_config;
 
 enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };
@@ -268,7 +278,8 @@ typedef struct {
     int64_t mo_lookups, mo_lookups_near[3];
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
-/* Switch kernel_timing / count_traversal after creation (instrumented passes). */
+/* Switch kernel_timing / count_traversal (0, 1 or 2, as mpss_config) after creation
+ * (instrumented passes). */
 int mpss_set_instrumentation(mpss_ctx *ctx, int kernel_timing, int count_traversal);
 int mpss_reset_render_stats(mpss_ctx *ctx);
 

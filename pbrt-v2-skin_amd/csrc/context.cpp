@@ -12,6 +12,10 @@ Context::Context(const mpss_config &cfg) : cfg_(cfg) {
     if (cfg.device < 0 || cfg.device >= ndev)
         throw Error(MPSS_ERR_INVALID, "mpss_create: device ordinal " + std::to_string(cfg.device) +
                                           " out of range (" + std::to_string(ndev) + " HIP devices)");
+    if (cfg.mo_near_field != 10236 && cfg.mo_near_field != 5088)
+        throw Error(MPSS_ERR_INVALID, "mpss_create: mo_near_field must be 10236 or 5088");
+    if (cfg.mo_band_dealing != 0 && cfg.mo_band_dealing != 1)
+        throw Error(MPSS_ERR_INVALID, "mpss_create: mo_band_dealing must be 0 or 1");
     max_error_ = cfg.max_error;
     min_dist_ = cfg.min_sample_distance;
     if (cfg.quick_render) {  // multipolesubsurface.cpp:401 [file line]
@@ -78,8 +82,10 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
     const BandLayout *layout = nullptr;
     const Material *m = nullptr;
     int mode;
+    GatherOpts opts;
     {
         std::lock_guard<std::mutex> g(mu_);
+        opts = gather_opts();
         if (!have_octree_) throw Error(MPSS_ERR_INVALID, "no irradiance points: call mpss_set_irradiance_points first");
         if (mid >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(mid));
         m = materials_[mid].get();
@@ -103,7 +109,7 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         return;
     }
     int *perm = nullptr;
-    if (ws && wave_queue_enabled()) {
+    if (ws) {
         const int64_t need = ((int64_t)q + 1023) / 1024 * 1024;
         if (ws->perm_n < need) {
             if (ws->pending) MPSS_HIP(hipEventSynchronize(ws->done));
@@ -115,7 +121,7 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
     if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
     try {
         launch_mo_gather(dev_octree_, layout, m->dev_profile, max_error_, q, p_dev, out_dev, NB, counters_dev,
-                         ws ? ws->work.ptr : nullptr, stream, mode, perm);
+                         ws ? ws->work.ptr : nullptr, perm, mode, opts, stream);
     } catch (...) {
         if (ws) release_ws(ws, stream);
         throw;
@@ -181,7 +187,7 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     mat->ior = m.layer_ior[0];
     mat->double_ref_sslf = m.double_ref_sslf != 0;
     mat->is_monte_carlo = m.use_monte_carlo != 0;  // Ft = 1 in Li (multipolesubsurface.cpp:285)
-    mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
+    mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp, cfg_.mo_band_dealing == 1);
     if (mat->rgb) {
         mat->dev_rgb.upload(mat->profile.table.data(), 3 * (size_t)mat->profile.length);
         for (int k = 0; k < 3; ++k) mat->rgb_rcp[k] = mat->profile.rcp[k];
@@ -215,7 +221,7 @@ uint32_t Context::set_material_tables(const float *rd, uint32_t len, const float
         mat->Kt[c] = 0.f;
     }
     mat->is_monte_carlo = is_mc;
-    mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp);
+    mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp, cfg_.mo_band_dealing == 1);
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));
     scene_dirty_ = true;

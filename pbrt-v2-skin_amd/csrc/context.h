@@ -97,6 +97,13 @@ public:
     void set_material_textures(uint32_t material, int albedo, int bump);
     std::vector<const TexView *> host_bump_views() const;
     float max_error() const { return max_error_; }
+    GatherOpts gather_opts() const {
+        GatherOpts o;
+        o.near_field = cfg_.mo_near_field;
+        o.steal = cfg_.mo_work_stealing != 0;
+        o.count_noprune = cfg_.count_traversal == 2;
+        return o;
+    }
     const mpss_config &config() const { return cfg_; }
 
     // scene + per-pixel path (render_host.cpp)
@@ -125,7 +132,7 @@ public:
     bool has_octree() const { return have_octree_; }
     mpss_render_stats render_stats();
     void reset_render_stats();
-    void set_instrumentation(bool timing, bool counting) {
+    void set_instrumentation(bool timing, int counting) {
         std::lock_guard<std::mutex> g(mu_);
         cfg_.kernel_timing = timing;
         cfg_.count_traversal = counting;

@@ -14,13 +14,12 @@
 // per group, so consecutive pre-order records share lines); only the table lookups are per-lane
 // gathers (one 8-byte load per band: the lerp pair).
 //
-// What bounds it: VALU issue (profiles/r01i_pmc.json: 12.6 G wave-instructions per launch,
-// ~89 % of the chip's VALU issue rate), so the per-record instruction count and the fraction of
-// lanes doing useful work set the speed. The traversal is the UNION of the wave's 64 pruned
-// traversals, so the 64 queries of a wave should be neighbours: the kernel sorts each
-// 1024-query chunk by a Morton key of the query position before dealing queries to lanes
-// (mo_kernel.hip), and the per-record work below is kept to packed-f32 arithmetic on 32-bit
-// table offsets from one uniform base pointer.
+// What bounds it: the L2 request rate of the per-lane table gathers (the texture
+// address units are ~90 % busy and the requests run at ~0.93 of the rate a pure gather
+// microbenchmark sustains). The traversal is the UNION of the wave's 64 pruned traversals, so the
+// 64 queries of a wave should be neighbours: each 1024-query chunk is sorted by a Morton key of
+// the query position before queries are dealt to lanes (mo_kernel.hip), and the per-record work
+// below is kept to packed-f32 arithmetic on 32-bit table offsets.
 //
 // Each query walks exactly the node set of SubsurfaceOctreeNode::Mo (diffusionutil.h:175-210)
 // minus subtrees that lie past the end of all of the group's profiles (they add +0 for these
@@ -35,7 +34,6 @@
 namespace mpss {
 
 constexpr int kGroups = 8;
-constexpr int kBandBlock = 512;  // default queries per chunk / workgroup (MPSS_MO_BS)
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -46,9 +44,9 @@ struct BandGroups {
 
 // Deal bands to groups: bands sorted by decreasing profile reach (L-1)/rcp, then either runs of
 // adjacent reach (default: group g's bands share one prune radius, so few of its lookups fall
-// past a band's profile end) or snake rounds (0..7, 7..0, ...: every group gets one of the 8
-// longest-reaching bands, equal work per group).
-inline BandGroups make_band_groups(const float *rcp) {
+// past a band's profile end) or, with `snake` (mpss_config.mo_band_dealing = 1), snake rounds
+// (0..7, 7..0, ...: every group gets one of the 8 longest-reaching bands, equal work per group).
+inline BandGroups make_band_groups(const float *rcp, bool snake = false) {
     int order[NB];
     for (int c = 0; c < NB; ++c) order[c] = c;
     for (int i = 1; i < NB; ++i)  // insertion sort by increasing rcp (= decreasing reach)
@@ -66,8 +64,8 @@ inline BandGroups make_band_groups(const float *rcp) {
     // Groups of adjacent reach (6 x 4 + 2 x 3 bands, by decreasing reach): each group's prune radius
     // fits all of its bands, 29 % fewer record visits than dealing the bands in snake rounds; the
     // groups' unequal work is evened out by the gather's work stealing (C2: 41.1 -> 37.3 ms per
-    // frame, profiles/r02j_variants.txt r02bf). MPSS_MO_SNAKE=1 deals snake rounds instead.
-    const bool contig = getenv("MPSS_MO_SNAKE") == nullptr;
+    // frame, profiles/r02j_variants.txt r02bf).
+    const bool contig = !snake;
     for (int r = 0; r < NB; ++r) {
         const int round = r / kGroups, k = r % kGroups;
         const int grp = contig ? (r < 24 ? r / 4 : 6 + (r - 24) / 3) : ((round & 1) ? kGroups - 1 - k : k);
@@ -126,24 +124,23 @@ typedef __attribute__((address_space(3))) const float lds_float;  // ds_read, ne
 
 // The lane's view of its group's 4 bands: table offsets (floats from BandTree::table), rcp, and
 // the workgroup's LDS copy of the first entries of each band (the near field).
+// LDS rows hold KLDS + 3 floats per band slot: entries 0..klim of the band (klim = min(KLDS, L - 2)),
+// zeros after, and a zero pair at row offset KLDS + 1. Lanes with klim <= s < L - 1 read the table
+// in L2; all others read LDS -- s < klim the near field, s >= L - 1 (past the profile end:
+// sampleProfile returns 0) the zero pair. The LDS/L2 choice is one unsigned range test.
 struct BandLane {
     uint32_t off[4];  // c * L (an empty slot reads band 0 with rcp 0; its sum is never stored)
     float rcp[4];
-    uint32_t zero;    // NB * L: the trailing zero pair
     uint32_t lm1;     // L - 1: sampleProfile's range end
-    uint32_t klim;    // min(KLDS, L - 1): s < klim <=> the pair (s, s + 1) is in the LDS copy
-    const float *lt;  // LDS rows of KLDS + 2 floats per band slot (generic pointer)
-    // NEAR 5 (rows of KLDS + 3 floats): klim = min(KLDS, L - 2), gspan = L - 1 - klim; lanes with
-    // klim <= s < L - 1 read the table, all others LDS -- s < klim the near field, s >= L - 1
-    // (past the profile end) the zero pair at row offset KLDS + 1: one select less per band than
-    // NEAR 2's zero-index and near-field tests. tb[j]: the band's table row.
-    uint32_t gspan;
-    const float *tb[4];
+    uint32_t klim;    // min(KLDS, L - 2): s < klim <=> the pair (s, s + 1) is in the LDS copy
+    uint32_t gspan;   // L - 1 - klim: s - klim < gspan (unsigned) <=> the pair is read from L2
+    const float *lt;  // LDS rows (generic pointer)
+    const float *tb[4];  // the bands' table rows
 };
-// Row length (floats) of a band's LDS near field for near-field mode NEAR.
-template <int KLDS, int NEAR>
+// Row length (floats) of a band's LDS near field.
+template <int KLDS>
 __host__ __device__ constexpr int near_row() {
-    return NEAR == 5 ? KLDS + 3 : KLDS + 2;
+    return KLDS + 3;
 }
 
 // Rd lookups of one record for the lane's 4 bands, accumulated:
@@ -154,17 +151,13 @@ __host__ __device__ constexpr int near_row() {
 // test); a lane past the end reads the zero pair, so its term is (0 * e) * w = +0 and the
 // running sum (which starts at +0 and is never -0) is unchanged: no masking instruction. All
 // four lookups are issued before any is consumed; the products run as packed f32.
+// Each lane's pair is one flat load whose address lies in LDS or in the table: the L2 request
+// rate is what bounds the gather, and only lanes outside the near field make requests.
 // COUNT: hist[0] += lookups inside the profile, hist[1..3] += those with s < 4096, 8192, 16384
 // (how much a near-field copy of that many entries per band in LDS would absorb).
-// Near field (KLDS > 0): a lane whose pair lies in the LDS copy reads it there, the others read
-// the table in L2 -- NEAR 1: two loads under complementary exec masks (ds_read2_b32 /
-// global_load_dwordx2), NEAR 2: one flat load whose per-lane address is in LDS or in the table.
-// The L2 request rate is what bounds the gather (profiles/r02b_pmc.json), and only lanes outside
-// the near field make requests.
 // The fetch half: f per band and the four pair loads (issued, not consumed).
-template <bool COUNT, int KLDS, int NEAR>
-__device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, const BandLane &b, float d2, float f[4],
-                                              RdPair v[4], int hist[4]) {
+template <bool COUNT, int KLDS>
+__device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float f[4], RdPair v[4], int hist[4]) {
     const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
     const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
     f[0] = f01.x;
@@ -174,44 +167,10 @@ __device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, c
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t s = (uint32_t)f[j];  // saturating convert: f >= 2^32 -> 0xffffffff >= lm1
-        const uint32_t idx = s < b.lm1 ? b.off[j] + s : b.zero;
-        if (KLDS > 0 && NEAR == 5) {
-            const bool glob = s - b.klim < b.gspan;  // unsigned: s < klim wraps past gspan
-            const uint32_t li = s < (uint32_t)(KLDS + 1) ? s : (uint32_t)(KLDS + 1);
-            const float *src = glob ? b.tb[j] + s : b.lt + j * (KLDS + 3) + li;
-            v[j] = *reinterpret_cast<const RdPair *>(src);
-        } else if (KLDS > 0 && NEAR == 2) {
-            const float *src = s < b.klim ? b.lt + j * (KLDS + 2) + s : table + idx;
-            v[j] = *reinterpret_cast<const RdPair *>(src);
-        } else if (KLDS > 0 && NEAR == 4) {
-            // LDS and L2 loads into separate registers, then a select: the two masked loads do not
-            // write the same VGPRs, so neither waits for the other (NEAR 1 serializes on that WAW)
-            const bool near = s < b.klim;
-            RdPair g{0.f, 0.f}, l{0.f, 0.f};
-            if (!near) g = *reinterpret_cast<const RdPair *>(table + idx);
-            if (near) {
-                const lds_float *row = (const lds_float *)b.lt + j * (KLDS + 2) + s;
-                l.a = row[0];
-                l.b = row[1];
-            }
-            // exactly one of g, l is the (zero-initialized) other path's: the sum is the loaded pair
-            // (table entries are never -0), and it needs both registers live, so they stay apart
-            v[j].a = g.a + l.a;
-            v[j].b = g.b + l.b;
-        } else if (KLDS > 0) {
-            if (s < b.klim) {
-                const lds_float *row = (const lds_float *)b.lt + j * (KLDS + 2) + s;
-                v[j].a = row[0];
-                v[j].b = row[1];
-            } else {
-                v[j] = *reinterpret_cast<const RdPair *>(table + idx);
-            }
-        } else if (NEAR == 3) {  // no request for a lane past the profile end: its pair is (0, 0)
-            v[j].a = v[j].b = 0.f;
-            if (s < b.lm1) v[j] = *reinterpret_cast<const RdPair *>(table + b.off[j] + s);
-        } else {
-            v[j] = *reinterpret_cast<const RdPair *>(table + idx);
-        }
+        const bool glob = s - b.klim < b.gspan;  // unsigned: s < klim wraps past gspan
+        const uint32_t li = s < (uint32_t)(KLDS + 1) ? s : (uint32_t)(KLDS + 1);
+        const float *src = glob ? b.tb[j] + s : b.lt + j * near_row<KLDS>() + li;
+        v[j] = *reinterpret_cast<const RdPair *>(src);
         if (COUNT && s < b.lm1 && b.rcp[j] > 0.f) {
             ++hist[0];
             hist[1] += s < 4096u;
@@ -222,7 +181,7 @@ __device__ __forceinline__ void band_rd_fetch(const float *__restrict__ table, c
 }
 
 // A wave-uniform pointer held in VGPRs for the whole traversal (opaque to rematerialization): the
-// per-lane address select of NEAR 5 then reads the band's row base straight from registers instead
+// per-lane address select of the near-field fetch then reads the band's row base straight from registers instead
 // of re-copying it from SGPRs (v_cndmask takes one SGPR operand at most) for every lookup.
 __device__ __forceinline__ const float *in_vgprs(const float *p) {
     const uint64_t u = (uint64_t)(uintptr_t)p;
@@ -254,12 +213,12 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
     }
 }
 
-template <bool POINT, bool COUNT, int KLDS, int NEAR>
-__device__ __forceinline__ void band_rd_accumulate(const float *__restrict__ table, const BandLane &b, float d2,
-                                                   const float e[4], float w, f2v acc[2], int hist[4]) {
+template <bool POINT, bool COUNT, int KLDS>
+__device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
+                                                   int hist[4]) {
     float f[4];
     RdPair v[4];
-    band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2, f, v, hist);
+    band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
     band_rd_combine<POINT>(f, v, e, w, acc);
 }
 
@@ -278,10 +237,10 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 
 // COUNT: k_nodes / k_pts = this lane's node / point visits; w_nodes / w_pts = the wave's node-loop
 // and point-loop iterations (uniform).
-// PAIR: a leaf's points two at a time -- both points' eight pair loads issued before either's
+// A leaf's points are taken two at a time -- both points' eight pair loads issued before either's
 // terms are formed (the same terms, summed in the same order), so a wave waits out one L2 round
 // trip per two points.
-template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = false>
+template <bool COUNT, int KLDS, bool VROWS>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
                                                  int hist[4], const float *lt) {
@@ -292,18 +251,13 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         b.rcp[j] = a.grcp[grp][j];
         b.off[j] = (uint32_t)(c >= 0 ? c : 0) * (uint32_t)a.L;
     }
-    b.zero = (uint32_t)NB * (uint32_t)a.L;
     b.lm1 = (uint32_t)(a.L - 1);
-    b.klim = (uint32_t)KLDS < b.lm1 ? (uint32_t)KLDS : b.lm1;
-    if (NEAR == 5) {
-        const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
-        b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
-        b.gspan = b.lm1 - b.klim;
+    const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
+    b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
+    b.gspan = b.lm1 - b.klim;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b.tb[j] = VROWS ? in_vgprs(a.table + b.off[j]) : a.table + b.off[j];
-    }
+    for (int j = 0; j < 4; ++j) b.tb[j] = VROWS ? in_vgprs(a.table + b.off[j]) : a.table + b.off[j];
     b.lt = lt;
-    const float *__restrict__ table = a.table;
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     const float rcp_min = a.groups.rcp_min[grp];
     const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
@@ -337,7 +291,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-                    band_rd_accumulate<false, COUNT, KLDS, NEAR>(table, b, d2, e, 1.f, acc, hist);
+                    band_rd_accumulate<false, COUNT, KLDS>(b, d2, e, 1.f, acc, hist);
                 } else {
                     open = true;
                 }
@@ -351,8 +305,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 const int live = (int)h.pad;
                 if (COUNT) w_pts += live;
                 int i0 = 0;
-                if (PAIR)
-                    for (; i0 + 1 < live; i0 += 2) {
+                for (; i0 + 1 < live; i0 += 2) {
                         const int ka = h.leaf_first + i0, kb = ka + 1;
                         const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];
                         const float4 ea = e_g[ka], eb = e_g[kb];
@@ -364,8 +317,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
-                        band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2a, fa, va, hist);
-                        band_rd_fetch<COUNT, KLDS, NEAR>(table, b, d2b, fb, vb, hist);
+                        band_rd_fetch<COUNT, KLDS>(b, d2a, fa, va, hist);
+                        band_rd_fetch<COUNT, KLDS>(b, d2b, fb, vb, hist);
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         band_rd_combine<true>(fa, va, e0, pa.w, lacc);
                         band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
@@ -379,7 +332,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-                    band_rd_accumulate<true, COUNT, KLDS, NEAR>(table, b, d2, e, ph.w, lacc, hist);
+                    band_rd_accumulate<true, COUNT, KLDS>(b, d2, e, ph.w, lacc, hist);
                 }
                 acc[0] += lacc[0];
                 acc[1] += lacc[1];

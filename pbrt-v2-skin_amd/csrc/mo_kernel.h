@@ -46,7 +46,16 @@ struct DeviceProfile {
     int L = 0;
     float host_rcp[NB];
     BandGroups groups{};   // band -> XCD group assignment for this profile
-    void upload(const float *table, int L, const float *rcp);
+    // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
+    void upload(const float *table, int L, const float *rcp, bool snake = false);
+};
+
+// Choices of the sharded gather (mpss_config.mo_near_field / mo_work_stealing; count_noprune =
+// mpss_config.count_traversal == 2, instrumented passes only).
+struct GatherOpts {
+    int near_field = 10236;
+    bool steal = true;
+    bool count_noprune = false;
 };
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
@@ -54,20 +63,16 @@ struct DeviceProfile {
 // pruned-kernel nodes entered, points evaluated}. The packet kernel reports only
 // the last two (the first two are 0); mode 1 follows the reference summation order.
 // mode: 0 spectrally sharded (default; needs `layout` for p.groups), 1 exact reference order, 2 packet.
-// work: kGroups ints of device scratch for mode 0 (the persistent grid's chunk counters).
+// work: kGroups ints of device scratch for mode 0 (the persistent grid's chunk counters); perm:
+// >= nq rounded up to 1024 ints of device scratch for mode 0 (the sorted query permutation).
 void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
-                      const float *queries, float *out, int out_stride, int32_t *counters, int *work,
-                      hipStream_t stream, int mode, int *perm = nullptr);
+                      const float *queries, float *out, int out_stride, int32_t *counters, int *work, int *perm,
+                      int mode, const GatherOpts &opts, hipStream_t stream);
 
 // Mo with the closed-form single dipole (dipole.h) as Rd, in the reference summation order.
 // dipole_dev: [4][NB] device floats zpos, zneg, sigma_tr, k. Nothing is pruned.
 void launch_mo_dipole(const DeviceOctree &t, const float *dipole_dev, float max_error, int nq, const float *queries,
                       float *out, int out_stride, int32_t *counters, hipStream_t stream);
-
-// perm (nullable, >= nq rounded up to 1024 ints of device scratch): run the wave-queue gather
-// (mo_sort_kernel + mo_band_wave_kernel) instead of the chunk-per-workgroup kernel. Callers pass
-// it when wave_queue_enabled() (default; MPSS_MO_WAVEQ=0 turns it off).
-bool wave_queue_enabled();
 
 // Mo with an rgbprofile material (multipole.cpp:85-107): table3 [3][L] R, G, B profiles (device),
 // rcp3 their rcpDsqSpacing (device and host copies), in the reference summation order. Queries
@@ -87,10 +92,11 @@ constexpr int kStatStride = 8;
 // out4[i * 8 + g] = the 4 bands of group g (BandGroups::pos gives a band's float offset).
 // hit_s / mat (hit_s nullable): only queries whose hit_s material field equals mat are evaluated
 // (scenes with several BSSRDF materials run one launch per material). counts: see kStatStride.
-// work: kGroups ints of device scratch (the chunk counters of the persistent grid).
+// work: kGroups ints of device scratch (the chunk counters of the persistent grid); perm: >= nq_max
+// rounded up to 1024 ints of device scratch.
 void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
                     int nq_max, const float4 *queries4, const int *count_dev, float4 *out4,
-                    const uint32_t *hit_s, int mat, unsigned long long *counts, int *work, hipStream_t stream,
-                    int *perm = nullptr);
+                    const uint32_t *hit_s, int mat, unsigned long long *counts, int *work, int *perm,
+                    const GatherOpts &opts, hipStream_t stream);
 
 }  // namespace mpss

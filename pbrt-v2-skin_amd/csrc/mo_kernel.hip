@@ -291,13 +291,11 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Spectrally sharded gather (mo_band.h). Persistent grid: workgroup b runs band group b % 8
-// (one XCD under the round-robin dispatch) and takes 1024-query chunks from that group's
-// counter until the queries run out (the query count is read on the device: the render path's
-// compacted hit list). Each chunk is sorted by a Morton key of its query positions (bitonic
-// sort in LDS) before the queries are dealt to lanes, so the 64 queries of a wave are
-// neighbours and walk nearly the same records (the traversal is the union of the wave's);
-// every result goes to its query's own slot, so the order changes no bit of any result.
+// Spectrally sharded gather (mo_band.h), in two launches: mo_sort_kernel sorts each 1024-query
+// chunk by a Morton key of its query positions into a permutation, then the persistent
+// mo_band_wave_kernel deals 64 sorted queries at a time to waves. Workgroup b starts on band group
+// b % 8 (one XCD under the round-robin dispatch), so each XCD's L2 holds only its group's tables.
+// Every result goes to its query's own slot, so neither the order nor the stealing changes a bit.
 // ---------------------------------------------------------------------------------------
 
 struct BandArgs {
@@ -315,8 +313,7 @@ struct BandArgs {
     unsigned long long *__restrict__ counts;  // render COUNT: [kStatStride * kGroups]
     int *__restrict__ work;              // [kGroups] chunk counters (zeroed before the launch)
     float klo[3], kinv[3];               // Morton key quantization (octree root bounds)
-    int sort;                            // 0: keep slot order (MPSS_MO_SORT=0, a tuning knob)
-    int *perm;                           // wave-queue gather: chunk-sorted query ids (-1: none)
+    int *perm;                           // chunk-sorted query ids (-1: none), mo_sort_kernel
 };
 
 __device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, float &py, float &pz) {
@@ -335,85 +332,8 @@ __device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, 
     return true;
 }
 
-template <bool COUNT, int BS, int KLDS, int NEAR, bool PAIR>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(8, 8))) void mo_band_kernel(BandArgs a) {
-    __shared__ unsigned long long keys[BS];
-    __shared__ int chunk_s;
-    __shared__ float lt[KLDS > 0 ? 4 * (KLDS + 2) : 1];
-    const int grp = (int)(blockIdx.x & (kGroups - 1));
-    const int tid = (int)threadIdx.x;
-    const int nq = a.count ? *a.count : a.nq;
-    if (KLDS > 0) {
-        // the group's near field: entries 0..KLDS of each band (past the table end: 0). Every
-        // workgroup fills it: chunks go to whichever workgroup asks first, not by block index.
-        for (int i = tid; i < 4 * (KLDS + 2); i += BS) {
-            const int j = i / (KLDS + 2), k = i % (KLDS + 2), c = a.t.groups.band[grp][j];
-            lt[i] = (c >= 0 && k <= KLDS && k < a.t.L) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
-        }
-    }
-    for (;;) {
-        if (tid == 0) chunk_s = atomicAdd(&a.work[grp], 1);
-        __syncthreads();
-        const int base = chunk_s * BS;
-        if (base >= nq) return;  // uniform over the workgroup
-        float px = 0.f, py = 0.f, pz = 0.f;
-        const bool in = base + tid < nq && band_query(a, base + tid, px, py, pz);
-        const uint32_t key = in ? (a.sort ? morton30(px, py, pz, a.klo, a.kinv) : 0u) : 0xffffffffu;  // dead last
-        keys[tid] = ((unsigned long long)key << 32) | (unsigned)tid;
-        __syncthreads();
-        for (int k = 2; k <= BS; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const int ixj = tid ^ j;
-                if (ixj > tid) {
-                    const unsigned long long x = keys[tid], y = keys[ixj];
-                    if ((x > y) == ((tid & k) == 0)) {
-                        keys[tid] = y;
-                        keys[ixj] = x;
-                    }
-                }
-                __syncthreads();
-            }
-        const unsigned long long mine = keys[tid];
-        const int q = base + (int)(mine & 0xffffffffull);
-        const bool live = (mine >> 32) != 0xffffffffull;
-        if (live) band_query(a, q, px, py, pz);
-        float acc[4];
-        int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, NEAR, PAIR>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
-        if (live) {
-            if (a.out4) {
-                a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int c = a.t.groups.band[grp][j];
-                    if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
-                }
-            }
-        }
-        if (COUNT) {
-            if (a.counters && live) {
-                atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
-                atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
-            }
-            if (a.counts) {
-                if (kn) atomicAdd(&a.counts[kStatStride * grp], (unsigned long long)kn);
-                if (kp) atomicAdd(&a.counts[kStatStride * grp + 1], (unsigned long long)kp);
-                if ((tid & 63) == 0) {
-                    atomicAdd(&a.counts[kStatStride * grp + 2], (unsigned long long)wn);
-                    atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
-            }
-        }
-        __syncthreads();  // chunk_s and keys are rewritten by the next chunk
-    }
-}
-
-// Wave-queue gather, step 1: each 1024-query chunk sorted by the Morton key of its live queries
-// (as mo_band_kernel does in place), written as a permutation: perm[base + i] = the i-th query
+// Step 1: each 1024-query chunk sorted by the Morton key of its live queries, written as a
+// permutation: perm[base + i] = the i-th query
 // of the chunk in key order, -1 past the live ones. Chunks at or past the query count write nothing.
 __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
     __shared__ unsigned long long keys[1024];
@@ -423,7 +343,7 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
     if (base >= nq) return;  // uniform over the block
     float px = 0.f, py = 0.f, pz = 0.f;
     const bool in = base + tid < nq && band_query(a, base + tid, px, py, pz);
-    const uint32_t key = in ? (a.sort ? morton30(px, py, pz, a.klo, a.kinv) : 0u) : 0xffffffffu;
+    const uint32_t key = in ? morton30(px, py, pz, a.klo, a.kinv) : 0xffffffffu;  // dead last
     keys[tid] = ((unsigned long long)key << 32) | (unsigned)tid;
     __syncthreads();
     for (int k = 2; k <= 1024; k <<= 1)
@@ -445,17 +365,19 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
 // Step 2: every wave takes 64 consecutive entries of perm at a time from its group's counter and
 // walks them to the end on its own -- no workgroup barrier between chunks, so a wave with a short
 // traversal does not wait for the slowest wave of its workgroup. Same traversal, same sums.
-// Waves per SIMD the register allocation targets: 8 with two workgroups per CU; the 10236-entry near
-// field fills the LDS with one workgroup (4 waves per SIMD), so up to 128 VGPRs are free to use.
+// Waves per SIMD the register allocation targets: 8 with two workgroups per CU (the 5088-entry near
+// field); the 10236-entry near field fills the LDS with one workgroup (4 waves per SIMD), so up to
+// 128 VGPRs are free to use -- the bands' row bases then stay in VGPRs for the whole traversal.
 template <int KLDS>
 constexpr int wave_kernel_wpe() {
     return KLDS > 5088 ? 4 : 8;
 }
 
-template <bool COUNT, int KLDS, int NEAR, bool PAIR, bool VROWS = (KLDS > 5088), bool STEAL = false>
+template <bool COUNT, int KLDS, bool STEAL>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS>(), wave_kernel_wpe<KLDS>())))
 void mo_band_wave_kernel(BandArgs a) {
-    constexpr int ROWF = near_row<KLDS, NEAR>();
+    constexpr int ROWF = near_row<KLDS>();
+    constexpr bool VROWS = KLDS > 5088;
     __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
     __shared__ int next_grp;
     const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -485,9 +407,9 @@ void mo_band_wave_kernel(BandArgs a) {
         }
     }
     if (KLDS > 0) {
-        // entries 0..kmax of each band, zeros after (NEAR 5: kmax = min(KLDS, L - 2), and the last
-        // two floats of a row are the zero pair of the lanes past the profile end)
-        const int kmax = NEAR == 5 ? (KLDS < a.t.L - 2 ? KLDS : a.t.L - 2) : (KLDS < a.t.L - 1 ? KLDS : a.t.L - 1);
+        // entries 0..kmax of each band, kmax = min(KLDS, L - 2), zeros after (the last two floats of
+        // a row are the zero pair of the lanes past the profile end)
+        const int kmax = KLDS < a.t.L - 2 ? KLDS : a.t.L - 2;
         for (int i = tid; i < 4 * ROWF; i += 1024) {
             const int j = i / ROWF, k = i % ROWF, c = a.t.groups.band[grp][j];
             lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
@@ -505,7 +427,7 @@ void mo_band_wave_kernel(BandArgs a) {
         const bool live = q >= 0 && band_query(a, q, px, py, pz);
         float acc[4];
         int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, NEAR, PAIR, VROWS>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        mo_band_traverse<COUNT, KLDS, VROWS>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
         if (live) {
             if (a.out4) {
                 a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -538,139 +460,47 @@ void mo_band_wave_kernel(BandArgs a) {
     }
 }
 
-// Gather variant (tuning knobs; default 1024-query chunks, a 4096-entry near field read by
-// flat loads, a leaf's points two at a time): MPSS_MO_BS = 1024 | 512, MPSS_MO_K = LDS entries
-// per band (0, 2048, 4096, 9216), MPSS_MO_NEAR = 1 (masked ds/global loads into the same VGPRs:
-// every pair waits out the other) | 2 (flat loads) | 3 (no near field, no request past the
-// profile end) | 4 (masked ds/global loads into separate VGPRs), MPSS_MO_PAIR = 0 | 1,
-// MPSS_MO_SORT = 0 (no Morton sort). Measured on C2 (profiles/r02_variants.txt): flat 4096
-// 120 ms/frame, masked 4096 121, no near field 127, 512-query chunks 124-126, the 9216-entry near
-// field (one workgroup per CU) 140, no sort 128 (lane efficiency 0.47 vs 0.60); round 2e
-// (profiles/r02j_variants.txt, Msamples/s): flat 4096 544, + point pairs 550, + 2^26-sample
-// batches 568; no near field with pairs 467; separate-VGPR masked loads 542; 9216 with pairs 479.
-}  // namespace
-
-// Default on (C2: 48.0 vs 50.4 ms per launch, profiles/r02j_variants.txt); MPSS_MO_WAVEQ=0 runs the
-// chunk-per-workgroup kernel and its tuning knobs below.
-bool wave_queue_enabled() {
-    const char *e = getenv("MPSS_MO_WAVEQ");
-    return !e || atoi(e) != 0;
-}
-
-namespace {
-
-struct BandVariant {
-    int bs, k, near, pair;
-};
-BandVariant band_variant() {
-    BandVariant v{1024, 4096, 2, 1};
-    if (const char *e = getenv("MPSS_MO_BS")) v.bs = atoi(e);
-    if (const char *e = getenv("MPSS_MO_K")) v.k = atoi(e);
-    if (const char *e = getenv("MPSS_MO_NEAR")) v.near = atoi(e);
-    if (const char *e = getenv("MPSS_MO_PAIR")) v.pair = atoi(e);
-    return v;
-}
-
-template <int BS, int KLDS, int NEAR, bool PAIR = false>
-void launch_band_v(const BandArgs &a, int nq_max, bool count, hipStream_t stream) {
-    // persistent grid: enough resident workgroups per XCD (32 CUs) to fill it; late ones find no work
-    const int chunks = (nq_max + BS - 1) / BS;
-    const int cap = 32 * (2048 / BS);
-    const int per_group = chunks < cap ? chunks : cap;
-    if (per_group <= 0) return;
-    const dim3 grid((unsigned)(per_group * kGroups));
-    if (count)
-        hipLaunchKernelGGL((mo_band_kernel<true, BS, KLDS, NEAR, PAIR>), grid, dim3(BS), 0, stream, a);
+// The sharded gather: the sort launch, then the persistent wave-queue launch. opts.near_field picks
+// the LDS near field per band: 10236 entries (one 1024-thread workgroup per CU holding the whole
+// 160 KB; 32 workgroups per group) or 5088 (two workgroups per CU, 64 per group). opts.steal: a
+// workgroup whose group queue runs dry moves on to the next group with work left (C2: 42.5 ->
+// 41.2 ms per launch, profiles/r02j_variants.txt). opts.count_noprune (instrumented pass only):
+// the reach pruning off, so each group walks exactly the records the reference's Mo() recursion
+// reads (bench.py's SURVEY 8d algorithmic bytes).
+template <bool COUNT, int KLDS>
+void launch_wave(const BandArgs &a, dim3 grid, bool steal, hipStream_t stream) {
+    if (steal)
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true>), grid, dim3(1024), 0, stream, a);
     else
-        hipLaunchKernelGGL((mo_band_kernel<false, BS, KLDS, NEAR, PAIR>), grid, dim3(BS), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false>), grid, dim3(1024), 0, stream, a);
 }
 
-void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, hipStream_t stream) {
+void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, const GatherOpts &opts,
+                 hipStream_t stream) {
     if (nq_max <= 0) return;
+    if (!a.perm) throw Error(-2, "launch_band: the sharded gather needs its permutation scratch");
+    if (opts.near_field != 10236 && opts.near_field != 5088)
+        throw Error(-1, "mo_near_field must be 10236 or 5088");
     for (int k = 0; k < 3; ++k) {
         const float ext = t.bmax[k] - t.bmin[k];
         a.klo[k] = t.bmin[k];
         a.kinv[k] = ext > 0.f ? 1023.99f / ext : 0.f;
     }
     MPSS_HIP(hipMemsetAsync(a.work, 0, sizeof(int) * kGroups, stream));
-    // bench.py's reference-traversal count (SURVEY 8d algorithmic bytes): the instrumented pass with
-    // the reach pruning off visits exactly the records the reference's Mo() recursion reads
-    if (count && getenv("MPSS_MO_COUNT_NOPRUNE")) a.t.prune_f = INFINITY;
-    const BandVariant v = band_variant();
-    const char *so = getenv("MPSS_MO_SORT");
-    a.sort = so ? atoi(so) : 1;
-    if (a.perm) {  // wave-queue gather (the default config: 4096-entry flat near field, point pairs)
-        const int chunks = (nq_max + 1023) / 1024;
-        hipLaunchKernelGGL(mo_sort_kernel, dim3((unsigned)chunks), dim3(1024), 0, stream, a);
-        const char *wg = getenv("MPSS_MO_WGS");  // resident workgroups per group, 2 per CU (tuning knob)
-        const int cap = wg ? std::max(1, std::min(64, atoi(wg))) : 64;
-        const int per_group = chunks < cap ? chunks : cap;
-        const dim3 grid((unsigned)(per_group * kGroups));
-        // near field: the sort's 8 KB left the workgroup, so two workgroups per CU have room for
-        // 5088 entries per band (4 x 5090 floats = 79.5 KB each) -- MPSS_MO_WK=4096 keeps the old size
-        // near field per band: 10236 entries (default) -- one workgroup of 16 waves per CU holds the
-        // whole 160 KB LDS, 32 workgroups per group; the wave queue keeps the gather L2-bound at 4
-        // waves per SIMD (C2: 43.9 ms per launch vs 46.6 with two workgroups x 5088 entries,
-        // profiles/r02j_variants.txt), and past-end lanes read an LDS zero pair (NEAR 5: 42.9 vs
-        // 43.5 ms; MPSS_MO_WN2=1 keeps NEAR 2). MPSS_MO_WK=5088 | 4096: two workgroups per CU.
-        // Workgroups whose group queue runs dry move on to the next group with units left (the
-        // slowest group finished ~3 ms after the others: 42.5 -> 41.2 ms per C2 frame launch,
-        // profiles/r02j_variants.txt r02bd / r02be); MPSS_MO_NOSTEAL=1 keeps each on its own group.
-        const char *wk = getenv("MPSS_MO_WK");
-        const int kw = wk ? atoi(wk) : 10236;
-        const dim3 grid1((unsigned)((chunks < 32 ? chunks : 32) * kGroups));
-        if (count) {
-            if (kw == 4096)
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
-            else if (kw == 10236 && getenv("MPSS_MO_WN2"))
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236)  // the instrumented pass steals too (its counts do not depend on it)
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 10236, 5, true, true, true>), grid1, dim3(1024), 0, stream, a);
-            else
-                hipLaunchKernelGGL((mo_band_wave_kernel<true, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
-        } else {
-            if (kw == 4096)
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 4096, 2, true>), grid, dim3(1024), 0, stream, a);
-            else if (kw == 10236 && getenv("MPSS_MO_WN2"))
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 2, true>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236 && getenv("MPSS_MO_NOVROWS"))
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true, false>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236 && getenv("MPSS_MO_NOSTEAL"))
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true>), grid1, dim3(1024), 0, stream, a);
-            else if (kw == 10236)  // default: work stealing across groups (41.2 vs 42.5 ms per C2 frame launch)
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 10236, 5, true, true, true>), grid1, dim3(1024), 0, stream, a);
-            else
-                hipLaunchKernelGGL((mo_band_wave_kernel<false, 5088, 2, true>), grid, dim3(1024), 0, stream, a);
-        }
-        MPSS_HIP(hipGetLastError());
-        return;
-    }
-    if (v.pair && v.k == 0)
-        launch_band_v<1024, 0, 0, true>(a, nq_max, count, stream);
-    else if (v.pair && v.k == 9216)
-        launch_band_v<1024, 9216, 2, true>(a, nq_max, count, stream);
-    else if (v.pair && v.near == 4)
-        launch_band_v<1024, 4096, 4, true>(a, nq_max, count, stream);
-    else if (v.near == 4)
-        launch_band_v<1024, 4096, 4, false>(a, nq_max, count, stream);
-    else if (v.pair)
-        launch_band_v<1024, 4096, 2, true>(a, nq_max, count, stream);
-    else if (v.bs == 1024 && v.k == 0 && v.near == 3)
-        launch_band_v<1024, 0, 3>(a, nq_max, count, stream);
-    else if (v.bs == 1024 && v.k == 0)
-        launch_band_v<1024, 0, 0>(a, nq_max, count, stream);
-    else if (v.bs == 512 && v.k == 0)
-        launch_band_v<512, 0, 0>(a, nq_max, count, stream);
-    else if (v.bs == 512 && v.k == 2048)
-        launch_band_v<512, 2048, 1>(a, nq_max, count, stream);
-    else if (v.bs == 1024 && v.k == 9216)
-        launch_band_v<1024, 9216, 1>(a, nq_max, count, stream);
-    else if (v.near == 2)
-        launch_band_v<1024, 4096, 2>(a, nq_max, count, stream);
+    if (count && opts.count_noprune) a.t.prune_f = INFINITY;
+    const int chunks = (nq_max + 1023) / 1024;
+    hipLaunchKernelGGL(mo_sort_kernel, dim3((unsigned)chunks), dim3(1024), 0, stream, a);
+    const bool wide = opts.near_field == 10236;
+    const int cap = wide ? 32 : 64;  // resident workgroups per group: 1 or 2 per CU of an XCD
+    const dim3 grid((unsigned)((chunks < cap ? chunks : cap) * kGroups));
+    if (count && wide)
+        launch_wave<true, 10236>(a, grid, opts.steal, stream);
+    else if (count)
+        launch_wave<true, 5088>(a, grid, opts.steal, stream);
+    else if (wide)
+        launch_wave<false, 10236>(a, grid, opts.steal, stream);
     else
-        launch_band_v<1024, 4096, 1>(a, nq_max, count, stream);
+        launch_wave<false, 5088>(a, grid, opts.steal, stream);
     MPSS_HIP(hipGetLastError());
 }
 
@@ -770,7 +600,7 @@ void DeviceOctree::upload(const FlatOctree &t) {
     }
 }
 
-void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
+void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool snake) {
     // two zero floats after the last band: the sharded gather's read for "past the profile end"
     const size_t n = (size_t)NB * len;
     if (table.n != n + 2) table.alloc(n + 2);
@@ -781,7 +611,7 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_) {
     rcp_min = rcp_[0];
     for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
-    groups = make_band_groups(rcp_);
+    groups = make_band_groups(rcp_, snake);
 }
 
 const BandLayout *DeviceOctree::find_layout(const BandGroups &g) const {
@@ -810,7 +640,8 @@ const BandLayout &DeviceOctree::ensure_layout(const BandGroups &g) {
 
 void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const DeviceProfile &p, float max_error,
                     int nq_max, const float4 *queries4, const int *count_dev, float4 *out4, const uint32_t *hit_s,
-                    int mat, unsigned long long *counts, int *work, hipStream_t stream, int *perm) {
+                    int mat, unsigned long long *counts, int *work, int *perm, const GatherOpts &opts,
+                    hipStream_t stream) {
     if (nq_max <= 0 || t.n_nodes <= 0) return;
     BandArgs a{};
     a.t = band_tree(t, layout, p, max_error);
@@ -823,12 +654,12 @@ void launch_mo_band(const DeviceOctree &t, const BandLayout &layout, const Devic
     a.counts = counts;
     a.work = work;
     a.perm = perm;
-    launch_band(a, nq_max, t, counts != nullptr, stream);
+    launch_band(a, nq_max, t, counts != nullptr, opts, stream);
 }
 
 void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const DeviceProfile &p, float max_error, int nq,
-                      const float *queries, float *out, int out_stride, int32_t *counters, int *work,
-                      hipStream_t stream, int mode, int *perm) {
+                      const float *queries, float *out, int out_stride, int32_t *counters, int *work, int *perm,
+                      int mode, const GatherOpts &opts, hipStream_t stream) {
     const bool exact = mode == 1;
     if (nq <= 0) return;
     if (t.n_nodes <= 0) throw Error(-1, "launch_mo_gather: octree is empty");
@@ -846,7 +677,7 @@ void launch_mo_gather(const DeviceOctree &t, const BandLayout *layout, const Dev
         b.counters = counters;
         b.work = work;
         b.perm = perm;
-        launch_band(b, nq, t, count, stream);
+        launch_band(b, nq, t, count, opts, stream);
         return;
     }
     MoArgs a{};  // value-initialized: unused fields (render-path queries, functor tables) are null

@@ -42,10 +42,12 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 6; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 7; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
-                                          // 6: GPU octree build (octree_on_host), mpss_octree_export
+                                          // 6: GPU octree build (octree_on_host), mpss_octree_export;
+                                          // 7: gather choices in mpss_config (mo_band_dealing,
+                                          //    mo_work_stealing, mo_near_field), count_traversal 2
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -67,6 +69,9 @@ void mpss_config_defaults(mpss_config *c) {
     c->sampler = MPSS_SAMPLER_HASH;
     c->replay_cores = 8;
     c->octree_on_host = 0;
+    c->mo_band_dealing = 0;
+    c->mo_work_stealing = 1;
+    c->mo_near_field = 10236;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -308,7 +313,7 @@ int mpss_get_render_stats(mpss_ctx *c, mpss_render_stats *out) {
 int mpss_set_instrumentation(mpss_ctx *c, int timing, int counting) {
     return guarded([&] {
         require(c, "mpss_set_instrumentation: null ctx");
-        reinterpret_cast<Context *>(c)->set_instrumentation(timing != 0, counting != 0);
+        reinterpret_cast<Context *>(c)->set_instrumentation(timing != 0, counting);
     });
 }
 

@@ -575,6 +575,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     int ns_max = 1;
     for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
     const float max_error = max_error_;
+    const GatherOpts gopts = gather_opts();
     RenderWorkspace *ws = acquire_ws();
     lk.unlock();
 
@@ -648,7 +649,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 grow(ws->hs, have, total, 1);
                 ws->hits = total;
             }
-            if (wave_queue_enabled()) grow(ws->perm, ws->perm_n, (total + 1023) / 1024 * 1024, 1);
+            grow(ws->perm, ws->perm_n, (total + 1023) / 1024 * 1024, 1);
             if (sc.any_tex && ws->tex_hits < total) {
                 int64_t have = ws->tex_hits;
                 grow(ws->alb, have, total, 1);
@@ -742,7 +743,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                     else
                         launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)total, ws->q.ptr,
                                        ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
-                                       ws->work.ptr, stream, wave_queue_enabled() ? ws->perm.ptr : nullptr);
+                                       ws->work.ptr, ws->perm.ptr, gopts, stream);
                 }
                 time_end(timing, stream, ev, 2, timed);
             }

@@ -42,7 +42,8 @@ class Config(C.Structure):
                 ("incenter", C.c_int), ("quick_render", C.c_int), ("exact_mo", C.c_int),
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
                 ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int), ("sampler", C.c_int),
-                ("replay_cores", C.c_int), ("octree_on_host", C.c_int)]
+                ("replay_cores", C.c_int), ("octree_on_host", C.c_int), ("mo_band_dealing", C.c_int),
+                ("mo_work_stealing", C.c_int), ("mo_near_field", C.c_int)]
 
 SAMPLER_HASH, SAMPLER_REFERENCE = 0, 1
 
@@ -489,6 +490,8 @@ class Context:
         return out
 
     def set_instrumentation(self, kernel_timing=False, count_traversal=False):
+        """count_traversal: False/0, True/1 (the gather's own visits), or 2 (the reference
+        traversal's visits: reach pruning off, results unchanged)."""
         check(_lib.mpss_set_instrumentation(self.h, int(kernel_timing), int(count_traversal)))
 
     def reset_render_stats(self):

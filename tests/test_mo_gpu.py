@@ -44,9 +44,9 @@ def wide_profile():
     return tab, rcp
 
 
-def run_gpu(mpss, torch, cloud, table, rcp, q, max_error, exact=True, mode=None):
+def run_gpu(mpss, torch, cloud, table, rcp, q, max_error, exact=True, mode=None, **cfg):
     p, n, E, area = cloud
-    ctx = mpss.Context(max_error=max_error, exact_mo=int(exact) if mode is None else mode)
+    ctx = mpss.Context(max_error=max_error, exact_mo=int(exact) if mode is None else mode, **cfg)
     mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
     ctx.set_irradiance_points(p, n, E, area)
     qd = torch.from_numpy(q).cuda()
@@ -162,20 +162,28 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
         assert np.array_equal(band, fast), npts
 
 
-@pytest.mark.parametrize("knob", ["MPSS_MO_SNAKE", "MPSS_MO_NOSTEAL"])
-def test_mo_grouping_and_stealing_are_bit_identical(oracle, mpss, torch_dev, skin_profile, monkeypatch, knob):
-    """The default gather deals bands into adjacent-reach groups and lets workgroups steal other
-    groups' units; snake-round groups (MPSS_MO_SNAKE) and per-XCD groups (MPSS_MO_NOSTEAL) evaluate
-    the same non-zero terms in the same order, so every sum must match bit for bit (and the oracle)."""
+@pytest.mark.parametrize("cfg", [dict(mo_band_dealing=1), dict(mo_work_stealing=0), dict(mo_near_field=5088),
+                                 dict(mo_band_dealing=1, mo_work_stealing=0, mo_near_field=5088)])
+def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profile, cfg):
+    """The default gather deals bands into adjacent-reach groups, lets workgroups steal other
+    groups' units and keeps 10236 profile entries per band in LDS; snake-round groups
+    (mo_band_dealing 1), per-XCD groups (mo_work_stealing 0) and the two-workgroups-per-CU near
+    field (mo_near_field 5088) evaluate the same non-zero terms in the same order, so every sum
+    must match bit for bit (and the oracle)."""
     cloud = synth.ellipsoid_cloud(120000, radii=RADII, seed=23, black_frac=0.05)
     q = synth.surface_queries(20000, radii=RADII, seed=29)
     table, rcp = skin_profile
     _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
     packet, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=2)
-    monkeypatch.setenv(knob, "1")
-    _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
+    _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
     assert np.array_equal(base, alt)
     assert np.array_equal(base, packet)  # one running sum per band, the packet kernel's order
     ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
     assert _rel_close(base, ref, 2e-5), np.abs(base - ref).max()
     assert np.any(ref > 0)
+
+
+def test_mo_gather_rejects_bad_choices(mpss, torch_dev):
+    for cfg in (dict(mo_near_field=4096), dict(mo_band_dealing=2)):
+        with pytest.raises(mpss.MpssError):
+            mpss.Context(**cfg)
