@@ -176,12 +176,29 @@ long o_tessellate(const o_scene *s, float min_dist, int incenter, o_surface_poin
  * sample j: light pos u0, u1, BSDF component, BSDF dir u0, u1. li_draws: RNG values Li draws per
  * camera-ray hit (6 with maxdepth > 0). Returns K; vals may be NULL to query it. */
 int o_replay_render_table(o_scene *s, int spp, int cores, int li_draws, int nthreads, float *vals);
+/* The same for the pixels [vx0, vx1) x [vy0, vy1) of the sample extent only: row of pixel (x, y),
+ * sample i at vals[(((y - vy0) * (vx1 - vx0) + x - vx0) * spp + i) * K]; tasks whose sub-window
+ * misses the window are not run. */
+int o_replay_render_table_window(o_scene *s, int spp, int cores, int li_draws, int nthreads, int vx0, int vx1,
+                                 int vy0, int vy1, float *vals);
 /* IrradianceTask's RNG(47 k) scrambles: scr[(i * nlights + l) * 2 + {0, 1}] */
 void o_replay_irradiance_scr(int n, int nlights, int cores, uint32_t *scr);
 /* o_irradiance / o_render_tile with the reference sampler's values instead of counter hashes */
 void o_irradiance_replay(o_scene *s, int n, const o_surface_point *pts, const uint32_t *scr, int nthreads, float *E);
 void o_render_tile_replay(o_scene *s, int spp, const float *vals, int K, int x0, int x1, int y0, int y1,
                           int nthreads, float *xyzw);
+/* o_render_tile_replay with a windowed table (o_replay_render_table_window's window) */
+void o_render_tile_replay_window(o_scene *s, int spp, const float *vals, int K, int vx0, int vx1, int vy0, int vy1,
+                                 int x0, int x1, int y0, int y1, int nthreads, float *xyzw);
+/* CPU baseline: SamplerRenderer::Render's task loop -- the sub-windows order[0..norder) of
+ * nTasks = norder tasks (o_render_task_count) taken from one shared counter by nthreads workers
+ * until `seconds` pass; hash sampler. Returns pixels rendered; *tasks_done, *elapsed (s). */
+long o_cpu_baseline(o_scene *s, int spp, uint32_t seed, int cores, int nthreads, double seconds, const int *order,
+                    int norder, long *tasks_done, double *elapsed);
+/* RoundUpPow2(max(32 * cores, xres * yres / 256)) (samplerrenderer.cpp:206-207) */
+int o_render_task_count(int xres, int yres, int cores);
+/* Sampler::ComputeSubWindow (sampler.cpp:55-78): out = x0, x1, y0, y1 */
+void o_sub_window(int num, int count, int xs, int xe, int ys, int ye, int *out);
 void o_irradiance(o_scene *s, int n, const o_surface_point *pts, uint32_t seed, int nthreads, float *E);
 void o_scene_set_octree(o_scene *s, int n, const float *p, const float *nrm, const float *E, const float *area,
                         float max_error);

@@ -25,6 +25,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "oracle.h"
 #include "../data/spectral_bands.h"
@@ -1454,6 +1455,7 @@ typedef struct {
     float *out;
     const float *vals; /* reference-sampler table (o_replay_render_table) or NULL */
     int K;
+    int vx0, vy0, vw;  /* the table's window: origin pixel and width (whole extent: 0, 0, xres + 1) */
 } tile_job;
 
 /* One pixel: its own samples, then neighbours' samples whose rounded image position lands
@@ -1472,8 +1474,8 @@ static void render_pixel(const tile_job *j, int px, int py, float *o4) {
             const float *row = NULL;
             float X, Y;
             if (j->vals) { /* imageX = xPos + imageSamples[2 i] (montecarlo.cpp:236-237) */
-                row = j->vals + (((size_t)qy * (size_t)(s->xres + 1) + (size_t)qx) * (size_t)j->spp + (size_t)si) *
-                                    (size_t)j->K;
+                row = j->vals + (((size_t)(qy - j->vy0) * (size_t)j->vw + (size_t)(qx - j->vx0)) * (size_t)j->spp +
+                                 (size_t)si) * (size_t)j->K;
                 X = (float)qx + row[0];
                 Y = (float)qy + row[1];
             } else {
@@ -1505,13 +1507,13 @@ static void *tile_worker(void *arg) {
     return NULL;
 }
 
-static void render_run(o_scene *s, int spp, uint32_t seed, const float *vals, int K, int x0, int x1, int y0, int y1,
-                       int nthreads, float *xyzw) {
+static void render_run(o_scene *s, int spp, uint32_t seed, const float *vals, int K, int vx0, int vy0, int vw, int x0,
+                       int x1, int y0, int y1, int nthreads, float *xyzw) {
     scene_prepare(s);
     if (nthreads < 1) nthreads = 1;
     tile_job *jobs = (tile_job *)malloc(nthreads * sizeof(tile_job));
     for (int t = 0; t < nthreads; ++t) {
-        tile_job j = {s, spp, x0, x1, y0, y1, nthreads, t, seed, xyzw, vals, K};
+        tile_job j = {s, spp, x0, x1, y0, y1, nthreads, t, seed, xyzw, vals, K, vx0, vy0, vw};
         jobs[t] = j;
     }
     run_threads(tile_worker, jobs, sizeof(tile_job), nthreads);
@@ -1519,12 +1521,111 @@ static void render_run(o_scene *s, int spp, uint32_t seed, const float *vals, in
 }
 
 void o_render_tile(o_scene *s, int spp, uint32_t seed, int x0, int x1, int y0, int y1, int nthreads, float *xyzw) {
-    render_run(s, spp, seed, NULL, 0, x0, x1, y0, y1, nthreads, xyzw);
+    render_run(s, spp, seed, NULL, 0, 0, 0, 0, x0, x1, y0, y1, nthreads, xyzw);
 }
 
 void o_render_tile_replay(o_scene *s, int spp, const float *vals, int K, int x0, int x1, int y0, int y1,
                           int nthreads, float *xyzw) {
-    render_run(s, spp, 0, vals, K, x0, x1, y0, y1, nthreads, xyzw);
+    render_run(s, spp, 0, vals, K, 0, 0, s->xres + 1, x0, x1, y0, y1, nthreads, xyzw);
+}
+
+void o_render_tile_replay_window(o_scene *s, int spp, const float *vals, int K, int vx0, int vx1, int vy0, int vy1,
+                                 int x0, int x1, int y0, int y1, int nthreads, float *xyzw) {
+    (void)vy1;
+    render_run(s, spp, 0, vals, K, vx0, vy0, vx1 - vx0, x0, x1, y0, y1, nthreads, xyzw);
+}
+
+/* ---- the CPU baseline: SamplerRenderer::Render's task loop (samplerrenderer.cpp:191-225) ----
+ * nTasks = RoundUpPow2(max(32 * cores, W * H / 256)) sub-windows (Sampler::ComputeSubWindow of the
+ * image), taken from one shared counter by a pool of nthreads workers (parallel.cpp's task queue)
+ * in the order order[0..ntasks) until `seconds` have passed; each task renders its pixels with the
+ * hash sampler into a private buffer. Returns the pixels rendered; tasks_done / elapsed out. */
+typedef struct {
+    o_scene *s;
+    int spp, ntasks, cores;
+    uint32_t seed;
+    const int *order;
+    double deadline;
+    int next;
+    long pixels, tasks;
+    pthread_mutex_t mu;
+} base_job;
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void sub_window(int num, int count, int xs, int xe, int ys, int ye, int *x0, int *x1, int *y0, int *y1);
+
+static void *base_worker(void *arg) {
+    base_job *b = (base_job *)arg;
+    o_scene *s = b->s;
+    tile_job j = {s, b->spp, 0, 0, 0, 0, 1, 0, b->seed, NULL, NULL, 0, 0, 0, 0};
+    float *buf = NULL;
+    size_t cap = 0;
+    long px = 0, nt = 0;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        int k = b->next < b->ntasks && now_s() < b->deadline ? b->next++ : -1;
+        pthread_mutex_unlock(&b->mu);
+        if (k < 0) break;
+        int x0, x1, y0, y1;
+        sub_window(b->order[k], b->ntasks, 0, s->xres, 0, s->yres, &x0, &x1, &y0, &y1);
+        size_t n = (size_t)(x1 - x0) * (size_t)(y1 - y0);
+        if (n > cap) {
+            free(buf);
+            cap = n;
+            buf = (float *)malloc(4 * sizeof(float) * cap);
+        }
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) render_pixel(&j, x, y, &buf[4 * ((size_t)(y - y0) * (x1 - x0) + (x - x0))]);
+        px += (long)n;
+        ++nt;
+    }
+    free(buf);
+    pthread_mutex_lock(&b->mu);
+    b->pixels += px;
+    b->tasks += nt;
+    pthread_mutex_unlock(&b->mu);
+    return NULL;
+}
+
+long o_cpu_baseline(o_scene *s, int spp, uint32_t seed, int cores, int nthreads, double seconds, const int *order,
+                    int norder, long *tasks_done, double *elapsed) {
+    scene_prepare(s);
+    if (nthreads < 1) nthreads = 1;
+    base_job b;
+    memset(&b, 0, sizeof(b));
+    b.s = s;
+    b.spp = spp;
+    b.seed = seed;
+    b.cores = cores;
+    b.ntasks = norder;
+    b.order = order;
+    pthread_mutex_init(&b.mu, NULL);
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    double t0 = now_s();
+    b.deadline = t0 + seconds;
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, base_worker, &b);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    *elapsed = now_s() - t0;
+    *tasks_done = b.tasks;
+    free(th);
+    pthread_mutex_destroy(&b.mu);
+    return b.pixels;
+}
+
+/* nTasks of SamplerRenderer::Render for an image and a core count */
+int o_render_task_count(int xres, int yres, int cores) {
+    int a = 32 * cores, b = (int)(((long)xres * yres) / (16 * 16)), m = a > b ? a : b, r = 1;
+    while (r < m) r <<= 1;
+    return r;
+}
+
+void o_sub_window(int num, int count, int xs, int xe, int ys, int ye, int *out) {
+    sub_window(num, count, xs, xe, ys, ye, &out[0], &out[1], &out[2], &out[3]);
 }
 
 /* ------------------------------------------------------------------ the reference sampler */
@@ -1582,6 +1683,7 @@ typedef struct {
     o_scene *s;
     int spp, K, li_draws, ntasks, next;
     float *vals;
+    int vx0, vx1, vy0, vy1;  /* rows are kept for pixels of this window of the sample extent */
     pthread_mutex_t mu;
 } rtab_job;
 
@@ -1594,6 +1696,9 @@ static void render_task(rtab_job *jb, int task) {
     int x0, x1, y0, y1;
     sub_window(task, jb->ntasks, 0, W1, 0, H1, &x0, &x1, &y0, &y1);
     if (x0 == x1 || y0 == y1) return; /* GetSubSampler returns NULL */
+    /* a task's stream is its own (RNG(taskNum)): tasks outside the window are skipped whole */
+    if (x1 <= jb->vx0 || x0 >= jb->vx1 || y1 <= jb->vy0 || y0 >= jb->vy1) return;
+    const int vw = jb->vx1 - jb->vx0;
     o_mt rng;
     o_mt_seed(&rng, (uint32_t)task);
     /* n1D: per light comp (L), comp (BSDF); then the emission integrator's 1, 1. n2D: pos, dir. */
@@ -1617,8 +1722,9 @@ static void render_task(rtab_job *jb, int task) {
             ld_shuffle_scrambled_1d(1, spp, time, &rng);
             for (int a = 0; a < c1; ++a) ld_shuffle_scrambled_1d(n1[a], spp, one[a], &rng);
             for (int a = 0; a < c2; ++a) ld_shuffle_scrambled_2d(n2[a], spp, two[a], &rng);
-            for (int i = 0; i < spp; ++i) {
-                float *row = jb->vals + (((size_t)y * W1 + x) * spp + i) * K;
+            const int keep = x >= jb->vx0 && x < jb->vx1 && y >= jb->vy0 && y < jb->vy1;
+            for (int i = 0; keep && i < spp; ++i) {
+                float *row = jb->vals + (((size_t)(y - jb->vy0) * vw + (x - jb->vx0)) * spp + i) * K;
                 row[0] = image[2 * i];
                 row[1] = image[2 * i + 1];
                 for (int l = 0; l < nl; ++l) {
@@ -1660,7 +1766,15 @@ static void *rtab_worker(void *arg) {
 
 static int round_pow2_int(int v) { int r = 1; while (r < v) r <<= 1; return r; }
 
+int o_replay_render_table_window(o_scene *s, int spp, int cores, int li_draws, int nthreads, int vx0, int vx1,
+                                 int vy0, int vy1, float *vals);
+
 int o_replay_render_table(o_scene *s, int spp, int cores, int li_draws, int nthreads, float *vals) {
+    return o_replay_render_table_window(s, spp, cores, li_draws, nthreads, 0, s->xres + 1, 0, s->yres + 1, vals);
+}
+
+int o_replay_render_table_window(o_scene *s, int spp, int cores, int li_draws, int nthreads, int vx0, int vx1,
+                                 int vy0, int vy1, float *vals) {
     int K = 2;
     for (int l = 0; l < s->nlights; ++l) {
         s->lights[l].replay_off = K;
@@ -1673,6 +1787,7 @@ int o_replay_render_table(o_scene *s, int spp, int cores, int li_draws, int nthr
     rtab_job jb;
     memset(&jb, 0, sizeof(jb));
     jb.s = s; jb.spp = spp; jb.K = K; jb.li_draws = li_draws; jb.vals = vals;
+    jb.vx0 = vx0; jb.vx1 = vx1; jb.vy0 = vy0; jb.vy1 = vy1;
     jb.ntasks = round_pow2_int(a > b ? a : b);
     pthread_mutex_init(&jb.mu, NULL);
     if (nthreads < 1) nthreads = 1;

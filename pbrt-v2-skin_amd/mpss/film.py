@@ -160,3 +160,30 @@ def write_exr(path, rgb, total_res=None, offset=(0, 0), compression="zip"):
         f.write(struct.pack("<%dQ" % len(offs), *offs))
         for b in blocks:
             f.write(b)
+
+
+def exrdiff(im1, im2, tol=0.0):
+    """pbrt's exrdiff tool (src/tools/exrdiff.cpp:73-109) on two RGB(A) images as WriteImageEXR
+    stores them (HALF channels, alpha 1): per channel value, skipping alpha and values that are 0
+    in both, d = |a - b| / a counts as a small difference above 0.5 % and a big one above 5 %;
+    avgDelta = (avg1 - avg2) / min(avg1, avg2) of the channel sums over 3 W H. The images "differ"
+    (exrdiff exits 1) when tol == 0 and any small/big difference exists, or when tol > 0 and
+    100 |avgDelta| > tol (tol in percent, the tool's -d). Returns the tool's report as a dict."""
+    a = np.asarray(im1, np.float32)[..., :3].astype(np.float16).astype(np.float32)
+    b = np.asarray(im2, np.float32)[..., :3].astype(np.float16).astype(np.float32)
+    if a.shape != b.shape:
+        raise ValueError("resolutions don't match: %s vs %s" % (a.shape, b.shape))
+    h, w, _ = a.shape
+    live = ~((a == 0) & (b == 0))
+    av, bv = a[live].astype(np.float64), b[live].astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = (np.abs(a[live] - b[live]) / a[live]).astype(np.float32)  # fabsf(...) / im1[i] in float
+    small, big = int((d > 0.005).sum()), int((d > 0.05).sum())
+    n3 = 3.0 * w * h
+    avg1, avg2 = av.sum() / n3, bv.sum() / n3
+    delta = (avg1 - avg2) / min(avg1, avg2)
+    mse = float(((av - bv) ** 2).sum() / n3)
+    differ = (tol == 0.0 and (big > 0 or small > 0)) or (tol > 0.0 and 100.0 * abs(delta) > tol)
+    return {"differ": bool(differ), "small": small, "big": big, "small_pct": 100.0 * small / n3,
+            "big_pct": 100.0 * big / n3, "avg1": avg1, "avg2": avg2, "avg_delta_pct": 100.0 * delta,
+            "mse": mse, "rms_pct": 100.0 * np.sqrt(mse), "tol_pct": tol}

@@ -57,6 +57,15 @@ def _lib():
     L.o_replay_irradiance_scr.argtypes = [C.c_int, C.c_int, C.c_int, vp]
     L.o_irradiance_replay.argtypes = [vp, C.c_int, vp, vp, C.c_int, f32p]
     L.o_render_tile_replay.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, f32p]
+    L.o_replay_render_table_window.restype = C.c_int
+    L.o_replay_render_table_window.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int] + [C.c_int] * 4 + [vp]
+    L.o_render_tile_replay_window.argtypes = [vp, C.c_int, vp, C.c_int] + [C.c_int] * 9 + [f32p]
+    L.o_cpu_baseline.restype = C.c_long
+    L.o_cpu_baseline.argtypes = [vp, C.c_int, C.c_uint32, C.c_int, C.c_int, C.c_double, vp, C.c_int,
+                                 C.POINTER(C.c_long), C.POINTER(C.c_double)]
+    L.o_render_task_count.restype = C.c_int
+    L.o_render_task_count.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.o_sub_window.argtypes = [C.c_int] * 6 + [vp]
     L._render_sigs = True
     return L
 
@@ -205,19 +214,43 @@ class OracleScene:
         L.o_replay_render_table(self.h, spp, cores, li_draws, nthreads or os.cpu_count(), vals.ctypes.data)
         return vals
 
-    def irradiance_replay(self, pts, cores=8, nthreads=None):
+    def replay_window(self, x0, x1, y0, y1):
+        """The sample-extent pixels a tile's film needs: the tile plus a one-pixel border."""
+        return (max(x0 - 1, 0), min(x1 + 1, self.sc.xres + 1), max(y0 - 1, 0), min(y1 + 1, self.sc.yres + 1))
+
+    def replay_table_window(self, spp, window, cores=8, li_draws=6, nthreads=None):
+        """replay_table restricted to window = (vx0, vx1, vy0, vy1) of the sample extent (only the
+        render tasks whose sub-window meets it run): (vy1-vy0, vx1-vx0, spp, K) float32."""
+        L = _lib()
+        vx0, vx1, vy0, vy1 = window
+        K = L.o_replay_render_table(self.h, spp, cores, li_draws, 1, None)
+        vals = np.zeros((vy1 - vy0, vx1 - vx0, spp, K), np.float32)
+        L.o_replay_render_table_window(self.h, spp, cores, li_draws, nthreads or os.cpu_count(), vx0, vx1, vy0, vy1,
+                                       vals.ctypes.data)
+        return vals
+
+    def irradiance_replay(self, pts, cores=8, nthreads=None, n_total=None):
+        """IrradianceTask with the reference sampler's RNG(47 k) scrambles; pts may be a prefix of
+        n_total points (the task split depends on the whole point count)."""
         pts = np.ascontiguousarray(pts, SURFACE_POINT)
-        scr = np.zeros((len(pts), max(1, len(self.sc.lights)), 2), np.uint32)
-        _lib().o_replay_irradiance_scr(len(pts), len(self.sc.lights), cores, scr.ctypes.data)
+        n_total = n_total or len(pts)
+        scr = np.zeros((n_total, max(1, len(self.sc.lights)), 2), np.uint32)
+        _lib().o_replay_irradiance_scr(n_total, len(self.sc.lights), cores, scr.ctypes.data)
+        scr = np.ascontiguousarray(scr[:len(pts)])
         E = np.zeros((len(pts), NB), np.float32)
         _lib().o_irradiance_replay(self.h, len(pts), pts.ctypes.data, scr.ctypes.data, nthreads or os.cpu_count(), E)
         return E
 
-    def render_tile_replay(self, spp, vals, x0, x1, y0, y1, nthreads=None):
+    def render_tile_replay(self, spp, vals, x0, x1, y0, y1, nthreads=None, window=None):
+        """vals: replay_table (whole extent) or, with window, replay_table_window(window)."""
         vals = np.ascontiguousarray(vals, np.float32)
         out = np.zeros(((y1 - y0) * (x1 - x0) * 4,), np.float32)
-        _lib().o_render_tile_replay(self.h, spp, vals.ctypes.data, vals.shape[-1], x0, x1, y0, y1,
-                                    nthreads or os.cpu_count(), out)
+        if window is None:
+            _lib().o_render_tile_replay(self.h, spp, vals.ctypes.data, vals.shape[-1], x0, x1, y0, y1,
+                                        nthreads or os.cpu_count(), out)
+        else:
+            _lib().o_render_tile_replay_window(self.h, spp, vals.ctypes.data, vals.shape[-1], *window, x0, x1, y0, y1,
+                                               nthreads or os.cpu_count(), out)
         return out.reshape(y1 - y0, x1 - x0, 4)
 
     def set_octree(self, pts, E):
@@ -232,30 +265,38 @@ class OracleScene:
         return out.reshape(y1 - y0, x1 - x0, 4)
 
 
+def render_task_count(xres, yres, cores):
+    return _lib().o_render_task_count(xres, yres, cores)
+
+
+def sub_window(num, count, xs, xe, ys, ye):
+    out = np.zeros(4, np.int32)
+    _lib().o_sub_window(num, count, xs, xe, ys, ye, out.ctypes.data)
+    return tuple(int(v) for v in out)
+
+
 def time_cpu_baseline(sc, ctx, spp, seed, seconds, nthreads=None):
-    """Time the oracle's pixel loop on a bounded, frame-representative sample: 16x16 tiles
-    visited in a fixed pseudo-random order over the whole frame, using the product's
-    Preprocess outputs (surface points + irradiance) for the octree."""
+    """Time the oracle's pixel loop the way SamplerRenderer::Render runs (samplerrenderer.cpp:
+    191-225): nTasks = RoundUpPow2(max(32 * cores, W * H / 256)) sub-windows of the frame, pulled
+    from one shared counter by a pool of one worker per host core, in a fixed random order until
+    `seconds` pass (a bounded sample of the same frame). The octree is built from the product's
+    Preprocess outputs (surface points + irradiance); Preprocess is not timed."""
     import mpss
-    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    cores = os.cpu_count() or 1
+    nthreads = nthreads or cores
     osc = OracleScene(sc, tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
     osc.set_octree(ctx.surface_points(), ctx.irradiance())
-    T = 16
-    tiles = [(x, y) for y in range(0, sc.yres, T) for x in range(0, sc.xres, T)]
-    rng = np.random.default_rng(1234)
-    order = rng.permutation(len(tiles))
-    px = ntiles = 0
-    t0 = time.perf_counter()
-    for k in order:
-        x, y = tiles[k]
-        x1, y1 = min(x + T, sc.xres), min(y + T, sc.yres)
-        osc.render_tile(spp, seed, x, x1, y, y1, nthreads)
-        px += (x1 - x) * (y1 - y)
-        ntiles += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
+    ntasks = render_task_count(sc.xres, sc.yres, cores)
+    order = np.random.default_rng(1234).permutation(ntasks).astype(np.int32)
+    tasks, el = C.c_long(), C.c_double()
+    px = _lib().o_cpu_baseline(osc.h, spp, seed, cores, nthreads, float(seconds), order.ctypes.data, ntasks,
+                               C.byref(tasks), C.byref(el))
     osc.close()
+    dt = el.value
     return {"value": round(px * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": nthreads, "kind": "port",
-            "sample": "%d of %d 16x16 tiles (%d px x %d spp) of the same frame in fixed random order, %.1f s, "
-                      "oracle/render.c (scalar C restatement, pthreads)" % (ntiles, len(tiles), px, spp, dt)}
+            "nproc": cores,
+            "sample": "%d of %d render tasks (pbrt's split RoundUpPow2(max(32 x %d cores, W*H/256)), %d px x %d spp, "
+                      "%.1f %% of the frame) in fixed random order, one pool of %d threads, %.1f s; oracle/render.c "
+                      "(scalar C restatement, pthreads)" % (tasks.value, ntasks, cores, px, spp,
+                                                           100.0 * px / (sc.xres * sc.yres), nthreads, dt),
+            "frame_fraction": round(px / float(sc.xres * sc.yres), 4)}

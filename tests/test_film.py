@@ -106,3 +106,21 @@ def test_write_image_dispatch(tmp_path):
     assert (tmp_path / "b.PFM").read_bytes().startswith(b"PF\n")
     with pytest.raises(ValueError):
         film.write_image(str(tmp_path / "b.png"), rgb)
+
+
+def test_exrdiff_restatement():
+    """exrdiff.cpp:73-109: per-value relative difference thresholds (0.5 %, 5 %) and the mean-delta
+    tolerance (-d, percent)."""
+    from mpss import film
+    a = np.ones((4, 5, 3), np.float32)
+    b = a.copy()
+    r = film.exrdiff(a, b)
+    assert not r["differ"] and r["small"] == 0 and r["avg_delta_pct"] == 0.0
+    b[0, 0, 0] = 1.01   # 1 % off: small only
+    b[1, 1, 1] = 1.1    # 10 % off: small and big
+    r = film.exrdiff(a, b)
+    assert r["differ"] and r["small"] == 2 and r["big"] == 1
+    assert r["avg_delta_pct"] == pytest.approx(-100 * (0.01 + 0.1) / 60 / (1 + 0.11 / 60), rel=1e-2)
+    assert not film.exrdiff(a, b, tol=0.5)["differ"] and film.exrdiff(a, b, tol=0.1)["differ"]
+    z = np.zeros_like(a)
+    assert film.exrdiff(z, z)["small"] == 0  # zero in both: skipped

@@ -104,3 +104,45 @@ def test_film_edge_semantics():
     big = np.float32(1000) + np.float32(1 - 2 ** -24)  # rounds up to 1001
     assert big == np.float32(1001) and extent(big, 2000) == (1000, 1001)
     assert extent(np.float32(0), 100) == (0, 0)
+
+
+def test_windowed_replay_table_and_render(small):
+    """o_replay_render_table_window keeps exactly the whole-extent table's rows of its window (a
+    task's RNG(taskNum) stream is its own, so skipping the tasks outside changes nothing), and a
+    tile rendered from the windowed table equals the tile rendered from the whole table."""
+    sc, o, _, _ = small
+    full = o.replay_table(sc.spp, cores=8, li_draws=6, nthreads=4)
+    x0, x1, y0, y1 = 13, 31, 7, 29
+    win = o.replay_window(x0, x1, y0, y1)
+    assert win == (12, 32, 6, 30)
+    part = o.replay_table_window(sc.spp, win, cores=8, li_draws=6, nthreads=4)
+    assert np.array_equal(part, full[win[2]:win[3], win[0]:win[1]])
+    a = o.render_tile_replay(sc.spp, full, x0, x1, y0, y1, nthreads=4)
+    b = o.render_tile_replay(sc.spp, part, x0, x1, y0, y1, nthreads=4, window=win)
+    assert np.array_equal(a, b) and (a[..., 1] > 0).any()
+    # a window touching the frame edge keeps the extent's last row / column (xres, yres)
+    win = o.replay_window(sc.xres - 5, sc.xres, sc.yres - 4, sc.yres)
+    assert win == (sc.xres - 6, sc.xres + 1, sc.yres - 5, sc.yres + 1)
+    part = o.replay_table_window(sc.spp, win, cores=8, li_draws=6, nthreads=4)
+    assert np.array_equal(part, full[win[2]:, win[0]:])
+
+
+def test_cpu_baseline_task_split(small):
+    """bench.py's CPU baseline runs SamplerRenderer::Render's task split: RoundUpPow2(max(32 cores,
+    W H / 256)) sub-windows (Sampler::ComputeSubWindow) that tile the image exactly once."""
+    sc, o, _, _ = small
+    assert orr.render_task_count(1024, 1024, 8) == 4096
+    assert orr.render_task_count(1024, 1024, 256) == 8192
+    assert orr.render_task_count(48, 48, 4) == 128
+    cover = np.zeros((sc.yres, sc.xres), np.int32)
+    n = orr.render_task_count(sc.xres, sc.yres, 4)
+    for k in range(n):
+        x0, x1, y0, y1 = orr.sub_window(k, n, 0, sc.xres, 0, sc.yres)
+        cover[y0:y1, x0:x1] += 1
+    assert np.all(cover == 1)
+    # a bounded run renders whole tasks only
+    import ctypes as C
+    order = np.arange(n, dtype=np.int32)
+    tasks, el = C.c_long(), C.c_double()
+    px = orr._lib().o_cpu_baseline(o.h, sc.spp, 3, 4, 4, 30.0, order.ctypes.data, n, C.byref(tasks), C.byref(el))
+    assert tasks.value == n and px == sc.xres * sc.yres and el.value > 0

@@ -6,6 +6,7 @@
 #
 # Steps:
 #   tests[=EXPR]      pytest -m gpu (optionally -k EXPR)          -> gpurun_out/TAG_pytest_gpu.log
+#                     (+ the image tests' unfloored errors         -> gpurun_out/TAG_parity.jsonl)
 #   smoke             __graft_entry__.smoke()                      -> gpurun_out/TAG_smoke.log
 #   bench[=CFG]       bench.py --config CFG (c2 default), 5 steps  -> gpurun_out/TAG_bench_CFG.jsonl
 #   quick[=CFG]       bench.py, 3 steps, no CPU baseline           -> gpurun_out/TAG_bench_CFG.jsonl
@@ -37,7 +38,7 @@ for step in "$@"; do
       k=()
       [ -n "$arg" ] && k=(-k "$arg")
       echo "== tests ${arg}"
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread "${k[@]}" > $log 2>&1 || fail tests $log 60
+      MPSS_PARITY_REPORT=gpurun_out/${TAG}_parity.jsonl timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread "${k[@]}" > $log 2>&1 || fail tests $log 60
       tail -1 $log ;;
     smoke)
       log=gpurun_out/${TAG}_smoke.log
