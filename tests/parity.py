@@ -1,11 +1,12 @@
 """The image parity criterion of the GPU tests, and the report of the error they actually reach.
 
-check_image(got, ref, name): film weights bit-exact (the sample-to-pixel mapping), XYZ within
-TOL = 1e-4 relative per pixel with a floor at 1e-3 of the window's peak (pixels far below the
-peak carry few samples, where a float reassociation of the Mo() sum is a larger fraction of the
-pixel). It also computes the UNFLOORED relative L-inf, max |gpu - cpu| / |cpu| over every
-channel value with cpu != 0 (and counts values that are 0 on one side only), and appends it,
-with the floored figure, to the JSONL file named by $MPSS_PARITY_REPORT (tools/gpu.sh sets it).
+check_image(got, ref, name): north_star's criterion as stated -- film weights bit-exact (the
+sample-to-pixel mapping) and XYZ within TOL = 1e-4 RELATIVE L-inf: max |gpu - cpu| / |cpu| over
+every channel value with cpu != 0, no absolute floor, and no value zero on one side only. (Round 2
+used a floor at 1e-3 of the window's peak; the measured unfloored error is <= 8e-7 on every
+image test, profiles/r03b_parity.jsonl, so the floor is gone.) Each call appends its figures
+(relative L-inf, where it occurs relative to the peak, the 99.9th percentile, and the round-2
+floored figure) to the JSONL file named by $MPSS_PARITY_REPORT (tools/gpu.sh sets it).
 """
 import json
 import os
@@ -42,5 +43,6 @@ def check_image(got, ref, name=None):
     st = image_errors(got, ref)
     record(name or os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], st)
     assert st["peak"] > 0
-    assert st["floored_worst"] <= TOL, "max |gpu-cpu| / bound = %g" % (st["floored_worst"] / TOL)
+    assert st["zero_mismatch"] == 0, "%d values are zero on one side only" % st["zero_mismatch"]
+    assert st["rel_linf"] <= TOL, "relative L-inf %g > %g" % (st["rel_linf"], TOL)
     return st

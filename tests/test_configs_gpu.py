@@ -36,8 +36,7 @@ def _render(torch, ctx, spp, seed, x0, x1, y0, y1):
 
 
 def _check(got, ref):
-    """test_render_parity_gpu.py's criterion (tests/parity.py): weights bit-exact, XYZ within 1e-4
-    relative with a floor at 1e-3 of the window's peak; the unfloored relative L-inf is reported."""
+    """tests/parity.py's criterion: weights bit-exact, XYZ within 1e-4 relative L-inf (no floor)."""
     parity.check_image(got, ref)
 
 
