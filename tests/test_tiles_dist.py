@@ -84,6 +84,70 @@ def test_gloo_world2_tiles_gather(W, H, T, dealer):
     assert q.get(timeout=5) is True
 
 
+class _FakeCtx:
+    """Stands in for mpss.Context in bench.py's own multi-GPU code: tile_costs from a radial blob,
+    render_tiles writing fake_pixels into CPU tensors."""
+
+    def __init__(self, W, H):
+        self.W, self.H = W, H
+
+    def tile_costs(self, rects):
+        cx, cy = self.W / 2.0, self.H / 2.0
+        sss = [int(100 * max(0.0, 1.0 - (((x0 + x1) / 2 - cx) ** 2 + ((y0 + y1) / 2 - cy) ** 2) /
+                                 (0.2 * self.W * self.H))) for x0, x1, y0, y1 in rects]
+        return np.array(sss, np.int64), np.array([(x1 - x0) * (y1 - y0) for x0, x1, y0, y1 in rects], np.int64)
+
+    def render_tiles(self, spp, seed, rects, ptrs, stream=None):
+        for (x0, x1, y0, y1), ptr in zip(rects, ptrs):
+            px = fake_pixels(seed, x0, x1, y0, y1).reshape(-1)
+            dst = np.ctypeslib.as_array((__import__("ctypes").c_float * px.size).from_address(ptr))
+            dst[:] = px
+
+    def reset_render_stats(self):
+        pass
+
+
+def _bench_worker(rank, world, port, W, H, T, frames, q):
+    """bench.py's deal + timed_steps (render, one dist.gather per step, max-over-ranks time) and
+    tiles.assemble, over gloo with the stand-in renderer."""
+    import argparse
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-skin_amd"))
+    import bench
+    from mpss import tiles as tl
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = _FakeCtx(W, H)
+    sc = argparse.Namespace(xres=W, yres=H, spp=4)
+    tiles, items_by_rank, bal, skin = bench.deal(ctx, sc, T, frames, world)
+    dt, gath, out = bench.timed_steps(argparse.Namespace(seed=3), ctx, sc, tiles, items_by_rank, frames, T, rank,
+                                      world, 2, 1, device="cpu")
+    if rank == 0:
+        img = np.zeros((frames, H, W, 4), np.float32)
+        tl.assemble(img, [g.numpy() for g in gath], items_by_rank, tiles, T)
+        ok = all(np.array_equal(img[f], fake_pixels(3 + f, 0, W, 0, H)) for f in range(frames))
+        q.put((bool(ok), dt > 0, skin))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H,T,frames", [(100, 70, 32, 1), (128, 96, 32, 2)])
+def test_gloo_world2_bench_timed_steps(W, H, T, frames):
+    """The code bench.py runs at N > 1 (deal by tile cost, timed steps with the film gather, the
+    MAX-over-ranks time, reassembly), at world size 2 over gloo."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, W, H, T, frames, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    ok, timed, skin = q.get(timeout=5)
+    assert ok and timed and skin > 0
+
+
 def test_rank_items_partition():
     sys.path.insert(0, os.path.join(ROOT, "pbrt-v2-skin_amd"))
     from mpss import tiles as tl

@@ -1,8 +1,10 @@
-"""Summarize a rocprofv3 output tree (gpurun_out/prof_TAG) into profiles/TAG_*:
-kernel_stats.csv copied as is, plus TAG_pmc.json with per-kernel means of every PMC counter
-(and FETCH_SIZE x 2 in bytes, the gfx950 correction from MI355X_MICROARCH.md).
+"""Summarize a rocprofv3 output tree (gpurun_out/prof_TAG[_CFG], tools/gpu.sh kt / pmc steps) into
+profiles/TAG[_CFG]_*: kernel_stats.csv copied as is, plus TAG[_CFG]_pmc.json with per-kernel means of
+every PMC counter (and FETCH_SIZE x 2 in bytes, the gfx950 correction from MI355X_MICROARCH.md).
+The summary records the bench config it profiled and the hash of the Mo-gather sources, so
+bench.py attaches its counters only to a line of the same config and kernel code.
 
-    python tools/summarize_prof.py r01b
+    python tools/summarize_prof.py r03c [c3]
 """
 import collections
 import csv
@@ -15,7 +17,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag):
+def main(tag, cfg="c2"):
+    if cfg != "c2":
+        tag = "%s_%s" % (tag, cfg)
     src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -44,11 +48,13 @@ def main(tag):
     from bench import kernel_source_hash  # the Mo-gather sources the counters describe
     head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                           text=True).stdout.strip()
-    out["__meta__"] = {"source_hash": kernel_source_hash(), "git_head_at_summary": head}
+    import time
+    out["__meta__"] = {"source_hash": kernel_source_hash(), "git_head_at_summary": head, "config": cfg,
+                       "written": time.strftime("%Y-%m-%dT%H:%M:%S")}
     with open(os.path.join(dst, "%s_pmc.json" % tag), "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     print("wrote profiles/%s_*" % tag)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "c2")
