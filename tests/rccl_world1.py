@@ -43,9 +43,9 @@ def main():
     ref = full.cpu().numpy().reshape(sc.yres, sc.xres, 4)
     t = torch.tensor([dt], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ok = bool(np.array_equal(img[0], ref)) and (ref[..., 1] > 0).any()
+    ok = bool(np.array_equal(img[0], ref) and (ref[..., 1] > 0).any())
     print(json.dumps({"backend": backend, "world": dist.get_world_size(), "tiles": len(tiles),
-                      "skin_tiles": skin_tiles, "step_s": float(t.item()) / 2, "film_equal": ok}), flush=True)
+                      "skin_tiles": int(skin_tiles), "step_s": float(t.item()) / 2, "film_equal": ok}), flush=True)
     ctx.close()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)
