@@ -152,6 +152,7 @@ private:
     std::vector<SurfacePoint> points_;
     std::vector<float> irradiance_;
     DevBuf<BvhNode> d_bvh_;
+    DevBuf<BvhNode> d_bvh_thread_;  // threaded copy (interior offset = end of subtree), any-hit walks
     DevBuf<TriRec> d_tris_;
     DevBuf<int32_t> d_tri_mesh_, d_tri_local_;
     std::vector<std::unique_ptr<DevBuf<float>>> d_mesh_bufs_;

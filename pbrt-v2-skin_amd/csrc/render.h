@@ -53,6 +53,10 @@ struct RenderMaterial {
 
 struct RenderScene {
     const BvhNode *bvh;
+    // the same nodes threaded for stackless any-hit walks: an interior node's offset is the end of
+    // its pre-order subtree (render_host.hip upload_scene); nbvh nodes
+    const BvhNode *bvh_thread;
+    int nbvh;
     const TriRec *tris;
     const int32_t *tri_mesh, *tri_local;
     const RenderMesh *meshes;

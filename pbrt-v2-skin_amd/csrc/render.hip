@@ -151,6 +151,156 @@ __device__ bool trace_any(const RenderScene &sc, V3 o, V3 d, float mint, float m
     return false;
 }
 
+// Sphere::Intersect out of line: its double-precision atan2 (the phi test) would otherwise set the
+// register budget of every kernel that inlines a light loop.
+__device__ __noinline__ bool sphere_hit_ool(const SphereView &s, V3 o, V3 d, float mint, float maxt, float &thit,
+                                            V3 *nn) {
+    return sphere_intersect(s, o, d, mint, maxt, thit, nn);
+}
+
+// ------------------------------------------------------------------ BVH traversal (per wave)
+// The hot kernels trace with the whole wave walking one node sequence: the node index is
+// wave-uniform, so node and triangle records are scalar loads, and no lane carries a stack.
+
+// Scene::IntersectP (bvh.cpp:442-488 + Sphere::IntersectP) for every active lane, as trace_any,
+// by a stackless walk of the threaded BVH: pre-order, so after an interior node the walk goes on at
+// node + 1 when some lane hit its box and at its subtree's end (the threaded offset) otherwise. A
+// lane evaluates a node when node >= its resume index; missing a box sets resume to the subtree's
+// end, a hit ends the lane. Each lane tests exactly the nodes and triangles its own traversal
+// reaches with the fixed maxt (any-hit prunes only by the box test, so the order does not change
+// the answer). strict: a triangle counts only when t < maxt (the BSDF ray toward an area light,
+// whose own surface is at maxt). spheres: test the area-light spheres first, as trace_any does.
+__device__ bool trace_any_wave(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, bool active, bool strict,
+                               bool spheres) {
+    bool hit = false;
+    if (active && spheres)
+        for (int l = 0; l < sc.nlights; ++l) {
+            float t;
+            if (!sc.lights[l].kind && sphere_hit_ool(sc.lights[l].s, o, d, mint, maxt, t, nullptr)) {
+                hit = true;
+                break;
+            }
+        }
+    const V3 inv = V3{1.f / d.x, 1.f / d.y, 1.f / d.z};
+    const int neg[3] = {inv.x < 0.f, inv.y < 0.f, inv.z < 0.f};
+    int resume = (active && !hit) ? 0 : INT_MAX;
+    const cptr<BvhNode> nodes = as_const(sc.bvh_thread);
+    const cptr<TriRec> tris = as_const(sc.tris);
+    int node = 0;
+    while (node < sc.nbvh) {
+        node = __builtin_amdgcn_readfirstlane(node);
+        const BvhNode n = nodes[node];
+        const bool act = node >= resume;
+        const bool in = act && bbox_hit(n, o, inv, neg, mint, maxt);
+        if (act && !in) resume = n.nprims > 0 ? node + 1 : n.offset;
+        if (n.nprims > 0) {
+            if (__builtin_amdgcn_ballot_w64(in) != 0) {
+                bool found = false;
+                for (int i = 0; i < (int)n.nprims; ++i) {
+                    const TriRec tr = tris[n.offset + i];
+                    float t, b1, b2;
+                    if (in && !found &&
+                        tri_intersect(o, d, mint, maxt, V3{tr.p1[0], tr.p1[1], tr.p1[2]},
+                                      V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2))
+                        found = !strict || t < maxt;
+                }
+                if (found) {
+                    hit = true;
+                    resume = INT_MAX;
+                }
+                if (__builtin_amdgcn_ballot_w64(resume != INT_MAX) == 0) break;  // every lane is done
+            }
+            node = node + 1;
+        } else {
+            node = __builtin_amdgcn_ballot_w64(in) != 0 ? node + 1 : n.offset;
+        }
+    }
+    return hit;
+}
+
+// Scene::Intersect's BVH part (bvh.cpp:388-439) for the active lanes whose rays share the direction
+// signs (dirIsNeg) of `pat`: with the signs shared, every lane's ordered traversal (near child first)
+// visits its nodes in one common order, so the wave walks the union with one stack of (node, lane
+// mask) entries in LDS; a lane enters a node only if it is in the entry's mask and hits the box with
+// its own current t. Each lane therefore tests exactly the nodes and triangles, in exactly the
+// order, of its own traversal, and ends with the same hit.
+__device__ void trace_closest_packet(const RenderScene &sc, V3 o, V3 inv, const int neg[3], V3 d, float mint, Hit &h,
+                                     uint64_t grp, int pat, int *snode, uint64_t *smask) {
+    const int lane = (int)(threadIdx.x & 63);
+    const bool mine = (grp >> lane) & 1ull;
+    const cptr<BvhNode> nodes = as_const(sc.bvh);
+    const cptr<TriRec> tris = as_const(sc.tris);
+    int node = 0, sp = 0;
+    uint64_t mask = grp;
+    for (;;) {
+        node = __builtin_amdgcn_readfirstlane(node);
+        const BvhNode n = nodes[node];
+        const bool in = mine && ((mask >> lane) & 1ull) && bbox_hit(n, o, inv, neg, mint, h.t);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+        if (m != 0 && n.nprims == 0) {  // interior: near child now, far child on the stack
+            const int a = (int)n.axis;
+            const bool far_first = ((pat >> a) & 1) != 0;  // dirIsNeg[axis]: the second child is near
+            snode[sp] = far_first ? node + 1 : n.offset;
+            smask[sp] = m;
+            ++sp;
+            node = far_first ? n.offset : node + 1;
+            mask = m;
+            continue;
+        }
+        if (m != 0) {  // leaf
+            for (int i = 0; i < (int)n.nprims; ++i) {
+                const TriRec tr = tris[n.offset + i];
+                float t, b1, b2;
+                if (in && tri_intersect(o, d, mint, h.t, V3{tr.p1[0], tr.p1[1], tr.p1[2]},
+                                        V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2)) {
+                    h.t = t;
+                    h.b1 = b1;
+                    h.b2 = b2;
+                    h.tri = tr.tri;
+                }
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = snode[sp];
+        mask = __builtin_amdgcn_readfirstlane((uint32_t)smask[sp]) |
+               ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(smask[sp] >> 32)) << 32);
+    }
+}
+
+// trace_closest for every active lane, by sign packets: the lanes are grouped by their rays'
+// direction signs and each group is traced as one packet (camera rays of one pixel share them).
+// snode / smask: this wave's kStack-entry stack in LDS.
+__device__ Hit trace_closest_wave(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, bool active, int *snode,
+                                  uint64_t *smask) {
+    Hit h;
+    h.tri = INT_MIN;
+    h.t = maxt;
+    const V3 inv = V3{1.f / d.x, 1.f / d.y, 1.f / d.z};
+    const int neg[3] = {inv.x < 0.f, inv.y < 0.f, inv.z < 0.f};
+    const int sgn = neg[0] | (neg[1] << 1) | (neg[2] << 2);
+    uint64_t todo = __builtin_amdgcn_ballot_w64(active);
+    while (todo != 0) {
+        const int lead = __builtin_ctzll(todo);
+        const int pat = __builtin_amdgcn_readlane(sgn, lead);
+        const uint64_t grp = __builtin_amdgcn_ballot_w64(active && sgn == pat) & todo;
+        todo &= ~grp;
+        trace_closest_packet(sc, o, inv, neg, d, mint, h, grp, pat, snode, smask);
+    }
+    if (active)
+        for (int l = 0; l < sc.nlights; ++l) {
+            if (sc.lights[l].kind) continue;  // an infinite light has no shape
+            float t;
+            V3 nn;
+            if (sphere_hit_ool(sc.lights[l].s, o, d, mint, h.t, t, &nn)) {
+                h.t = t;
+                h.tri = -1 - l;
+                h.lnn = nn;
+            }
+        }
+    return h;
+}
+
 // DiffuseAreaLight::Sample_L (lights/diffuse.cpp:75-87) + VisibilityTester::SetSegment (light.h:87-92)
 struct LightSampleOut {
     V3 wi;
@@ -551,8 +701,9 @@ __device__ __forceinline__ void image_sample(const RenderScene &sc, uint32_t see
 // Scene::Intersect. Surface hits are compacted (one atomic per wave, sample order kept inside
 // the wave) so the shading kernel runs on full waves; a miss or an area-light hit ends here.
 __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList pl, SampleRecs rec) {
-    __shared__ int stk_all[kStack * 256];
-    int *stk = stk_all + threadIdx.x;
+    __shared__ int snode_all[kStack * 4];  // one traversal stack per wave (trace_closest_wave)
+    __shared__ uint64_t smask_all[kStack * 4];
+    const int wv = (int)(threadIdx.x >> 6);
     const int k = piece_of(pl, (int)blockIdx.x);
     const TileBatch &tb = pl.tb[k];
     rec.flags += pl.off[k];
@@ -574,9 +725,8 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList 
     film_extent(Y, sc.yres, ly, hy);
     const bool live = in_range && lx < tb.x1 && hx >= tb.x0 && ly < tb.y1 && hy >= tb.y0;
     uint32_t flags = 0;
-    Hit h;
-    h.tri = INT_MIN;
-    V3 d = V3{0.f, 0.f, 0.f};
+    V3 d = V3{1.f, 1.f, 1.f};
+    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
     if (live) {
         flags |= REC_LIVE;
         const uint32_t edge = (lx < px ? REC_XLO : 0u) | (hx > px ? REC_XHI : 0u) | (ly < py ? REC_YLO : 0u) |
@@ -587,9 +737,11 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList 
         }
         // PerspectiveCamera::GenerateRay (cameras/perspective.cpp)
         const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
-        const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
         d = xform_vector(sc.camera_to_world, normalize(pcam));
-        h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 256);
+    }
+    // Scene::Intersect, the wave's rays as sign packets (one pixel's samples share one packet)
+    const Hit h = trace_closest_wave(sc, o, d, 0.f, INFINITY, live, snode_all + kStack * wv, smask_all + kStack * wv);
+    if (live) {
         if (h.tri == INT_MIN) {  // SamplerRenderer::Li: Li += lights[i]->Le(ray) for every light
             if (sc.n_infinite > 0) flags |= REC_LE | (0xffu << REC_LIGHT_SHIFT);
         } else if (h.tri < 0) {  // an area light's own surface: Le only
@@ -698,8 +850,6 @@ static_assert(sizeof(DirectTerms) == 64, "one 64-B record per light sample");
 __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
                                                            int max_hits, int ns_max, DirectTerms *terms,
                                                            float4 *__restrict__ inf_st) {
-    __shared__ int stk_all[kStack * 256];
-    int *stk = stk_all + threadIdx.x;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per_hit = sc.nlights * ns_max;
     const int nhits = *rec.hit_count;
@@ -772,7 +922,7 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     if (lightPdf > 0.f && ls.nonblack && ncomp > 0) {
         const V3 wi_l = to_local(fr, ls.wi);
         const Lobe f1 = bsdf_lobe(mat, dot(ls.wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
-        if (!lobe_black(mat, f1) && !trace_any(sc, ls.so, ls.sd, ls.smint, ls.smaxt, stk, 256)) {
+        if (!lobe_black(mat, f1) && !trace_any_wave(sc, ls.so, ls.sd, ls.smint, ls.smaxt, true, false, true)) {
             const float bsdfPdf = bsdf_pdf(mat, wo_l, wi_l);
             const float w = power_heuristic(lightPdf, bsdfPdf);
             out.k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
@@ -801,32 +951,42 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                 lightPdf = L.kind ? infinite_pdf(L, wi) : sphere_pdf(L.s, fr.p, wi);
                 if (lightPdf != 0.f) {
                     const float w = power_heuristic(bsdfPdf, lightPdf);
-                    // An area light is hit only if the ray meets its sphere at all: the sphere test
-                    // with maxt = inf accepts every hit that the traversal's (smaller maxt) accepts,
-                    // so a miss here is a miss there and the trace is skipped. A hit at tl bounds the
-                    // traversal: the closest primitive is the light iff nothing is hit before tl
-                    // (ties at tl go to the sphere in both, its test runs last).
-                    float tmax = INFINITY;
-                    bool need_trace = true;
-                    if (!L.kind) {
-                        float tl;
-                        need_trace = sphere_intersect(L.s, fr.p, wi, reps, INFINITY, tl, nullptr);
-                        tmax = tl;
-                    }
-                    Hit hl;
-                    hl.tri = INT_MIN;
-                    if (need_trace) hl = trace_closest(sc, fr.p, wi, reps, tmax, stk, 256);
-                    // Li = lightIsect.Le(-wi) when the hit primitive is this light; light->Le(ray)
-                    // when the ray escapes (0 for an area light)
-                    bool lit;
+                    // Li = lightIsect.Le(-wi) when Scene::Intersect's closest primitive is this light;
+                    // light->Le(ray) when the ray escapes (0 for an area light). Both are answered by
+                    // any-hit walks:
+                    //  * infinite light: the ray escapes iff it hits no triangle and no light sphere;
+                    //  * area light: the ray meets the light only if it meets its sphere at all (the
+                    //    sphere test with maxt = inf accepts every hit the closest-hit search would), at
+                    //    tl. The closest-hit search from maxt = tl ends on a triangle iff one lies at
+                    //    t < tl (at t == tl the spheres, tested last, take over), and otherwise its
+                    //    sphere loop alone decides -- so: no triangle before tl (strict any-hit), then
+                    //    the sphere loop from tl, exactly as trace_closest runs it.
+                    bool lit = false;
                     if (L.kind) {
-                        lit = hl.tri == INT_MIN;
+                        lit = !trace_any_wave(sc, fr.p, wi, reps, INFINITY, true, false, true);
                         if (lit) {
                             inf_coords(L, wi, st.z, st.w);
                             lit = inf_nonblack(L, st.z, st.w);
                         }
                     } else {
-                        lit = hl.tri == -1 - l && dot(hl.lnn, -wi) > 0.f;
+                        float tl;
+                        if (sphere_hit_ool(L.s, fr.p, wi, reps, INFINITY, tl, nullptr) &&
+                            !trace_any_wave(sc, fr.p, wi, reps, tl, true, true, false)) {
+                            float ht = tl;
+                            int who = INT_MIN;
+                            V3 lnn = V3{0.f, 0.f, 0.f};
+                            for (int k = 0; k < sc.nlights; ++k) {
+                                if (sc.lights[k].kind) continue;
+                                float t;
+                                V3 nn;
+                                if (sphere_hit_ool(sc.lights[k].s, fr.p, wi, reps, ht, t, &nn)) {
+                                    ht = t;
+                                    who = -1 - k;
+                                    lnn = nn;
+                                }
+                            }
+                            lit = who == -1 - l && dot(lnn, -wi) > 0.f;
+                        }
                     }
                     if (lit) {
                         out.adn = absdot(wi, fr.nn);

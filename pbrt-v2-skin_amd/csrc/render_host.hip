@@ -120,6 +120,18 @@ void Context::upload_scene() {
     const int depth = bvh_depth(scene_.bvh, 0);
     if (depth > 47) throw Error(MPSS_ERR_INTERNAL, "BVH deeper than the 48-entry traversal stack");
     d_bvh_.upload(scene_.bvh.data(), scene_.bvh.size());
+    {
+        // the threaded copy for stackless any-hit walks: the nodes are in pre-order (a node's subtree
+        // is [i, end_i)), so an interior node's offset becomes end_i -- where a walk continues after
+        // missing it; a leaf's end is i + 1
+        std::vector<BvhNode> th = scene_.bvh;
+        std::vector<int32_t> end(th.size());
+        for (size_t i = th.size(); i-- > 0;)
+            end[i] = th[i].nprims > 0 ? (int32_t)i + 1 : end[th[i].offset];
+        for (size_t i = 0; i < th.size(); ++i)
+            if (th[i].nprims == 0) th[i].offset = end[i];
+        d_bvh_thread_.upload(th.data(), th.size());
+    }
     d_tris_.upload(scene_.tris.data(), scene_.tris.size());
     d_tri_mesh_.upload(scene_.tri_mesh.data(), scene_.tri_mesh.size());
     d_tri_local_.upload(scene_.tri_local.data(), scene_.tri_local.size());
@@ -262,6 +274,8 @@ void Context::upload_scene() {
 RenderScene Context::render_scene() const {
     RenderScene sc{};
     sc.bvh = d_bvh_.ptr;
+    sc.bvh_thread = d_bvh_thread_.ptr;
+    sc.nbvh = (int)scene_.bvh.size();
     sc.tris = d_tris_.ptr;
     sc.tri_mesh = d_tri_mesh_.ptr;
     sc.tri_local = d_tri_local_.ptr;
