@@ -641,7 +641,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             int64_t total = 0;
             while (pe < pieces.size() && (pe == pi || total + pieces[pe].tb.nsamples <= max_batch))
                 total += pieces[pe++].tb.nsamples;
-            // hits <= samples; the hit arrays grow to the largest batch seen (<= ~290 B per hit)
+            // per-sample buffers: the batch's camera samples (primary_kernel may give each a hit slot)
             if (ws->n < total) {
                 int64_t have = ws->n;
                 grow(ws->flags, have, total, 1);
@@ -649,36 +649,25 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 grow(ws->slot, have, total, 1);
                 ws->n = total;
             }
-            if (ws->hits < total) {
-                int64_t h0 = ws->hits;
-                for (auto *b : {&ws->q, &ws->ha, &ws->hb, &ws->xyz}) {
-                    int64_t have = h0;
+            if (ws->rec_n < total) {
+                for (auto *b : {&ws->ha, &ws->hb}) {
+                    int64_t have = ws->rec_n;
                     grow(*b, have, total, 1);
                 }
-                int64_t have = h0;
-                grow(ws->mo, have, total, kGroups);
-                have = h0;
-                grow(ws->ld, have, total, ROW);
-                have = h0;
+                int64_t have = ws->rec_n;
                 grow(ws->hs, have, total, 1);
-                ws->hits = total;
-            }
-            grow(ws->perm, ws->perm_n, (total + 1023) / 1024 * 1024, 1);
-            if (sc.any_tex && ws->tex_hits < total) {
-                int64_t have = ws->tex_hits;
-                grow(ws->alb, have, total, 1);
-                have = ws->tex_hits;
-                grow(ws->frame, have, total, 2);
-                ws->tex_hits = total;
+                ws->rec_n = total;
             }
             if (ws->px < total / spp) {
                 int64_t have = ws->px;
                 grow(ws->spill, have, total / spp, 1);
                 ws->px = total / spp;
             }
+            if (!ws->ray_count.ptr) ws->ray_count.alloc(1);
             MPSS_HIP(hipMemsetAsync(ws->count.ptr, 0, sizeof(int), stream));
+            MPSS_HIP(hipMemsetAsync(ws->ray_count.ptr, 0, sizeof(int), stream));
             MPSS_HIP(hipMemsetAsync(ws->spill.ptr, 0, sizeof(uint32_t) * (size_t)(total / spp), stream));
-            auto recs = [&](int64_t off) {
+            auto recs = [&](int64_t off) {  // (the per-hit pointers are read after the hit-count resize)
                 return SampleRecs{ws->flags.ptr + off, ws->spill.ptr + off / spp, ws->slot.ptr + off, ws->ld.ptr,
                                   ws->ha.ptr, ws->hb.ptr, ws->hs.ptr, ws->q.ptr, ws->count.ptr, ws->mo.ptr,
                                   ws->xyz.ptr, ws->alb.ptr, ws->frame.ptr};
@@ -715,9 +704,37 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             time_begin(timing, stream, ev);
             launch_pieces(false);
             time_end(timing, stream, ev, 1, timed);
+            // the batch's hit count sizes everything after the compaction: one read-back per batch
+            // (the stream only waits for primary_kernel; the GPU idles for the round trip alone)
+            int nh_dev = 0;
+            MPSS_HIP(hipMemcpyAsync(&nh_dev, ws->count.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
+            MPSS_HIP(hipStreamSynchronize(stream));
+            const int64_t nh = std::max<int64_t>(1, nh_dev);
+            if (ws->hits < nh) {
+                for (auto *b : {&ws->q, &ws->xyz}) {
+                    int64_t have = ws->hits;
+                    grow(*b, have, nh, 1);
+                }
+                int64_t have = ws->hits;
+                grow(ws->mo, have, nh, kGroups);
+                have = ws->hits;
+                grow(ws->ld, have, nh, ROW);
+                ws->hits = nh;
+            }
+            grow(ws->perm, ws->perm_n, (nh + 1023) / 1024 * 1024, 1);
+            if (sc.any_tex && ws->tex_hits < nh) {
+                int64_t have = ws->tex_hits;
+                grow(ws->alb, have, nh, 1);
+                have = ws->tex_hits;
+                grow(ws->frame, have, nh, 2);
+                ws->tex_hits = nh;
+            }
             {
                 const SampleRecs rec = recs(0);
-                const int64_t lanes = total * std::max<int64_t>(1, (int64_t)nlights) * ns_max;
+                const int64_t lanes = nh * std::max<int64_t>(1, (int64_t)nlights) * ns_max;
+                if (lanes >= ((int64_t)1 << 30))  // RayQueue ids carry the lane in 30 bits
+                    throw Error(MPSS_ERR_INVALID, "render_tile: too many light samples per batch; lower "
+                                                  "max_batch_samples");
                 grow(ws->terms, ws->terms_n, lanes, 64);
                 DirectTerms *terms = reinterpret_cast<DirectTerms *>(ws->terms.ptr);
                 float4 *inf_st = nullptr;
@@ -725,24 +742,35 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                     grow(ws->st, ws->st_n, lanes, 1);
                     inf_st = ws->st.ptr;
                 }
+                if (ws->ray_n < 2 * lanes) {  // <= 2 visibility rays per direct-light lane
+                    int64_t have = ws->ray_n;
+                    grow(ws->rays, have, 2 * lanes, 2);
+                    have = ws->ray_n;
+                    grow(ws->ray_id, have, 2 * lanes, 1);
+                    ws->ray_n = 2 * lanes;
+                }
+                const RayQueue rq{ws->rays.ptr, ws->ray_id.ptr, ws->ray_count.ptr};
                 time_begin(timing, stream, ev);
                 if (sc.any_tex)
-                    hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                                       sc, rec, spp, seed, (int)total);
+                    hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, sc,
+                                       rec, spp, seed, (int)nh);
                 if (nlights > 0) {
                     hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       stream, sc, rec, spp, seed, (int)total, ns_max, terms, inf_st);
+                                       stream, sc, rec, spp, seed, (int)nh, ns_max, terms, inf_st, rq);
+                    // persistent: 8 waves per CU's worth of workgroups walk the queue
+                    const int64_t tblocks = std::min<int64_t>((2 * lanes + 255) / 256, 2048);
+                    hipLaunchKernelGGL(trace_rays_kernel, dim3((unsigned)tblocks), dim3(256), 0, stream, sc, rq, terms);
                     if (sc.n_infinite > 0)
-                        hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((total + 255) / 256)),
-                                           dim3(256), 0, stream, sc, rec, (int)total, ns_max,
-                                           (const DirectTerms *)terms, (const float4 *)inf_st);
+                        hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((nh + 255) / 256)), dim3(256),
+                                           0, stream, sc, rec, (int)nh, ns_max, (const DirectTerms *)terms,
+                                           (const float4 *)inf_st);
                     else
-                        hipLaunchKernelGGL(direct_combine_kernel<false>, dim3((unsigned)((total + 255) / 256)),
-                                           dim3(256), 0, stream, sc, rec, (int)total, ns_max,
-                                           (const DirectTerms *)terms, (const float4 *)nullptr);
+                        hipLaunchKernelGGL(direct_combine_kernel<false>, dim3((unsigned)((nh + 255) / 256)), dim3(256),
+                                           0, stream, sc, rec, (int)nh, ns_max, (const DirectTerms *)terms,
+                                           (const float4 *)nullptr);
                 } else {
-                    hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                                       stream, sc, rec, (int)total);
+                    hipLaunchKernelGGL(shade_nolight_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream,
+                                       sc, rec, (int)nh);
                 }
                 time_end(timing, stream, ev, 4, timed);
             }
@@ -751,11 +779,11 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 for (const SssMat &s : sss) {
                     if (s.m->rgb)  // Mo() rows in band order (the material's pos is the identity)
                         launch_mo_rgb(dev_octree_, s.m->dev_rgb.ptr, s.m->dev_rgb_rcp.ptr, s.m->rgb_rcp,
-                                      s.m->profile.length, max_error, (int)total, nullptr, ws->q.ptr, ws->count.ptr,
+                                      s.m->profile.length, max_error, (int)nh, nullptr, ws->q.ptr, ws->count.ptr,
                                       sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, (float *)ws->mo.ptr, 4 * kGroups,
                                       nullptr, stream);
                     else
-                        launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)total, ws->q.ptr,
+                        launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)nh, ws->q.ptr,
                                        ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
                                        ws->work.ptr, ws->perm.ptr, gopts, stream);
                 }
@@ -764,22 +792,17 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             time_begin(timing, stream, ev);
             {
                 const SampleRecs rec = recs(0);
-                hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
-                                   rec, (int)total);
+                hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, sc, rec,
+                                   (int)nh);
                 if (sc.n_infinite > 0)
-                    hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, sc,
-                                       rec, (int)total);
+                    hipLaunchKernelGGL(sky_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, sc, rec,
+                                       (int)nh);
             }
             launch_pieces(true);
             time_end(timing, stream, ev, 3, timed);
             MPSS_HIP(hipGetLastError());
             n_samples += total;
-            if (counting) {  // instrumented pass only: synchronous read of the hit count
-                int cnt = 0;
-                MPSS_HIP(hipMemcpyAsync(&cnt, ws->count.ptr, sizeof(int), hipMemcpyDeviceToHost, stream));
-                MPSS_HIP(hipStreamSynchronize(stream));
-                n_sss += cnt;
-            }
+            if (counting) n_sss += nh_dev;
             pi = pe;
         }
     } catch (...) {
