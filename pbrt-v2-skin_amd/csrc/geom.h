@@ -203,8 +203,15 @@ MPSS_HD bool sphere_intersect(const SphereView &s, V3 o, V3 d, float mint, float
     }
     V3 ph = ro + d * th;
     if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * s.r;
-    float phi = m_atan2(ph.y, ph.x);
-    if (phi < 0.f) phi += 2.f * kPiF;
+    // The phi test can only reject below phiMax = Radians(360) = 2.f * kPiF exactly (the float
+    // expression (kPiF / 180.f) * 360.f rounds to it), and phi never exceeds 2.f * kPiF: atan2 lies in
+    // [-pi, pi], and a negative phi plus 2.f * kPiF rounds to at most 2.f * kPiF. A full sphere
+    // therefore skips the (double-evaluated) atan2 with the same outcome.
+    float phi = 0.f;
+    if (s.phi_max < 2.f * kPiF) {
+        phi = m_atan2(ph.y, ph.x);
+        if (phi < 0.f) phi += 2.f * kPiF;
+    }
     if (phi > s.phi_max) {  // zmin/zmax never clip a full sphere
         if (th == t1) return false;
         if (t1 > maxt) return false;
