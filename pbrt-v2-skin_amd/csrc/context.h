@@ -67,19 +67,17 @@ std::unique_ptr<ImageTexture> build_imagemap(const mpss_imagemap &m);
 // same workspace after the kernels of the previous one.
 // Per-sample buffers (flags, slot, and the hit records primary_kernel writes: ha, hb, hs) are sized
 // for the batch's camera samples; everything after the hit compaction (Mo() queries and results,
-// direct-light terms, visibility rays, XYZ) for the batch's actual hit count, which render_tiles
-// reads back once per batch.
+// direct-light terms, XYZ) for the batch's actual hit count, which render_tiles reads back once per
+// batch.
 struct RenderWorkspace {
     DevBuf<uint32_t> flags, hs, spill;
     DevBuf<int32_t> slot;
     DevBuf<int> count, work, perm;  // perm: the sharded gather's sorted query ids
     int64_t perm_n = 0;
-    DevBuf<float4> q, mo, ha, hb, xyz, alb, frame, st, rays;
+    DevBuf<float4> q, mo, ha, hb, xyz, alb, frame, st;
     DevBuf<unsigned char> terms;
-    DevBuf<uint32_t> ray_id;
-    DevBuf<int> ray_count;
     DevBuf<float> ld;
-    int64_t n = 0, rec_n = 0, hits = 0, tex_hits = 0, terms_n = 0, st_n = 0, px = 0, ray_n = 0;
+    int64_t n = 0, rec_n = 0, hits = 0, tex_hits = 0, terms_n = 0, st_n = 0, px = 0;
     hipEvent_t done = nullptr;
     int device = 0;
     bool pending = false;

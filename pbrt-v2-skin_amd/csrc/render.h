@@ -162,19 +162,10 @@ __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float
 
 __global__ void primary_kernel(RenderScene sc, PieceList pl, SampleRecs rec0);
 struct DirectTerms;
-// Shadow / light-visibility rays of shade_direct_kernel: ray[2 k] = {o, mint}, ray[2 k + 1] = {d, maxt},
-// id[k] = direct-term lane << 2 | term (2: the BSDF-sampled term) | strict (1); *count rays.
-struct RayQueue {
-    float4 *ray;
-    uint32_t *id;
-    int *count;
-};
 // inf_st (null without infinite lights): per lane, the radiance-map lookup coordinates (s, t)
 // of the light-sampled and the BSDF-sampled direction of an infinite light's EstimateDirect
 __global__ void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed, int max_hits, int ns_max,
-                                    DirectTerms *terms, float4 *inf_st, RayQueue rq);
-// the visibility rays of shade_direct_kernel (any-hit walks); a blocked ray clears its term
-__global__ void trace_rays_kernel(RenderScene sc, RayQueue rq, DirectTerms *terms);
+                                    DirectTerms *terms, float4 *inf_st);
 // Per surface hit of a material with textures: the camera ray's differentials (scaled by
 // 1/sqrt(spp)), ComputeDifferentials, the albedo lookup (-> hit_alb) and the bumped shading frame
 // (-> hit_frame), before shade_direct_kernel reads them.

@@ -14,7 +14,6 @@
 #include "render.h"
 
 #include <climits>
-#include <cstddef>
 
 #include "../../data/spectral_bands.h"
 #include "geom.h"
@@ -850,7 +849,7 @@ static_assert(sizeof(DirectTerms) == 64, "one 64-B record per light sample");
 
 __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, SampleRecs rec, int spp, uint32_t seed,
                                                            int max_hits, int ns_max, DirectTerms *terms,
-                                                           float4 *__restrict__ inf_st, RayQueue rq) {
+                                                           float4 *__restrict__ inf_st) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int per_hit = sc.nlights * ns_max;
     const int nhits = *rec.hit_count;
@@ -916,11 +915,6 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
         ub0 = van_der_corput(nidx, hash3(seed, pix, 16u * l + DIM_BSDF_DIR));
         ub1 = sobol2(nidx, hash3(seed, pix, 16u * l + DIM_BSDF_DIR + 8u));
     }
-    // The terms are formed here as if their rays were unoccluded; each ray that decides one goes to
-    // the ray queue and trace_rays_kernel clears the term's lobe when the ray is blocked.
-    bool need1 = false, need2 = false, strict2 = false;
-    V3 r1o{}, r1d{}, r2o{}, r2d{};
-    float r1min = 0.f, r1max = 0.f, r2max = 0.f;
     // --- light sampling: ed += f * Li * (|wi.n| * w / lightPdf)
     const LightSampleOut ls = L.kind ? sample_infinite(L, fr.p, reps, lu0, lu1) : sample_light(L, fr.p, reps, lu0, lu1);
     float lightPdf = ls.pdf;
@@ -928,16 +922,11 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     if (lightPdf > 0.f && ls.nonblack && ncomp > 0) {
         const V3 wi_l = to_local(fr, ls.wi);
         const Lobe f1 = bsdf_lobe(mat, dot(ls.wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
-        if (!lobe_black(mat, f1)) {  // visibility: the shadow ray (VisibilityTester::Unoccluded)
+        if (!lobe_black(mat, f1) && !trace_any_wave(sc, ls.so, ls.sd, ls.smint, ls.smaxt, true, false, true)) {
             const float bsdfPdf = bsdf_pdf(mat, wo_l, wi_l);
             const float w = power_heuristic(lightPdf, bsdfPdf);
             out.k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
             out.l1 = f1;
-            need1 = true;
-            r1o = ls.so;
-            r1d = ls.sd;
-            r1min = ls.smint;
-            r1max = ls.smaxt;
         }
     }
     // --- BSDF sampling (BSDF::Sample_f, reflection.cpp:675-733): ed += f * Li * |wi.n| * w / pdf
@@ -972,17 +961,17 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                     //    t < tl (at t == tl the spheres, tested last, take over), and otherwise its
                     //    sphere loop alone decides -- so: no triangle before tl (strict any-hit), then
                     //    the sphere loop from tl, exactly as trace_closest runs it.
-                    // The sphere-side answers are formed here; the triangle-side any-hit walk is the
-                    // queued ray (spheres included for the infinite light, strict t < tl for the area
-                    // light).
                     bool lit = false;
                     if (L.kind) {
-                        inf_coords(L, wi, st.z, st.w);
-                        lit = inf_nonblack(L, st.z, st.w);
-                        r2max = INFINITY;
+                        lit = !trace_any_wave(sc, fr.p, wi, reps, INFINITY, true, false, true);
+                        if (lit) {
+                            inf_coords(L, wi, st.z, st.w);
+                            lit = inf_nonblack(L, st.z, st.w);
+                        }
                     } else {
                         float tl;
-                        if (sphere_hit_ool(L.s, fr.p, wi, reps, INFINITY, tl, nullptr)) {
+                        if (sphere_hit_ool(L.s, fr.p, wi, reps, INFINITY, tl, nullptr) &&
+                            !trace_any_wave(sc, fr.p, wi, reps, tl, true, true, false)) {
                             float ht = tl;
                             int who = INT_MIN;
                             V3 lnn = V3{0.f, 0.f, 0.f};
@@ -997,8 +986,6 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                                 }
                             }
                             lit = who == -1 - l && dot(lnn, -wi) > 0.f;
-                            r2max = tl;
-                            strict2 = true;
                         }
                     }
                     if (lit) {
@@ -1006,9 +993,6 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
                         out.w2 = w;
                         out.pdf2 = bsdfPdf;
                         out.l2 = f2;
-                        need2 = true;
-                        r2o = fr.p;
-                        r2d = wi;
                     }
                 }
             }
@@ -1016,53 +1000,6 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     }
     terms[gid] = out;
     if (L.kind) inf_st[gid] = st;
-    // queue the rays, one atomic per wave; a wave's rays stay together in the queue (coherent walks)
-    const uint64_t m1 = __builtin_amdgcn_ballot_w64(need1), m2 = __builtin_amdgcn_ballot_w64(need2);
-    if ((m1 | m2) == 0) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const uint64_t below = (1ull << lane) - 1ull;
-    int base = 0;
-    if (lane == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
-        base = atomicAdd(rq.count, (int)(__builtin_popcountll(m1) + __builtin_popcountll(m2)));
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (need1) {
-        const int k = base + (int)__builtin_popcountll(m1 & below);
-        rq.ray[2 * (size_t)k] = make_float4(r1o.x, r1o.y, r1o.z, r1min);
-        rq.ray[2 * (size_t)k + 1] = make_float4(r1d.x, r1d.y, r1d.z, r1max);
-        rq.id[k] = (uint32_t)gid << 2;
-    }
-    if (need2) {
-        const int k = base + (int)__builtin_popcountll(m1) + (int)__builtin_popcountll(m2 & below);
-        rq.ray[2 * (size_t)k] = make_float4(r2o.x, r2o.y, r2o.z, reps);
-        rq.ray[2 * (size_t)k + 1] = make_float4(r2d.x, r2d.y, r2d.z, r2max);
-        rq.id[k] = ((uint32_t)gid << 2) | 2u | (strict2 ? 1u : 0u);
-    }
-}
-
-// The queued rays of shade_direct_kernel, 64 consecutive rays per wave: one any-hit walk each
-// (trace_any_wave: area-light spheres too unless strict; strict: only triangles with t < maxt
-// count). A blocked ray clears its term's lobe (kind 0: direct_combine_kernel skips the term).
-__global__ __launch_bounds__(256) void trace_rays_kernel(RenderScene sc, RayQueue rq, DirectTerms *terms) {
-    const int n = *rq.count;
-    const int lane = (int)(threadIdx.x & 63);
-    const int nw = (int)(gridDim.x * (blockDim.x >> 6));
-    for (int base = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < n; base += nw * 64) {
-        const int k = base + lane;
-        const bool act = k < n;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = make_float4(1.f, 1.f, 1.f, 0.f);
-        uint32_t id = 0;
-        if (act) {
-            a = rq.ray[2 * (size_t)k];
-            b = rq.ray[2 * (size_t)k + 1];
-            id = rq.id[k];
-        }
-        const bool strict = (id & 1u) != 0;
-        const bool occ = trace_any_wave(sc, V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, a.w, b.w, act, strict, !strict);
-        if (act && occ) {
-            uint32_t *t = reinterpret_cast<uint32_t *>(terms + (id >> 2));
-            t[(id & 2u) ? offsetof(DirectTerms, l2) / 4 : offsetof(DirectTerms, l1) / 4] = 0u;  // Lobe::kind
-        }
-    }
 }
 
 // ------------------------------------------------------------------ textures

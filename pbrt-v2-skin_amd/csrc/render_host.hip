@@ -663,9 +663,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 grow(ws->spill, have, total / spp, 1);
                 ws->px = total / spp;
             }
-            if (!ws->ray_count.ptr) ws->ray_count.alloc(1);
             MPSS_HIP(hipMemsetAsync(ws->count.ptr, 0, sizeof(int), stream));
-            MPSS_HIP(hipMemsetAsync(ws->ray_count.ptr, 0, sizeof(int), stream));
             MPSS_HIP(hipMemsetAsync(ws->spill.ptr, 0, sizeof(uint32_t) * (size_t)(total / spp), stream));
             auto recs = [&](int64_t off) {  // (the per-hit pointers are read after the hit-count resize)
                 return SampleRecs{ws->flags.ptr + off, ws->spill.ptr + off / spp, ws->slot.ptr + off, ws->ld.ptr,
@@ -732,7 +730,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             {
                 const SampleRecs rec = recs(0);
                 const int64_t lanes = nh * std::max<int64_t>(1, (int64_t)nlights) * ns_max;
-                if (lanes >= ((int64_t)1 << 30))  // RayQueue ids carry the lane in 30 bits
+                if (lanes > (int64_t)INT32_MAX)
                     throw Error(MPSS_ERR_INVALID, "render_tile: too many light samples per batch; lower "
                                                   "max_batch_samples");
                 grow(ws->terms, ws->terms_n, lanes, 64);
@@ -742,24 +740,13 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                     grow(ws->st, ws->st_n, lanes, 1);
                     inf_st = ws->st.ptr;
                 }
-                if (ws->ray_n < 2 * lanes) {  // <= 2 visibility rays per direct-light lane
-                    int64_t have = ws->ray_n;
-                    grow(ws->rays, have, 2 * lanes, 2);
-                    have = ws->ray_n;
-                    grow(ws->ray_id, have, 2 * lanes, 1);
-                    ws->ray_n = 2 * lanes;
-                }
-                const RayQueue rq{ws->rays.ptr, ws->ray_id.ptr, ws->ray_count.ptr};
                 time_begin(timing, stream, ev);
                 if (sc.any_tex)
                     hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, sc,
                                        rec, spp, seed, (int)nh);
                 if (nlights > 0) {
                     hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
-                                       stream, sc, rec, spp, seed, (int)nh, ns_max, terms, inf_st, rq);
-                    // persistent: 8 waves per CU's worth of workgroups walk the queue
-                    const int64_t tblocks = std::min<int64_t>((2 * lanes + 255) / 256, 2048);
-                    hipLaunchKernelGGL(trace_rays_kernel, dim3((unsigned)tblocks), dim3(256), 0, stream, sc, rq, terms);
+                                       stream, sc, rec, spp, seed, (int)nh, ns_max, terms, inf_st);
                     if (sc.n_infinite > 0)
                         hipLaunchKernelGGL(direct_combine_kernel<true>, dim3((unsigned)((nh + 255) / 256)), dim3(256),
                                            0, stream, sc, rec, (int)nh, ns_max, (const DirectTerms *)terms,
