@@ -816,6 +816,33 @@ __device__ __forceinline__ float lobe_value(const RenderMaterial &mat, const Lob
     return L.kind == 1u ? mat.R[c] * L.a * L.b * L.c / L.d : (mat.T[c] * L.a) * (1.f - L.b);
 }
 
+// x / d (IEEE, correctly rounded) for many x over one d, from inv = x-independent RN(1 / d): with
+// q = RN(x inv) and the exact residual r = x - d q (one FMA), RN(q + r inv) is RN(x / d) -- Markstein's
+// correction, valid when nothing under- or overflows (it replaces the ~10-instruction IEEE division
+// sequence by 3 instructions; tools/check_div.c runs it against x / d on 2e8 random operand pairs, 0
+// differences). Outside the guarded range, and when d itself is out of range (dok false), it divides.
+__device__ __forceinline__ float div_by(float x, float d, float inv, bool dok) {
+    const float q = x * inv;
+    const float r = __builtin_fmaf(-d, q, x);
+    const float q1 = __builtin_fmaf(r, inv, q);
+    const float ax = fabsf(x), aq = fabsf(q1);
+    if (dok && ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f) return q1;
+    return x / d;
+}
+struct Den {  // one denominator shared by the 30 bands
+    float d, inv;
+    bool ok;
+};
+__device__ __forceinline__ Den make_den(float d) {
+    const float ad = fabsf(d);
+    return Den{d, 1.f / d, ad >= 0x1p-60f && ad <= 0x1p60f};
+}
+// lobe_value with the reflection lobe's division by L.d done through den = make_den(L.d)
+__device__ __forceinline__ float lobe_value_den(const RenderMaterial &mat, const Lobe &L, int c, const Den &den) {
+    return L.kind == 1u ? div_by(mat.R[c] * L.a * L.b * L.c, den.d, den.inv, den.ok)
+                        : (mat.T[c] * L.a) * (1.f - L.b);
+}
+
 __device__ __forceinline__ bool lobe_black(const RenderMaterial &mat, const Lobe &L) {
     if (L.kind == 0u) return true;
     for (int c = 0; c < NB; ++c)
@@ -1098,18 +1125,20 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
                 inf_lookup(L, st.x, st.y, rgb1);
                 inf_lookup(L, st.z, st.w, rgb2);
             }
+            const Den d1 = make_den(e.l1.d), d2 = make_den(e.l2.d), dp = make_den(e.pdf2);
 #pragma unroll
             for (int c = 0; c < NB; ++c) {
                 const float Li1 = inf ? illum_band(rgb1, c) : L.Lemit[c];
                 const float Li2 = inf ? illum_band(rgb2, c) : L.Lemit[c];
                 float ed = 0.f;
-                if (e.l1.kind) ed += lobe_value(mat, e.l1, c) * Li1 * e.k1;
-                if (e.l2.kind) ed += lobe_value(mat, e.l2, c) * Li2 * e.adn * e.w2 / e.pdf2;
+                if (e.l1.kind) ed += lobe_value_den(mat, e.l1, c, d1) * Li1 * e.k1;
+                if (e.l2.kind) ed += div_by(lobe_value_den(mat, e.l2, c, d2) * Li2 * e.adn * e.w2, dp.d, dp.inv, dp.ok);
                 Ld[c] += ed;
             }
         }
+        const Den dn = make_den((float)ns);
 #pragma unroll
-        for (int c = 0; c < NB; ++c) ld[c] += Ld[c] / (float)ns;
+        for (int c = 0; c < NB; ++c) ld[c] += div_by(Ld[c], dn.d, dn.inv, dn.ok);
     }
     float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
 #pragma unroll
