@@ -81,6 +81,9 @@ float o_sample_profile(const float *data, int len, float rcp, float dsq);
 /* ---- rho table (multipole.cpp:466-549; reflection.cpp:132-153,228-240,391-403,548-580,623-652) ---- */
 void o_rho_table(float roughness, float eta, int n_entries /*1025*/, int sqrt_samples /*256*/,
                  int nthreads, float *hd, float *hh);
+/* doublerefsslf: fixed != 0 -> FixedFresnelDielectric (reflection.h:315-324) in the Microfacet */
+void o_rho_table_ex(float roughness, float eta, int fixed, int n_entries, int sqrt_samples, int nthreads, float *hd,
+                    float *hh);
 uint32_t o_mt_first(uint32_t seed, int n, uint32_t *out); /* MT19937 stream check */
 /* MT19937, core/rng.cpp (RNG::Seed, RNG::RandomUInt) */
 typedef struct { uint32_t mt[624]; int mti; } o_mt;

@@ -153,6 +153,7 @@ typedef struct {
     int L;
     float rcp[O_NB];
     int rgb; /* rgbprofile: rd rows 0..2 = R, G, B (multipole.cpp:85-107) */
+    int lambert; /* the area-light sphere's default "matte" material: one Lambertian(R) BxDF */
 } o_mat;
 
 typedef struct { float bmin[3], bmax[3]; int left, right, first, count; } o_bnode;
@@ -818,6 +819,33 @@ static float mt_pdf(const o_mat *m, v3 wo, v3 wi) {
     pdf *= 4 * cosi * cosi * et * et / den;
     return pdf;
 }
+/* ConcentricSampleDisk (montecarlo.cpp:306-348); theta *= M_PI / 4.f is a double product */
+static void concentric_disk(float u1, float u2, float *dx, float *dy) {
+    float r, theta;
+    float sx = 2 * u1 - 1, sy = 2 * u2 - 1;
+    if (sx == 0.0 && sy == 0.0) { *dx = 0.f; *dy = 0.f; return; }
+    if (sx >= -sy) {
+        if (sx > sy) { r = sx; theta = sy > 0.0 ? sy / r : 8.0f + sy / r; }
+        else { r = sy; theta = 2.0f - sx / r; }
+    } else {
+        if (sx <= sy) { r = -sx; theta = 4.0f - sy / r; }
+        else { r = -sy; theta = 6.0f + sx / r; }
+    }
+    theta = (float)((double)theta * (3.14159265358979323846 / 4.0));
+    *dx = r * fcos(theta);
+    *dy = r * fsin(theta);
+}
+/* Lambertian::f = R * INV_PI; BxDF::Pdf: SameHemisphere ? AbsCosTheta(wi) * INV_PI : 0;
+ * BxDF::Sample_f: CosineSampleHemisphere (montecarlo.h:128-133), z flipped to wo's side
+ * (reflection.h, reflection.cpp:566-578) */
+static float lambert_pdf(v3 wo, v3 wi) { return wo.z * wi.z > 0.f ? fabsf(wi.z) * INV_PI_F : 0.f; }
+static void lambert_sample(v3 wo, float u1, float u2, v3 *wi, float *pdf) {
+    float x, y;
+    concentric_disk(u1, u2, &x, &y);
+    *wi = mk(x, y, sqrtf(fmaxf(0.f, 1.f - x * x - y * y)));
+    if (wo.z < 0.f) wi->z *= -1.f;
+    *pdf = lambert_pdf(wo, *wi);
+}
 static void mf_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *pdf);
 static void mt_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *pdf) {
     mf_sample(m, wo, u1, u2, wi, pdf);
@@ -843,7 +871,11 @@ static void mt_sample(const o_mat *m, v3 wo, float u1, float u2, v3 *wi, float *
  * local wi rather than re-projecting the world one). */
 static int bsdf_f(const o_mat *m, const frame_t *fr, v3 woW, v3 wiW, v3 wol, v3 wil, float f[O_NB]) {
     int ok;
-    if (dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)
+    if (m->lambert) { /* one BRDF: f = 0 + R * INV_PI on the reflection side */
+        if (!(dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)) return 0;
+        for (int c = 0; c < O_NB; ++c) f[c] = 0.f + m->R[c] * INV_PI_F;
+        ok = 1;
+    } else if (dot(wiW, fr->ng) * dot(woW, fr->ng) > 0.f)
         ok = m->has_refl && mf_f(m, wol, wil, f);
     else
         ok = m->has_trans && mt_f(m, wol, wil, f);
@@ -858,7 +890,8 @@ static float bsdf_pdf(const o_mat *m, v3 wo, v3 wi) {
     int n = m->has_refl + m->has_trans;
     if (n == 0) return 0.f;
     float pdf = 0.f;
-    if (m->has_refl) pdf += mf_pdf(m, wo, wi);
+    if (m->lambert) pdf += lambert_pdf(wo, wi);
+    else if (m->has_refl) pdf += mf_pdf(m, wo, wi);
     if (m->has_trans) pdf += mt_pdf(m, wo, wi);
     return pdf / (float)n;
 }
@@ -1288,6 +1321,109 @@ static void to_xyz(const float L[O_NB], float xyz[3]) { /* Spectrum::ToXYZ + sam
     xyz[0] = X; xyz[1] = Y; xyz[2] = Z;
 }
 
+/* Sphere::Intersect's DifferentialGeometry at the camera ray's thit (sphere.cpp:114-152, object
+ * space = world - centre) and the BSDF frame on it (reflection.cpp:754-762): nn = Normalize(Cross(dpdu,
+ * dpdv)) = ng, sn = Normalize(dpdu), tn = Cross(nn, sn) */
+static frame_t sphere_frame(const o_light *L, v3 o, v3 d, float t) {
+    frame_t fr;
+    memset(&fr, 0, sizeof(fr));
+    v3 ph = add(sub(o, L->c), mul(d, t));
+    if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * L->r;
+    float cz = ph.z / L->r;
+    float theta = facos(cz < -1.f ? -1.f : (cz > 1.f ? 1.f : cz));
+    float zr = sqrtf(ph.x * ph.x + ph.y * ph.y);
+    float izr = 1.f / zr;
+    float cphi = ph.x * izr, sphi = ph.y * izr;
+    v3 dpdu = mk(-L->phimax * ph.y, L->phimax * ph.x, 0.f);
+    v3 dpdv = mul(mk(ph.z * cphi, ph.z * sphi, -L->r * fsin(theta)), L->thetamax - L->thetamin);
+    fr.p = add(ph, L->c);
+    fr.nn = fr.ng = nrm(crs(dpdu, dpdv));
+    fr.sn = nrm(dpdu);
+    fr.tn = crs(fr.nn, fr.sn);
+    return fr;
+}
+
+/* UniformSampleAllLights -> EstimateDirect (integrator.cpp:47-174) at shading point fr->p with
+ * BSDF mat (its frame fr), rayEpsilon reps; row: reference-sampler values or NULL (hashes) */
+static void direct_light(const o_scene *s, int spp, uint32_t seed, uint32_t pix, int si, const float *row,
+                         const o_mat *mat, const frame_t *pfr, float reps, v3 wo, float ld[O_NB]) {
+    for (int c = 0; c < O_NB; ++c) ld[c] = 0.f;
+    for (int l = 0; l < s->nlights; ++l) {
+        const o_light *Lt = &s->lights[l];
+        const int ns = Lt->ns_pow2;
+        float Ld[O_NB];
+        for (int c = 0; c < O_NB; ++c) Ld[c] = 0.f;
+        uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + D_PERM) & (uint32_t)(spp - 1)) : 0u;
+        uint32_t base = (uint32_t)(si ^ xr) * (uint32_t)ns;
+        uint32_t a0 = hash3(seed, pix, 16u * l + D_LIGHT_POS), a1 = hash3(seed, pix, 16u * l + D_LIGHT_POS + 8u);
+        uint32_t b0 = hash3(seed, pix, 16u * l + D_BSDF_DIR), b1 = hash3(seed, pix, 16u * l + D_BSDF_DIR + 8u);
+        uint32_t bc = hash3(seed, pix, 16u * l + D_BSDF_COMP);
+        for (int j = 0; j < ns; ++j) {
+            uint32_t k = base + (uint32_t)j;
+            float ed[O_NB], f[O_NB];
+            for (int c = 0; c < O_NB; ++c) ed[c] = 0.f;
+            /* LightSample(sample, lightSampleOffsets[l], j), BSDFSample(sample, bsdfSampleOffsets[l], j) */
+            float lu0, lu1, ubc, ub0, ub1;
+            if (row) {
+                const float *e = row + s->lights[l].replay_off + 5 * j;
+                lu0 = e[0]; lu1 = e[1]; ubc = e[2]; ub0 = e[3]; ub1 = e[4];
+            } else {
+                lu0 = vdc(k, a0); lu1 = sobol(k, a1); ubc = vdc(k, bc); ub0 = vdc(k, b0); ub1 = sobol(k, b1);
+            }
+            lsamp ls = light_sample(Lt, pfr->p, reps, lu0, lu1);
+            float lightPdf = ls.pdf;
+            if (lightPdf > 0.f && ls.nonblack && (mat->has_refl || mat->has_trans)) {
+                if (bsdf_f(mat, pfr, wo, ls.wi, to_local(pfr, wo), to_local(pfr, ls.wi), f) &&
+                    !occluded(s, ls.so, ls.sd, ls.smint, ls.smaxt)) {
+                    float bsdfPdf = bsdf_pdf(mat, to_local(pfr, wo), to_local(pfr, ls.wi));
+                    float w = power_h(lightPdf, bsdfPdf);
+                    float k1 = absdot(ls.wi, pfr->nn) * w / lightPdf;
+                    for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * ls.Li[c] * k1;
+                }
+            }
+            int ncomp = mat->has_refl + mat->has_trans;
+            if (ncomp > 0) {
+                /* BSDF::Sample_f: component by uComponent, R before T */
+                int which = (int)floorf(ubc * (float)ncomp);
+                if (which > ncomp - 1) which = ncomp - 1;
+                int pick_t = !mat->has_refl || which == 1;
+                v3 wil, wol = to_local(pfr, wo);
+                float bsdfPdf;
+                if (pick_t) mt_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
+                else if (mat->lambert) lambert_sample(wol, ub0, ub1, &wil, &bsdfPdf);
+                else mf_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
+                if (bsdfPdf != 0.f) {
+                    v3 wi = to_world(pfr, wil);
+                    if (ncomp > 1) {
+                        bsdfPdf += pick_t ? mf_pdf(mat, wol, wil) : mt_pdf(mat, wol, wil);
+                        bsdfPdf /= (float)ncomp;
+                    }
+                    if (bsdf_f(mat, pfr, wo, wi, to_local(pfr, wo), wil, f) && bsdfPdf > 0.f) {
+                        lightPdf = Lt->kind ? inf_pdf(Lt, wi) : light_pdf(Lt, pfr->p, wi);
+                        if (lightPdf != 0.f) {
+                            float w = power_h(bsdfPdf, lightPdf);
+                            hit_t hl = intersect(s, pfr->p, wi, reps, INFINITY);
+                            float Li[O_NB];
+                            memset(Li, 0, sizeof(Li));
+                            if (hl.tri != NO_HIT) { /* Li = lightIsect.Le(-wi) if it is this light */
+                                if (hl.tri == -1 - l && dot(hl.lnn, neg(wi)) > 0.f) memcpy(Li, Lt->Le, sizeof(Li));
+                            } else if (Lt->kind) { /* Li = light->Le(ray) */
+                                inf_le_dir(Lt, wi, Li);
+                            }
+                            if (!black(Li)) {
+                                float adn = absdot(wi, pfr->nn);
+                                for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Li[c] * adn * w / bsdfPdf;
+                            }
+                        }
+                    }
+                }
+            }
+            for (int c = 0; c < O_NB; ++c) Ld[c] += ed[c];
+        }
+        for (int c = 0; c < O_NB; ++c) ld[c] += Ld[c] / (float)ns;
+    }
+}
+
 /* row: the sample's reference-sampler values (o_replay_render_table layout) or NULL (hashes) */
 static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, int si, float X, float Y,
                       const float *row, float xyz[3]) {
@@ -1309,10 +1445,21 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
         to_xyz(L, xyz);
         return;
     }
-    if (h.tri < 0) { /* an area light's own surface: emitted radiance only */
+    if (h.tri < 0) { /* an area light's own sphere (multipolesubsurface.cpp:253-304): L = Le(wo), then
+                      * Ld from every light at the sphere point with the shape's material -- pbrt's
+                      * default "matte" (api.cpp:241,1085; matte.cpp:49-71: Kd 0.5, sigma 0, one
+                      * Lambertian) -- and no BSSRDF; SpecularReflect/Transmit add 0 */
         const o_light *Lt = &s->lights[-1 - h.tri];
         if (dot(h.lnn, neg(d)) > 0.f)
             for (int c = 0; c < O_NB; ++c) L[c] += Lt->Le[c];
+        /* R = Spectrum(0.5f); only lambert / has_refl / R are read */
+#define H5 0.5f, 0.5f, 0.5f, 0.5f, 0.5f
+        static const o_mat matte = {.R = {H5, H5, H5, H5, H5, H5}, .has_refl = 1, .lambert = 1};
+#undef H5
+        frame_t fr = sphere_frame(Lt, o, d, h.t);
+        float ld[O_NB];
+        direct_light(s, spp, seed, pix, si, row, &matte, &fr, 5e-4f * h.t, neg(d), ld); /* sphere.cpp:155 */
+        for (int c = 0; c < O_NB; ++c) L[c] += ld[c];
         to_xyz(L, xyz);
         return;
     }
@@ -1359,82 +1506,8 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
             L[c] += t < 0.f ? 0.f : t;
         }
     }
-    /* UniformSampleAllLights -> EstimateDirect (integrator.cpp:47-174) */
     float ld[O_NB];
-    for (int c = 0; c < O_NB; ++c) ld[c] = 0.f;
-    for (int l = 0; l < s->nlights; ++l) {
-        const o_light *Lt = &s->lights[l];
-        const int ns = Lt->ns_pow2;
-        float Ld[O_NB];
-        for (int c = 0; c < O_NB; ++c) Ld[c] = 0.f;
-        uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + D_PERM) & (uint32_t)(spp - 1)) : 0u;
-        uint32_t base = (uint32_t)(si ^ xr) * (uint32_t)ns;
-        uint32_t a0 = hash3(seed, pix, 16u * l + D_LIGHT_POS), a1 = hash3(seed, pix, 16u * l + D_LIGHT_POS + 8u);
-        uint32_t b0 = hash3(seed, pix, 16u * l + D_BSDF_DIR), b1 = hash3(seed, pix, 16u * l + D_BSDF_DIR + 8u);
-        uint32_t bc = hash3(seed, pix, 16u * l + D_BSDF_COMP);
-        for (int j = 0; j < ns; ++j) {
-            uint32_t k = base + (uint32_t)j;
-            float ed[O_NB], f[O_NB];
-            for (int c = 0; c < O_NB; ++c) ed[c] = 0.f;
-            /* LightSample(sample, lightSampleOffsets[l], j), BSDFSample(sample, bsdfSampleOffsets[l], j) */
-            float lu0, lu1, ubc, ub0, ub1;
-            if (row) {
-                const float *e = row + s->lights[l].replay_off + 5 * j;
-                lu0 = e[0]; lu1 = e[1]; ubc = e[2]; ub0 = e[3]; ub1 = e[4];
-            } else {
-                lu0 = vdc(k, a0); lu1 = sobol(k, a1); ubc = vdc(k, bc); ub0 = vdc(k, b0); ub1 = sobol(k, b1);
-            }
-            lsamp ls = light_sample(Lt, fr.p, reps, lu0, lu1);
-            float lightPdf = ls.pdf;
-            if (lightPdf > 0.f && ls.nonblack && (mat->has_refl || mat->has_trans)) {
-                if (bsdf_f(mat, &fr, wo, ls.wi, to_local(&fr, wo), to_local(&fr, ls.wi), f) &&
-                    !occluded(s, ls.so, ls.sd, ls.smint, ls.smaxt)) {
-                    float bsdfPdf = bsdf_pdf(mat, to_local(&fr, wo), to_local(&fr, ls.wi));
-                    float w = power_h(lightPdf, bsdfPdf);
-                    float k1 = absdot(ls.wi, fr.nn) * w / lightPdf;
-                    for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * ls.Li[c] * k1;
-                }
-            }
-            int ncomp = mat->has_refl + mat->has_trans;
-            if (ncomp > 0) {
-                /* BSDF::Sample_f: component by uComponent, R before T */
-                int which = (int)floorf(ubc * (float)ncomp);
-                if (which > ncomp - 1) which = ncomp - 1;
-                int pick_t = !mat->has_refl || which == 1;
-                v3 wil, wol = to_local(&fr, wo);
-                float bsdfPdf;
-                if (pick_t) mt_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
-                else mf_sample(mat, wol, ub0, ub1, &wil, &bsdfPdf);
-                if (bsdfPdf != 0.f) {
-                    v3 wi = to_world(&fr, wil);
-                    if (ncomp > 1) {
-                        bsdfPdf += pick_t ? mf_pdf(mat, wol, wil) : mt_pdf(mat, wol, wil);
-                        bsdfPdf /= (float)ncomp;
-                    }
-                    if (bsdf_f(mat, &fr, wo, wi, to_local(&fr, wo), wil, f) && bsdfPdf > 0.f) {
-                        lightPdf = Lt->kind ? inf_pdf(Lt, wi) : light_pdf(Lt, fr.p, wi);
-                        if (lightPdf != 0.f) {
-                            float w = power_h(bsdfPdf, lightPdf);
-                            hit_t hl = intersect(s, fr.p, wi, reps, INFINITY);
-                            float Li[O_NB];
-                            memset(Li, 0, sizeof(Li));
-                            if (hl.tri != NO_HIT) { /* Li = lightIsect.Le(-wi) if it is this light */
-                                if (hl.tri == -1 - l && dot(hl.lnn, neg(wi)) > 0.f) memcpy(Li, Lt->Le, sizeof(Li));
-                            } else if (Lt->kind) { /* Li = light->Le(ray) */
-                                inf_le_dir(Lt, wi, Li);
-                            }
-                            if (!black(Li)) {
-                                float adn = absdot(wi, fr.nn);
-                                for (int c = 0; c < O_NB; ++c) ed[c] += f[c] * Li[c] * adn * w / bsdfPdf;
-                            }
-                        }
-                    }
-                }
-            }
-            for (int c = 0; c < O_NB; ++c) Ld[c] += ed[c];
-        }
-        for (int c = 0; c < O_NB; ++c) ld[c] += Ld[c] / (float)ns;
-    }
+    direct_light(s, spp, seed, pix, si, row, mat, &fr, reps, wo, ld);
     for (int c = 0; c < O_NB; ++c) L[c] += ld[c];
     to_xyz(L, xyz);
 }

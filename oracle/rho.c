@@ -4,7 +4,8 @@
  * Beckmann(roughness)) (materials/layeredskin.cpp:104-109), i.e. BxDF::rho
  * (core/reflection.cpp:623-652) with Microfacet::Sample_f/f (reflection.cpp:228-240,
  * 391-397), Beckmann::D/Sample_f (reflection.h:507-529, reflection.cpp:548-570),
- * FresnelDielectric::Evaluate + FrDiel (reflection.cpp:62-84,132-153), KahanSum
+ * FresnelDielectric::Evaluate + FrDiel (reflection.cpp:62-84,132-153) -- or, with LayeredSkin's
+ * "doublerefsslf", FixedFresnelDielectric (reflection.h:315-324; layeredskin.cpp:105) --, KahanSum
  * (core/kahansum.h), StratifiedSample2D (montecarlo.cpp:158-168) and MT19937
  * (core/rng.cpp).  All channels of this BxDF are equal (R=1, spectrally flat
  * Fresnel), so the table is computed as scalars and replicated. */
@@ -80,7 +81,7 @@ static float fs(float x) { return (float)sin((double)x); }
 typedef struct { float x, y, z; } v3;
 static float dot3(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
-typedef struct { float rms2, rcp_rms2, eta; } mf;
+typedef struct { float rms2, rcp_rms2, eta; int fixed; } mf;
 
 static float beck_d(const mf *m, v3 wh) { /* reflection.h:514-521 */
     float ct = fabsf(wh.z);
@@ -124,6 +125,7 @@ static float mf_f(const mf *m, v3 wo, v3 wi) { /* reflection.cpp:228-240 with R 
     wh.x *= inv; wh.y *= inv; wh.z *= inv;
     float cth = dot3(wi, wh);
     float F = fresnel_diel(cth, 1.f, m->eta);
+    if (m->fixed) F = F + (F * (1.f - F)) * (1.f - F); /* FixedFresnelDielectric: val + val (1 - val)(1 - val) */
     return 1.f * beck_d(m, wh) * mf_G(wo, wi, wh) * F / (4.f * cti * cto);
 }
 
@@ -219,12 +221,18 @@ static float rho_hh(const mf *m, int sq) {
 }
 
 void o_rho_table(float roughness, float eta, int n_entries, int sqrt_samples, int nthreads, float *hd, float *hh) {
+    o_rho_table_ex(roughness, eta, 0, n_entries, sqrt_samples, nthreads, hd, hh);
+}
+
+void o_rho_table_ex(float roughness, float eta, int fixed, int n_entries, int sqrt_samples, int nthreads, float *hd,
+                    float *hh) {
     rho_job j;
     memset(&j, 0, sizeof(j));
     float rms = roughness < 1e-3f ? 1e-3f : roughness; /* Beckmann ctor, reflection.h:509-513 */
     j.m.rms2 = rms * rms;
     j.m.rcp_rms2 = 1 / j.m.rms2;
     j.m.eta = eta;
+    j.m.fixed = fixed;
     j.sqrt_samples = sqrt_samples;
     j.n_entries = n_entries;
     j.hd = hd;

@@ -490,4 +490,70 @@ MPSS_HD float power_heuristic(float fpdf, float gpdf) {  // montecarlo.h:270-273
     return (f * f) / (f * f + g * g);
 }
 
+// ---------------------------------------------------------------- the light sphere's own surface
+// An area light's sphere carries pbrt's default material, "matte" (api.cpp:241,1085): Kd =
+// Spectrum(0.5f), sigma 0 -> one Lambertian BRDF (matte.cpp:49-71). f = R * INV_PI.
+constexpr float kMatteF = 0.5f * 0.31830988618379067154f;
+
+// ConcentricSampleDisk (montecarlo.cpp:306-348); `theta *= M_PI / 4.f` is a double product
+MPSS_HD void concentric_disk(float u1, float u2, float &dx, float &dy) {
+    float r, theta;
+    const float sx = 2 * u1 - 1, sy = 2 * u2 - 1;
+    if (sx == 0.f && sy == 0.f) {
+        dx = dy = 0.f;
+        return;
+    }
+    if (sx >= -sy) {
+        if (sx > sy) {
+            r = sx;
+            theta = sy > 0.f ? sy / r : 8.0f + sy / r;
+        } else {
+            r = sy;
+            theta = 2.0f - sx / r;
+        }
+    } else if (sx <= sy) {
+        r = -sx;
+        theta = 4.0f - sy / r;
+    } else {
+        r = -sy;
+        theta = 6.0f + sx / r;
+    }
+    theta = (float)((double)theta * (3.14159265358979323846 / 4.0));
+    dx = r * m_cos(theta);
+    dy = r * m_sin(theta);
+}
+
+// BxDF::Pdf / Sample_f defaults for the Lambertian (reflection.cpp): SameHemisphere ? |cos wi| / pi : 0;
+// wi = CosineSampleHemisphere(u1, u2) (montecarlo.h:128-133), z turned to wo's side
+MPSS_HD float lambert_pdf(V3 wo, V3 wi) { return wo.z * wi.z > 0.f ? fabsf(wi.z) * 0.31830988618379067154f : 0.f; }
+MPSS_HD void lambert_sample(V3 wo, float u1, float u2, V3 &wi, float &pdf) {
+    float x, y;
+    concentric_disk(u1, u2, x, y);
+    wi = V3{x, y, sqrtf(fmaxf(0.f, 1.f - x * x - y * y))};
+    if (wo.z < 0.f) wi.z *= -1.f;
+    pdf = lambert_pdf(wo, wi);
+}
+
+// Sphere::Intersect's DifferentialGeometry at a camera ray's thit (sphere.cpp:114-152; object space =
+// world - centre) and the BSDF frame on it (reflection.cpp:754-762): nn = Normalize(Cross(dpdu, dpdv))
+// = ng (no shading normals), sn = Normalize(dpdu), tn = Cross(nn, sn).
+MPSS_HD ShadingFrame sphere_frame(const SphereView &s, V3 o, V3 d, float t) {
+    ShadingFrame fr{};
+    V3 ph = (o - s.c) + d * t;
+    if (ph.x == 0.f && ph.y == 0.f) ph.x = 1e-5f * s.r;
+    const float cz = ph.z / s.r;
+    const float theta = m_acos(cz < -1.f ? -1.f : (cz > 1.f ? 1.f : cz));
+    const float zr = sqrtf(ph.x * ph.x + ph.y * ph.y);
+    const float izr = 1.f / zr;
+    const float cphi = ph.x * izr, sphi = ph.y * izr;
+    const V3 dpdu = V3{-s.phi_max * ph.y, s.phi_max * ph.x, 0.f};
+    const V3 dpdv = V3{ph.z * cphi, ph.z * sphi, -s.r * m_sin(theta)} * (s.theta_max - s.theta_min);
+    fr.p = ph + s.c;
+    fr.nn = normalize(cross(dpdu, dpdv));
+    fr.ng = fr.nn;
+    fr.sn = normalize(dpdu);
+    fr.tn = cross(fr.nn, fr.sn);
+    return fr;
+}
+
 }  // namespace mpss

@@ -125,7 +125,17 @@ enum : uint32_t {
     // carries it into the neighbour: left (x-1), right (x+1), up (y-1), down (y+1)
     REC_XLO = 16u, REC_XHI = 32u, REC_YLO = 64u, REC_YHI = 128u,
     REC_LIGHT_SHIFT = 8,
-    REC_MAT_SHIFT = 16
+    REC_MAT_SHIFT = 16,
+    REC_LSURF = 1u << 24  // hit an area light's sphere: its surface is shaded (default matte), Ld valid
+};
+
+// hit_s of a compacted slot: sample index (bits 0-15) | material, or light index for HS_LIGHT records
+// (bits 16-23; 0xff = a miss with infinite lights) | flags
+enum : uint32_t {
+    HS_LE = 1u << 28,     // HS_LIGHT: the light sphere faces the camera ray (Le(wo) counts)
+    HS_LSURF = 1u << 29,  // HS_LIGHT: a light sphere's surface, shaded with the default matte material
+    HS_LIGHT = 1u << 30,  // a light seen directly (no mesh surface, no Mo())
+    HS_SSS = 1u << 31     // a mesh surface whose material has a MultipoleBSSRDF
 };
 
 // Per camera sample: flags and the slot of its surface hit; per surface hit (compacted, one

@@ -744,9 +744,10 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList 
     if (live) {
         if (h.tri == INT_MIN) {  // SamplerRenderer::Li: Li += lights[i]->Le(ray) for every light
             if (sc.n_infinite > 0) flags |= REC_LE | (0xffu << REC_LIGHT_SHIFT);
-        } else if (h.tri < 0) {  // an area light's own surface: Le only
+        } else if (h.tri < 0) {  // an area light's own sphere: Le(wo) if it faces wo, then matte shading
             const int l = -1 - h.tri;
-            if (dot(h.lnn, -d) > 0.f) flags |= REC_LE | ((uint32_t)l << REC_LIGHT_SHIFT);
+            flags |= REC_LSURF | ((uint32_t)l << REC_LIGHT_SHIFT);
+            if (dot(h.lnn, -d) > 0.f) flags |= REC_LE;
         } else if (h.tri != INT_MIN) {
             const uint32_t mid = sc.meshes[sc.tri_mesh[h.tri]].material;
             flags |= REC_SURF | (mid << REC_MAT_SHIFT);
@@ -754,7 +755,7 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList 
         }
     }
     // every sample with radiance (a surface hit, or an area light seen directly) gets a slot
-    const bool surf = (flags & REC_SURF) != 0, has_l = surf || (flags & REC_LE);
+    const bool surf = (flags & REC_SURF) != 0, has_l = surf || (flags & (REC_LE | REC_LSURF));
     const uint64_t m = __builtin_amdgcn_ballot_w64(has_l);
     const int lane = (int)(threadIdx.x & 63);
     int base = 0;
@@ -768,11 +769,14 @@ __global__ __launch_bounds__(256) void primary_kernel(RenderScene sc, PieceList 
         rec.hit_a[slot] = make_float4(h.t, h.b1, h.b2, __int_as_float(h.tri));
         rec.hit_b[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(pix));
         // sample index (16 bits) | material (8 bits) | SSS bit 31
-        rec.hit_s[slot] = (uint32_t)s | (flags & (0xffu << REC_MAT_SHIFT)) | ((flags & REC_SSS) ? 0x80000000u : 0u);
+        rec.hit_s[slot] = (uint32_t)s | (flags & (0xffu << REC_MAT_SHIFT)) | ((flags & REC_SSS) ? HS_SSS : 0u);
     } else if (has_l) {
-        // light seen directly: light index (8 bits; 0xff = the infinite lights of a miss) | bit 30
-        rec.hit_s[slot] = (((flags >> REC_LIGHT_SHIFT) & 0xffu) << REC_MAT_SHIFT) | 0x40000000u;
+        // a light seen directly: light index (0xff = the infinite lights of a miss); a light sphere's
+        // surface is also shaded (HS_LSURF), its Le counted when it faces the ray (HS_LE)
+        rec.hit_s[slot] = (uint32_t)s | (((flags >> REC_LIGHT_SHIFT) & 0xffu) << REC_MAT_SHIFT) | HS_LIGHT |
+                          ((flags & REC_LSURF) ? HS_LSURF : 0u) | ((flags & REC_LE) ? HS_LE : 0u);
         rec.hit_b[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(pix));
+        if (flags & REC_LSURF) rec.hit_a[slot] = make_float4(h.t, 0.f, 0.f, __int_as_float(h.tri));
     }
 }
 
@@ -798,22 +802,27 @@ struct Lobe {
     float a, b, c, d;
 };
 
-__device__ __forceinline__ Lobe bsdf_lobe(const RenderMaterial &mat, bool refl, V3 wo_l, V3 wi_l) {
+// The shading point's BSDF is a mesh material's (mat), or -- mat == nullptr -- the default matte of a
+// light sphere seen directly (geom.h kMatteF): kind 3, f = 0 + R * INV_PI on the reflection side.
+__device__ __forceinline__ Lobe bsdf_lobe(const RenderMaterial *mat, bool refl, V3 wo_l, V3 wi_l) {
     Lobe L{0u, 0.f, 0.f, 0.f, 1.f};
-    if (refl) {  // the ng test keeps BRDFs only
-        if (mat.has_refl) {
-            const MfTerms t = microfacet_terms(mat.mf, wo_l, wi_l);
+    if (!mat) {
+        if (refl) L = Lobe{3u, 0.f + kMatteF, 0.f, 0.f, 1.f};
+    } else if (refl) {  // the ng test keeps BRDFs only
+        if (mat->has_refl) {
+            const MfTerms t = microfacet_terms(mat->mf, wo_l, wi_l);
             if (!t.zero) L = Lobe{1u, t.D, t.G, t.F, t.den};
         }
-    } else if (mat.has_trans) {  // ... or BTDFs only
-        const MtTerms t = mt_terms_ool(mat.mf, wo_l, wi_l);
+    } else if (mat->has_trans) {  // ... or BTDFs only
+        const MtTerms t = mt_terms_ool(mat->mf, wo_l, wi_l);
         if (!t.zero) L = Lobe{2u, t.s, t.F, 0.f, 1.f};
     }
     return L;
 }
 
-__device__ __forceinline__ float lobe_value(const RenderMaterial &mat, const Lobe &L, int c) {
-    return L.kind == 1u ? mat.R[c] * L.a * L.b * L.c / L.d : (mat.T[c] * L.a) * (1.f - L.b);
+__device__ __forceinline__ float lobe_value(const RenderMaterial *mat, const Lobe &L, int c) {
+    if (L.kind == 3u) return L.a;
+    return L.kind == 1u ? mat->R[c] * L.a * L.b * L.c / L.d : (mat->T[c] * L.a) * (1.f - L.b);
 }
 
 // x / d (IEEE, correctly rounded) for many x over one d, from inv = x-independent RN(1 / d): with
@@ -838,25 +847,28 @@ __device__ __forceinline__ Den make_den(float d) {
     return Den{d, 1.f / d, ad >= 0x1p-60f && ad <= 0x1p60f};
 }
 // lobe_value with the reflection lobe's division by L.d done through den = make_den(L.d)
-__device__ __forceinline__ float lobe_value_den(const RenderMaterial &mat, const Lobe &L, int c, const Den &den) {
-    return L.kind == 1u ? div_by(mat.R[c] * L.a * L.b * L.c, den.d, den.inv, den.ok)
-                        : (mat.T[c] * L.a) * (1.f - L.b);
+__device__ __forceinline__ float lobe_value_den(const RenderMaterial *mat, const Lobe &L, int c, const Den &den) {
+    if (L.kind == 3u) return L.a;
+    return L.kind == 1u ? div_by(mat->R[c] * L.a * L.b * L.c, den.d, den.inv, den.ok)
+                        : (mat->T[c] * L.a) * (1.f - L.b);
 }
 
-__device__ __forceinline__ bool lobe_black(const RenderMaterial &mat, const Lobe &L) {
+__device__ __forceinline__ bool lobe_black(const RenderMaterial *mat, const Lobe &L) {
     if (L.kind == 0u) return true;
+    if (L.kind == 3u) return false;
     for (int c = 0; c < NB; ++c)
         if (lobe_value(mat, L, c) != 0.f) return false;
     return true;
 }
 
 // BSDF::Pdf (reflection.cpp:736-751): mean of the matching lobes' pdfs, R then T
-__device__ __forceinline__ float bsdf_pdf(const RenderMaterial &mat, V3 wo_l, V3 wi_l) {
-    const int n = mat.has_refl + mat.has_trans;
+__device__ __forceinline__ float bsdf_pdf(const RenderMaterial *mat, V3 wo_l, V3 wi_l) {
+    if (!mat) return lambert_pdf(wo_l, wi_l);  // (0 + pdf) / 1
+    const int n = mat->has_refl + mat->has_trans;
     if (n == 0) return 0.f;
     float pdf = 0.f;
-    if (mat.has_refl) pdf += microfacet_pdf(mat.mf, wo_l, wi_l);
-    if (mat.has_trans) pdf += mt_pdf_ool(mat.mf, wo_l, wi_l);
+    if (mat->has_refl) pdf += microfacet_pdf(mat->mf, wo_l, wi_l);
+    if (mat->has_trans) pdf += mt_pdf_ool(mat->mf, wo_l, wi_l);
     return pdf / (float)n;
 }
 
@@ -885,7 +897,8 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     if (slot >= nhits || slot >= max_hits) return;
     const int lj = (int)(gid % per_hit), l = lj / ns_max, j = lj % ns_max;
     const uint32_t hs = rec.hit_s[slot];
-    if (hs & 0x40000000u) {  // an area light seen directly: no shading point, no Mo()
+    const bool lsurf = (hs & HS_LSURF) != 0;  // a light sphere's own surface: matte, no Mo()
+    if ((hs & HS_LIGHT) && !lsurf) {  // a miss with infinite lights: no shading point, no Mo()
         if (lj == 0) rec.hit_q[slot] = make_float4(0.f, 0.f, 0.f, -1.f);
         return;
     }
@@ -901,18 +914,25 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     const uint32_t pix = __float_as_uint(hb.w);
     const V3 d = V3{hb.x, hb.y, hb.z};
     const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
-    const int mi = sc.tri_mesh[tri], lt = sc.tri_local[tri];
-    const RenderMesh &mesh = sc.meshes[mi];
-    const V3 p = o + d * ha.x;  // Ray::operator()
-    const float reps = 1e-3f * ha.x;
-    ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - ha.y - ha.z, ha.y, ha.z);
     const V3 wo = -d;
-    const RenderMaterial &mat = sc.materials[mid];
-    if (mat.has_bump) {  // BSDF on the bumped dgs: nn, sn = Normalize(dpdu), tn = Cross(nn, sn)
-        const float4 a = rec.hit_frame[2 * (size_t)slot], b = rec.hit_frame[2 * (size_t)slot + 1];
-        fr.nn = V3{a.x, a.y, a.z};
-        fr.sn = V3{b.x, b.y, b.z};
-        fr.tn = cross(fr.nn, fr.sn);
+    ShadingFrame fr;
+    float reps;
+    const RenderMaterial *mat = nullptr;
+    if (lsurf) {  // Sphere::Intersect: rayEpsilon = 5e-4f * thit (sphere.cpp:155)
+        fr = sphere_frame(sc.lights[-1 - tri].s, o, d, ha.x);
+        reps = 5e-4f * ha.x;
+    } else {
+        const RenderMesh &mesh = sc.meshes[sc.tri_mesh[tri]];
+        const V3 p = o + d * ha.x;  // Ray::operator()
+        reps = 1e-3f * ha.x;
+        fr = tri_shading(mesh.view, sc.tri_local[tri], p, 1.f - ha.y - ha.z, ha.y, ha.z);
+        mat = &sc.materials[mid];
+        if (mat->has_bump) {  // BSDF on the bumped dgs: nn, sn = Normalize(dpdu), tn = Cross(nn, sn)
+            const float4 a = rec.hit_frame[2 * (size_t)slot], b = rec.hit_frame[2 * (size_t)slot + 1];
+            fr.nn = V3{a.x, a.y, a.z};
+            fr.sn = V3{b.x, b.y, b.z};
+            fr.tn = cross(fr.nn, fr.sn);
+        }
     }
     if (lj == 0) {
         float ct = absdot(wo, fr.nn);
@@ -920,7 +940,7 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
         rec.hit_q[slot] = make_float4(fr.p.x, fr.p.y, fr.p.z, sss ? ct : -1.f);
         if (j >= ns) return;
     }
-    const int ncomp = mat.has_refl + mat.has_trans;
+    const int ncomp = mat ? mat->has_refl + mat->has_trans : 1;
     const V3 wo_l = to_local(fr, wo);
     const float ng_wo = dot(wo, fr.ng);
     // LightSample(sample, offsets, j) / BSDFSample(sample, offsets, j) (light.cpp, reflection.cpp)
@@ -960,17 +980,19 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     if (ncomp > 0) {
         int which = (int)floorf(ubc * (float)ncomp);
         which = which < ncomp - 1 ? which : ncomp - 1;
-        const bool pick_t = !mat.has_refl || which == 1;
+        const bool pick_t = mat && (!mat->has_refl || which == 1);
         V3 wi_l;
         float bsdfPdf;
-        if (pick_t)
-            mt_sample_ool(mat.mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
+        if (!mat)
+            lambert_sample(wo_l, ub0, ub1, wi_l, bsdfPdf);
+        else if (pick_t)
+            mt_sample_ool(mat->mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
         else
-            beckmann_sample(mat.mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
+            beckmann_sample(mat->mf, wo_l, ub0, ub1, wi_l, bsdfPdf);
         if (bsdfPdf != 0.f) {
             const V3 wi = to_world(fr, wi_l);
             if (ncomp > 1) {
-                bsdfPdf += pick_t ? microfacet_pdf(mat.mf, wo_l, wi_l) : mt_pdf_ool(mat.mf, wo_l, wi_l);
+                bsdfPdf += pick_t ? microfacet_pdf(mat->mf, wo_l, wi_l) : mt_pdf_ool(mat->mf, wo_l, wi_l);
                 bsdfPdf /= (float)ncomp;
             }
             const Lobe f2 = bsdf_lobe(mat, dot(wi, fr.ng) * ng_wo > 0.f, wo_l, wi_l);
@@ -1040,7 +1062,7 @@ __global__ __launch_bounds__(256) void shade_tex_kernel(RenderScene sc, SampleRe
     const int nhits = *rec.hit_count;
     if (slot >= nhits || slot >= max_hits) return;
     const uint32_t hs = rec.hit_s[slot];
-    if (hs & 0x40000000u) return;
+    if (hs & HS_LIGHT) return;
     const RenderMaterial &mat = sc.materials[(hs >> REC_MAT_SHIFT) & 0xffu];
     const bool want_alb = (hs >> 31) && mat.has_alb_tex;
     if (!want_alb && !mat.has_bump) return;
@@ -1103,8 +1125,10 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
     const int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     const int nhits = *rec.hit_count;
     if (slot >= nhits || slot >= max_hits) return;
-    if (rec.hit_s[slot] & 0x40000000u) return;
-    const RenderMaterial &mat = sc.materials[(rec.hit_s[slot] >> REC_MAT_SHIFT) & 0xffu];
+    const uint32_t hs = rec.hit_s[slot];
+    if ((hs & HS_LIGHT) && !(hs & HS_LSURF)) return;
+    // a light sphere's surface: the matte lobe (kind 3) needs no material
+    const RenderMaterial *mat = (hs & HS_LIGHT) ? nullptr : &sc.materials[(hs >> REC_MAT_SHIFT) & 0xffu];
     const size_t base = (size_t)slot * sc.nlights * ns_max;
     float ld[NB];
 #pragma unroll
@@ -1221,9 +1245,10 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
     const RenderMaterial *mat = nullptr;
     float kss = 0.f, arg[3] = {0.f, 0.f, 0.f};
     bool alb = false;
-    if ((hs & 0x40000000u) && ((hs >> REC_MAT_SHIFT) & 0xffu) == 0xffu) return;  // escaped: sky_kernel
-    if (hs & 0x40000000u) {
-        le = sc.lights[(hs >> REC_MAT_SHIFT) & 0xffu].Lemit;
+    if ((hs & HS_LIGHT) && !(hs & HS_LSURF)) return;  // escaped: sky_kernel
+    if (hs & HS_LIGHT) {  // a light sphere: L = 0 + Le(wo) (if it faces the ray) + Ld of its matte surface
+        if (hs & HS_LE) le = sc.lights[(hs >> REC_MAT_SHIFT) & 0xffu].Lemit;
+        ld = rec.ld + (size_t)slot * ROW;
     } else {
         ld = rec.ld + (size_t)slot * ROW;
         if (hs >> 31) {
@@ -1276,7 +1301,7 @@ __global__ __launch_bounds__(256) void sky_kernel(RenderScene sc, SampleRecs rec
     const int nhits = *rec.hit_count;
     if (slot >= nhits || slot >= max_hits) return;
     const uint32_t hs = rec.hit_s[slot];
-    if (!((hs & 0x40000000u) && ((hs >> REC_MAT_SHIFT) & 0xffu) == 0xffu)) return;
+    if (!((hs & HS_LIGHT) && !(hs & HS_LSURF))) return;
     const float4 hb = rec.hit_b[slot];
     float Ls[NB];
 #pragma unroll

@@ -67,6 +67,7 @@ def lib():
     L.o_sample_profile.restype = C.c_float
     L.o_sample_profile.argtypes = [f32p, C.c_int, C.c_float, C.c_float]
     L.o_rho_table.argtypes = [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)]
+    L.o_rho_table_ex.argtypes = [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)]
     L.o_mt_first.restype = C.c_uint32
     L.o_mt_first.argtypes = [C.c_uint32, C.c_int, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")]
     L.o_octree_build.restype = C.c_void_p
@@ -153,10 +154,11 @@ def compute_profile(mua, musp, eta, thickness, desired_length=512, lerp=True):
     return table, rcp, spacing, total
 
 
-def rho_table(roughness, eta, n_entries=1025, sqrt_samples=256):
+def rho_table(roughness, eta, n_entries=1025, sqrt_samples=256, fixed=False):
+    """fixed: LayeredSkin's doublerefsslf (FixedFresnelDielectric, reflection.h:315-324)."""
     hd = np.zeros(n_entries, np.float32)
     hh = C.c_float()
-    lib().o_rho_table(roughness, eta, n_entries, sqrt_samples, nthreads(), hd, C.byref(hh))
+    lib().o_rho_table_ex(roughness, eta, int(fixed), n_entries, sqrt_samples, nthreads(), hd, C.byref(hh))
     return hd, hh.value
 
 

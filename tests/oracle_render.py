@@ -275,6 +275,29 @@ def sub_window(num, count, xs, xe, ys, ye):
     return tuple(int(v) for v in out)
 
 
+def host_cpus():
+    """CPUs this process may run on: its affinity mask, capped by the cgroup CPU quota. On the GPU
+    box nproc counts the whole host's CPUs, while a job gets a share of them (16 per GPU); threads
+    beyond the share only contend."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max"):
+                quota, period = parts[0], parts[1]
+            else:
+                quota = parts[0]
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    period = f.read().split()[0]
+            if quota not in ("max", "-1"):
+                n = min(n, max(1, int(quota) // int(period)))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return max(1, n)
+
+
 def time_cpu_baseline(sc, ctx, spp, seed, seconds, nthreads=None):
     """Time the oracle's pixel loop the way SamplerRenderer::Render runs (samplerrenderer.cpp:
     191-225): nTasks = RoundUpPow2(max(32 * cores, W * H / 256)) sub-windows of the frame, pulled
@@ -282,7 +305,7 @@ def time_cpu_baseline(sc, ctx, spp, seed, seconds, nthreads=None):
     `seconds` pass (a bounded sample of the same frame). The octree is built from the product's
     Preprocess outputs (surface points + irradiance); Preprocess is not timed."""
     import mpss
-    cores = os.cpu_count() or 1
+    cores = host_cpus()
     nthreads = nthreads or cores
     osc = OracleScene(sc, tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
     osc.set_octree(ctx.surface_points(), ctx.irradiance())
@@ -294,7 +317,7 @@ def time_cpu_baseline(sc, ctx, spp, seed, seconds, nthreads=None):
     osc.close()
     dt = el.value
     return {"value": round(px * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": nthreads, "kind": "port",
-            "nproc": cores,
+            "nproc": os.cpu_count(), "cpu_share": cores,
             "sample": "%d of %d render tasks (pbrt's split RoundUpPow2(max(32 x %d cores, W*H/256)), %d px x %d spp, "
                       "%.1f %% of the frame) in fixed random order, one pool of %d threads, %.1f s; oracle/render.c "
                       "(scalar C restatement, pthreads)" % (tasks.value, ntasks, cores, px, spp,

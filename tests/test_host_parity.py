@@ -33,11 +33,16 @@ def test_skin_layers_variants(oracle, mpss, params):
         assert np.array_equal(a, b)
 
 
-def test_rho_table_bit_exact(oracle, mpss):
-    hd_p, hh_p = mpss.host_rho_table(0.3, 1.4, n=33, sqrt_samples=32)
-    hd_o, hh_o = oracle.rho_table(0.3, 1.4, n_entries=33, sqrt_samples=32)
+@pytest.mark.parametrize("fixed", [False, True])
+def test_rho_table_bit_exact(oracle, mpss, fixed):
+    """fixed: LayeredSkin "doublerefsslf" -- FixedFresnelDielectric (reflection.h:315-324)."""
+    hd_p, hh_p = mpss.host_rho_table(0.3, 1.4, n=33, sqrt_samples=32, double_ref_sslf=fixed)
+    hd_o, hh_o = oracle.rho_table(0.3, 1.4, n_entries=33, sqrt_samples=32, fixed=fixed)
     assert np.array_equal(hd_p, hd_o)
     assert hh_p == hh_o
+    if fixed:  # the fixed variant reflects more than the plain one
+        hd_n, _ = oracle.rho_table(0.3, 1.4, n_entries=33, sqrt_samples=32)
+        assert np.all(hd_o >= hd_n) and np.any(hd_o > hd_n)
 
 
 @pytest.mark.parametrize("desired", [16, 64])

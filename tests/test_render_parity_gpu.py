@@ -18,7 +18,6 @@ import pytest
 import oracle_render as orr
 import parity
 
-pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOL = 1e-4
 
@@ -38,6 +37,7 @@ def pair(mpss, oracle):
     return torch, sc, ctx, o
 
 
+@pytest.mark.gpu
 def test_surface_points_bit_exact(pair):
     torch, sc, ctx, o = pair
     got = ctx.surface_points()
@@ -46,6 +46,7 @@ def test_surface_points_bit_exact(pair):
     assert got.tobytes() == ref.tobytes()
 
 
+@pytest.mark.gpu
 def test_irradiance_parity(pair):
     torch, sc, ctx, o = pair
     pts = ctx.surface_points()
@@ -68,6 +69,7 @@ def _check(got, ref):
     parity.check_image(got, ref)
 
 
+@pytest.mark.gpu
 def test_image_parity_full_frame(pair):
     torch, sc, ctx, o = pair
     pts = ctx.surface_points()
@@ -78,6 +80,7 @@ def test_image_parity_full_frame(pair):
     assert (ref[..., 1] > 0).mean() > 0.05  # the test actually covers shaded pixels
 
 
+@pytest.mark.gpu
 def test_image_parity_ragged_tile(pair):
     """An interior tile whose borders cut through the face (edge samples of neighbours)."""
     torch, sc, ctx, o = pair
@@ -89,6 +92,7 @@ def test_image_parity_ragged_tile(pair):
     _check(got, ref)
 
 
+@pytest.mark.gpu
 def test_c1_tissue_full_frame(mpss, oracle):
     """Config C1 (BASELINE.json configs[0]): scenes/tissue.pbrt at its full 256x256, 8 spp, the
     reference's CPU-runnable case -- the whole frame on the GPU against the CPU restatement."""
@@ -109,6 +113,7 @@ def test_c1_tissue_full_frame(mpss, oracle):
     _check(got, ref)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene,kt", [("skin.pbrt", None), ("tissue.pbrt", [0.6, 0.8, 1.0])])
 def test_image_parity_transmission_lobe(mpss, oracle, scene, kt):
     """LayeredSkin with a non-black Kt (CreateLayeredSkinMaterial's default Spectrum(1), or a
@@ -144,6 +149,7 @@ def _sky_light(deg, axis, L=(0.3, 0.35, 0.45), scale=(2, 2, 2), ns=4):
 @pytest.mark.parametrize("scene,lights", [("tissue_sky.pbrt", None), ("skin.pbrt", "sky+area"),
                                           ("skin.pbrt", "sky"), ("tissue.pbrt", "map+area"), ("skin.pbrt", "map"),
                                           ("skin.pbrt", "grace")])
+@pytest.mark.gpu
 def test_image_parity_infinite_light(mpss, oracle, scene, lights):
     """LightSource "infinite" (lights/infinite.cpp), constant or with a radiance map: Sample_L /
     Pdf (Distribution2D) for irradiance and both MIS halves of EstimateDirect, Le (MIPMap
@@ -186,3 +192,66 @@ def test_image_parity_infinite_light(mpss, oracle, scene, lights):
     got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 17)
     ref = o.render_tile(sc.spp, 17, 0, sc.xres, 0, sc.yres)
     _check(got, ref)
+
+
+def _visible_sphere_scene(pbrtscene):
+    """skin.pbrt with a second sphere light in front of the face, in frame: its surface carries pbrt's
+    default "matte" material (api.cpp:241,1085), so a camera ray that hits it returns Le(wo) plus the
+    direct light the matte surface receives from the scene's other lights (multipolesubsurface.cpp:
+    253-304); it also shadows and lights the face."""
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=48, yres=48, spp=4)
+    sc.integrator["minsampledistance"] = 0.008
+    for m in sc.materials:
+        m["desired_length"] = 128
+    front = dict(center=[0.53, -2.53, 0.51], radius=0.12, L=[6.0, 5.0, 4.0], nsamples=2)
+    sc.lights = [sc.lights[0], front, _sky_light(40, [1, 1, 0], ns=2)]
+    return sc
+
+
+@pytest.mark.gpu
+def test_image_parity_light_sphere_in_frame(mpss, oracle):
+    import torch
+    from mpss import pbrtscene
+    sc = _visible_sphere_scene(pbrtscene)
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=8)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    o.set_octree(pts, o.irradiance(pts, 8))
+    got = _render_gpu(torch, ctx, sc, 0, sc.xres, 0, sc.yres, 23)
+    ref = o.render_tile(sc.spp, 23, 0, sc.xres, 0, sc.yres)
+    _check(got, ref)
+    assert _sphere_pixels(sc, sc.lights[1]).sum() >= 20  # the case covers the sphere
+
+
+def _sphere_pixels(sc, li):
+    """Pixels whose centre ray meets the sphere (the camera's own matrices; test bookkeeping only)."""
+    r2c, c2w = (m.astype(np.float64) for m in sc.raster_to_camera())
+    ys, xs = np.mgrid[0:sc.yres, 0:sc.xres] + 0.5
+    pc = np.stack([xs, ys, np.zeros_like(xs), np.ones_like(xs)], -1) @ r2c.T
+    dc = pc[..., :3] / pc[..., 3:]
+    d = dc @ c2w[:3, :3].T
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    oc = c2w[:3, 3] - np.asarray(li["center"], np.float64)
+    b = d @ oc
+    return b * b - (oc @ oc - li["radius"] ** 2) > 0
+
+
+def test_light_sphere_matte_shading_oracle(oracle):
+    """The oracle's light-sphere shading (CPU only): with the scene's other lights on, the pixels
+    whose centre ray meets the front sphere gain its matte surface's direct light on top of Le."""
+    import mpss
+    from mpss import pbrtscene
+    ys = []
+    for others in (True, False):
+        sc = _visible_sphere_scene(pbrtscene)
+        sc.xres = sc.yres = 24
+        sc.materials[0]["desired_length"] = 64
+        if not others:
+            sc.lights = [sc.lights[1]]
+        o = orr.OracleScene(sc, orr.tables_from_host(sc, mpss), mpss.default_config(
+            **pbrtscene.integrator_config(sc)), mpss)
+        ys.append(o.render_tile(sc.spp, 3, 0, sc.xres, 0, sc.yres)[..., 1])
+    px = _sphere_pixels(sc, sc.lights[0])
+    assert px.sum() >= 5
+    assert np.all(ys[0][px] > ys[1][px])

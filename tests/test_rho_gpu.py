@@ -26,7 +26,6 @@ def test_gpu_rho_table_vs_host_and_oracle(mpss, oracle, rough, eta, fixed):
     host, _ = mpss.host_rho_table(rough, eta, double_ref_sslf=fixed)
     ulps = np.abs(rho.view(np.int32).astype(np.int64) - host.view(np.int32).astype(np.int64))
     assert ulps.max() <= 1 and (ulps == 0).mean() >= 0.999, (ulps.max(), (ulps != 0).sum())
-    if not fixed:  # the oracle restates the FresnelDielectric variant
-        ref, _ = oracle.rho_table(rough, eta)
-        assert np.array_equal(host, ref)
+    ref, _ = oracle.rho_table(rough, eta, fixed=fixed)  # FresnelDielectric, or FixedFresnelDielectric
+    assert np.array_equal(host, ref)
     print("material build (profile 16 + rho 1025 x 256^2 on the GPU): %.3f s" % dt)
