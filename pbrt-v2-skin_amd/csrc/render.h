@@ -49,6 +49,10 @@ struct RenderMaterial {
     float mix;
     TexView alb_tex, bump_tex;
     int band_pos[NB];     // band c's float offset in a hit's Mo() row (this profile's BandGroups::pos)
+    // R's range for direct_combine's per-term quotient guard: every R[c] >= 0 (r_nonneg), the least
+    // nonzero R[c] and the largest (0, 0 when R is black)
+    float r_lo, r_hi;
+    int r_nonneg;
 };
 
 struct RenderScene {

@@ -1113,6 +1113,19 @@ __global__ __launch_bounds__(256) void shade_nolight_kernel(RenderScene sc, Samp
     for (int k = 0; k < 8; ++k) row[k] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// One test per light sample for the Microfacet half: every band's dividend x = ((R[c] D) G) F and quotient
+// x / den lie in div_by's guarded range [2^-100, 2^100] (or x = +0), so the 30 quotients take div_by's fast
+// path (RN(x inv) and one Markstein correction) with no per-band range test: the same values. R, D, G, F
+// >= 0, so x >= +0. r_lo / r_hi bound R's nonzero values; the factor-2 margins absorb the roundings of
+// the bound's own products and of x's (a few ulps).
+__device__ __forceinline__ bool refl_quotients_safe(const RenderMaterial &m, const Lobe &L, const Den &den) {
+    if (!den.ok || !m.r_nonneg || !(L.a >= 0.f && L.b >= 0.f && L.c >= 0.f)) return false;
+    if (L.a == 0.f || L.b == 0.f || L.c == 0.f || m.r_hi == 0.f) return true;  // every x = +0: q = +-0 exactly
+    const float abc = (L.a * L.b) * L.c;
+    const float lo = m.r_lo * abc, hi = m.r_hi * abc, ai = fabsf(den.inv);
+    return lo >= 0x1p-99f && hi <= 0x1p99f && lo * ai >= 0x1p-99f && hi * ai <= 0x1p99f;
+}
+
 // ld[c] = sum over lights of (sum over j of (0 + light term + BSDF term)) / ns, band by band in
 // the order UniformSampleAllLights accumulates (Ld += EstimateDirect; L += Ld / nSamples). Each
 // light sample's record is read once and added to all 30 per-band accumulators (registers);
@@ -1150,6 +1163,18 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
                 inf_lookup(L, st.z, st.w, rgb2);
             }
             const Den d1 = make_den(e.l1.d), d2 = make_den(e.l2.d), dp = make_den(e.pdf2);
+            if (!e.l2.kind && e.l1.kind == 1u && refl_quotients_safe(*mat, e.l1, d1)) {
+                // the common term: a Microfacet light-sample half alone, its quotients on the fast path
+#pragma unroll
+                for (int c = 0; c < NB; ++c) {
+                    const float Li1 = inf ? illum_band(rgb1, c) : L.Lemit[c];
+                    const float x = mat->R[c] * e.l1.a * e.l1.b * e.l1.c;
+                    const float q = x * d1.inv;
+                    const float f1 = __builtin_fmaf(__builtin_fmaf(-d1.d, q, x), d1.inv, q);
+                    Ld[c] += 0.f + f1 * Li1 * e.k1;
+                }
+                continue;
+            }
 #pragma unroll
             for (int c = 0; c < NB; ++c) {
                 const float Li1 = inf ? illum_band(rgb1, c) : L.Lemit[c];

@@ -238,6 +238,15 @@ void Context::upload_scene() {
         bool black = true;
         for (int c = 0; c < NB; ++c) black = black && m.Kr[c] == 0.f;
         r.has_refl = !black;
+        r.r_lo = INFINITY;
+        r.r_hi = 0.f;
+        r.r_nonneg = 1;
+        for (int c = 0; c < NB; ++c) {
+            if (!(m.Kr[c] >= 0.f)) r.r_nonneg = 0;
+            if (m.Kr[c] > 0.f) r.r_lo = std::min(r.r_lo, m.Kr[c]);
+            r.r_hi = std::max(r.r_hi, m.Kr[c]);
+        }
+        if (black) r.r_lo = 0.f;
         memcpy(r.T, m.Kt, sizeof(r.T));
         bool tblack = true;
         for (int c = 0; c < NB; ++c) tblack = tblack && m.Kt[c] == 0.f;
