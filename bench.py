@@ -41,9 +41,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # query-record, as the reference reads them once). Re-reads the sharding adds are not counted.
 REC_HDR_BYTES = 16
 REF_RECORD_BYTES = 12 + 4 + 4 * 30  # position, area / sumArea, 30-band E / Et
-# The gather's real ceiling: L2 requests of per-lane 8-byte table gathers, measured by
-# tools/microbench/l2_gather.hip on MI355X (profiles/r02_l2_gather_ceiling.json).
-L2_GATHER_CEILING_REQ_S = 2.46e11
+# The gather's real ceiling: L2 requests of per-lane 8-byte table gathers (64 lanes on 64 distinct lines
+# per instruction), the best rate any load form sustains on MI355X: tools/microbench/l2_policy.hip,
+# profiles/r03_l2_policy.json (2.69e11 lane loads/s; round 2's l2_gather.hip, with hash arithmetic per
+# load, reached 2.46e11).
+L2_GATHER_CEILING_REQ_S = 2.69e11
 # sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
 KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
                   "pbrt-v2-skin_amd/csrc/octree.h")
@@ -286,8 +288,9 @@ def main(a):
     roofline = {"kernel": "mo_sort_kernel + mo_band_wave_kernel (Mo gather, spectrally sharded, wave queue)",
                 "bound": "l2_requests", "achieved": None, "peak": L2_GATHER_CEILING_REQ_S / 1e9, "unit": "Greq/s",
                 "frac": None, "traffic": None, "avg_launch_ms": round(shade_launch_ms, 4),
-                "peak_source": "tools/microbench/l2_gather.hip: per-lane 8-byte gathers from a per-XCD-resident "
-                               "table (profiles/r02_l2_gather_ceiling.json)",
+                "peak_source": "tools/microbench/l2_policy.hip: per-lane 8-byte gathers from a per-XCD-resident "
+                               "table, 64 distinct lines per instruction, best load form "
+                               "(profiles/r03_l2_policy.json)",
                 "algorithmic": {"achieved_gbs": round(mo_gbs, 1), "peak_gbs": HBM_PEAK_GBS,
                                 "frac": round(mo_gbs / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": mo_bytes_step / launches_per_step,

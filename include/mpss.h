@@ -26,7 +26,11 @@
  * mpss_mo_batch, mpss_render_tile(s) and the query functions may be called concurrently from
  * several host threads, each with its own stream; every call takes its own device workspace.
  * Calls that change the context (materials, meshes, lights, camera, points, preprocess) are
- * serialized against each other and must not race with renders that depend on what they change.
+ * serialized against each other. Those that replace device state a render reads (the octree via
+ * mpss_set_irradiance_points / mpss_preprocess, the scene buffers, the replay table) first wait
+ * until every render / mo_batch call in flight has queued its kernels, then for those kernels; a
+ * render started after such a call sees the new state. Which of two racing calls goes first is
+ * the caller's to order.
  * Pointers named *_dev are HIP device pointers (e.g. torch CUDA tensors' data_ptr());
  * all other arrays are caller-owned host memory that is copied in.
  * stream: a hipStream_t (NULL = legacy default stream).

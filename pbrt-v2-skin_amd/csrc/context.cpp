@@ -42,11 +42,18 @@ RenderWorkspace::~RenderWorkspace() {
     }
 }
 
-// A free workspace from the pool, or a new one (mu_ held).
+// A free workspace from the pool -- preferably one whose last user's kernels are done, so this call
+// need not queue behind another stream -- or a new one (mu_ held).
 RenderWorkspace *Context::acquire_ws() {
     if (!ws_free_.empty()) {
-        RenderWorkspace *w = ws_free_.back().release();
-        ws_free_.pop_back();
+        size_t pick = ws_free_.size() - 1;
+        for (size_t i = ws_free_.size(); i-- > 0;)
+            if (!ws_free_[i]->pending || hipEventQuery(ws_free_[i]->done) == hipSuccess) {
+                pick = i;
+                break;
+            }
+        RenderWorkspace *w = ws_free_[pick].release();
+        ws_free_.erase(ws_free_.begin() + (std::ptrdiff_t)pick);
         return w;
     }
     auto w = std::make_unique<RenderWorkspace>();
@@ -57,13 +64,37 @@ RenderWorkspace *Context::acquire_ws() {
     return w.release();
 }
 
-// Back to the pool after its last kernel on `stream` (the next user waits on `done`).
+// Back to the pool after its last kernel on `stream` (the next user waits on `done`). The pool keeps
+// at most kMaxIdleWorkspaces: a burst of concurrent callers does not pin its peak memory (a full C2
+// batch workspace is several GB) for the context's lifetime; the oldest idle one is freed first.
+constexpr size_t kMaxIdleWorkspaces = 4;
 void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) {
     const hipError_t e = hipEventRecord(ws->done, stream);
     ws->pending = e == hipSuccess;
-    std::lock_guard<std::mutex> g(mu_);
-    ws_free_.emplace_back(ws);
+    std::unique_ptr<RenderWorkspace> drop;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        ws_free_.emplace_back(ws);
+        if (ws_free_.size() > kMaxIdleWorkspaces) {
+            drop = std::move(ws_free_.front());
+            ws_free_.erase(ws_free_.begin());
+        }
+    }
+    drop.reset();  // waits for its last kernels, outside the lock
     MPSS_HIP(e);
+}
+
+// mu_ held (by the caller's lock on it): wait out every in-flight render_tiles / mo_batch, then
+// their kernels, before device state they read is replaced.
+void Context::quiesce_locked() {
+    idle_.wait(mu_, [&] { return inflight_ == 0; });
+    MPSS_HIP(hipDeviceSynchronize());
+}
+
+// An in-flight call has queued its kernels (mu_ not held).
+void Context::end_inflight() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (--inflight_ == 0) idle_.notify_all();
 }
 
 void Context::ensure_layouts() {
@@ -98,7 +129,12 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
             layout = &dev_octree_.ensure_layout(m->dev_profile.groups);
             ws = acquire_ws();
         }
+        ++inflight_;  // until the kernels are queued (an octree rebuild waits for it)
     }
+    struct Done {
+        Context *c;
+        ~Done() { c->end_inflight(); }
+    } done{this};
     if (mode == -1) {
         launch_mo_dipole(dev_octree_, m->dev_dipole.ptr, max_error_, q, p_dev, out_dev, NB, counters_dev, stream);
         return;
@@ -337,7 +373,7 @@ const Material &Context::material(uint32_t id) const {
 void Context::set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area) {
     activate();
     std::lock_guard<std::mutex> g(mu_);
-    MPSS_HIP(hipDeviceSynchronize());  // no gather of the old octree may still be running
+    quiesce_locked();  // no gather of the old octree may still be in flight or running
     build_octree_locked(n, p, nrm, E, area);
 }
 

@@ -1,6 +1,7 @@
 // context.h -- per-integrator state behind the C ABI (one mpss_ctx per
 // MultipoleSubsurfaceIntegrator instance; reference integrators/multipolesubsurface.h:36-80).
 #pragma once
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -180,6 +181,14 @@ private:
     // serializes everything that changes the context (scene, materials, octree, stats) and the
     // workspace pool; launches happen outside it
     mutable std::mutex mu_;
+    // render_tiles / mo_batch calls between taking their device pointers (under mu_) and queueing
+    // their last kernel; a call that replaces what they read (octree and band layouts, scene
+    // buffers, replay table) first waits for none to be in flight, then for the queued kernels
+    // (quiesce_locked). Guarded by mu_.
+    int inflight_ = 0;
+    std::condition_variable_any idle_;
+    void quiesce_locked();
+    void end_inflight();
     // kernel timing (cfg_.kernel_timing) and traversal counting (cfg_.count_traversal)
     struct Timed {
         hipEvent_t a, b;

@@ -115,6 +115,7 @@ void Context::set_camera(const float *r2c, const float *c2w, int xres, int yres)
 
 void Context::upload_scene() {
     activate();
+    quiesce_locked();  // the scene buffers in-flight renders read are about to be replaced
     if (scene_.meshes.empty()) throw Error(MPSS_ERR_INVALID, "scene has no meshes");
     build_bvh(scene_);
     const int depth = bvh_depth(scene_.bvh, 0);
@@ -322,7 +323,7 @@ void Context::set_surface_points(uint32_t n, const SurfacePoint *pts) {
 void Context::preprocess(uint32_t seed) {
     activate();
     std::lock_guard<std::mutex> g(mu_);
-    MPSS_HIP(hipDeviceSynchronize());  // no render of the previous octree may still be running
+    quiesce_locked();  // no render of the previous octree may still be in flight or running
     if (scene_dirty_) upload_scene();
     if (scene_.lights.empty()) {  // "if (scene->lights.size() == 0) return;" -> no octree, no SSS
         have_octree_ = false;
@@ -517,7 +518,7 @@ void Context::ensure_replay_table(int spp) {
     if (replay_spp_ == spp && replay_vals_.ptr) return;
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     const int T = replay_render_tasks(W, H, std::max(1, cfg_.replay_cores));
-    MPSS_HIP(hipDeviceSynchronize());  // no render may still read the old table
+    quiesce_locked();  // no render may still read the old table
     replay_vals_.alloc((size_t)(W + 1) * (H + 1) * spp * replay_k_);
     DevBuf<uint32_t> mt;
     mt.alloc((size_t)624 * T);
@@ -600,6 +601,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     const float max_error = max_error_;
     const GatherOpts gopts = gather_opts();
     RenderWorkspace *ws = acquire_ws();
+    ++inflight_;  // until this call's kernels are queued (see quiesce_locked)
     lk.unlock();
 
     std::vector<Timed> timed;
@@ -803,6 +805,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         }
     } catch (...) {
         release_ws(ws, stream);
+        end_inflight();
         throw;
     }
     release_ws(ws, stream);
@@ -810,6 +813,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     timed_.insert(timed_.end(), timed.begin(), timed.end());
     stats_.samples += n_samples;
     stats_.sss_samples += n_sss;
+    if (--inflight_ == 0) idle_.notify_all();
 }
 
 // Tile-cost probe (mpss_tile_costs): classes per pixel centre, summed per rectangle on the host.
