@@ -5,15 +5,15 @@ samplerrenderer.cpp:191-217): every camera sample is traced, shaded (direct ligh
 Mo() octree gather) and splatted into the film; the film tiles of every rank reach rank 0
 through one RCCL gather per step.
 
-* N = 1 (default): config C2, skin.pbrt 1024x1024 at 64 spp on one MI355X -- BASELINE.json's
-  metric configuration.
-* N > 1 (default): config C3, ONE skin.pbrt 2048x2048 frame at 256 spp per step split over the
-  N GPUs (strong scaling: north_star's tile scaling of one frame). Tiles (64x64) are dealt by
-  estimated cost (mpss_tile_costs: camera rays through the pixel centres that hit skin; the
-  deal is computed identically on every rank, mpss/tiles.py deal_balanced), so the face is spread
-  evenly. A secondary C2 weak-scaling figure (one C2 frame per GPU per step) rides along in
-  the same JSON line.
-* --config c3 / c5 select BASELINE.json's other configurations explicitly.
+* Every N (default): config C2, skin.pbrt 1024x1024 at 64 spp -- BASELINE.json's metric is quoted on
+  it "@ 1/2/4/8 MI355X", so `value` at every N is the same workload and the driver's per-N
+  efficiency compares like with like. At N > 1 a step renders N C2 frames (one frame's work per GPU:
+  weak scaling) whose 128x128 tiles are dealt over the ranks by estimated cost (mpss_tile_costs:
+  camera rays through the pixel centres that hit skin; the deal is computed identically on every
+  rank, mpss/tiles.py deal_balanced), then gathered on rank 0 by one RCCL gather per step.
+* N > 1 also reports, as `secondary.c3_strong`, north_star's tile scaling of ONE frame: config C3
+  (2048x2048, 256 spp) split over the N GPUs as cost-dealt 64x64 tiles (strong scaling).
+* --config c3 / c5 select BASELINE.json's other configurations explicitly (their own scaling).
 
 Preprocess (tessellation, irradiance kernel, octree build) runs once before timing and is
 reported separately, as SURVEY.md §8d prescribes.
@@ -89,16 +89,16 @@ def parse(argv=None):
                     help="camera samples per render batch, log2 (mpss_config.max_batch_samples; default 2^24)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 weak-scaling figure at N > 1")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C3 strong-scaling figure at N > 1")
     ap.add_argument("--out", default=None, help="write rank 0's first frame as .pfm/.exr")
     ap.add_argument("--pmc-json", default=None,
                     help="rocprofv3 PMC summary (tools/summarize_prof.py) of this bench command; default: the "
                          "newest profiles/*_pmc.json of this config whose source_hash matches the kernel sources")
     a = ap.parse_args(argv)
     if a.config is None:
-        a.config = "c2" if a.gpus == 1 else "c3"
+        a.config = "c2"
     if a.tile is None:
-        a.tile = 128 if a.gpus == 1 else 64
+        a.tile = 64 if a.config == "c3" and a.gpus > 1 else 128
     return a
 
 
@@ -318,8 +318,8 @@ def main(a):
                 roofline["hbm_frac"] = round(roofline["hbm_gbs"] / HBM_PEAK_GBS, 4)
 
     secondary = None
-    if world > 1 and a.config != "c2" and not a.no_secondary:
-        secondary = c2_weak_secondary(a, rank, world, local)
+    if world > 1 and a.config == "c2" and not a.no_secondary:
+        secondary = c3_strong_secondary(a, rank, world, local)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -369,20 +369,20 @@ def main(a):
         dist.destroy_process_group()
 
 
-def c2_weak_secondary(a, rank, world, local):
-    """C2 weak scaling beside a strong-scaling line: one skin.pbrt 1024x1024 64-spp frame per GPU
-    per step, tiles of all N frames dealt by cost over the N ranks."""
+def c3_strong_secondary(a, rank, world, local):
+    """C3 strong scaling beside the C2 line: ONE skin.pbrt 2048x2048 256-spp frame per step split
+    over the N ranks as cost-dealt 64x64 tiles, gathered on rank 0 (north_star's tile scaling)."""
     import torch
-    sc, ctx, _, _, _, _, _ = build_scene(a, "c2", local)
-    T = 128
-    tiles, items_by_rank, _, _ = deal(ctx, sc, T, world, world)
+    sc, ctx, _, _, _, _, _ = build_scene(a, "c3", local)
+    T = 64
+    tiles, items_by_rank, balance, _ = deal(ctx, sc, T, 1, world)
     torch.cuda.synchronize()
-    dt, _, _ = timed_steps(a, ctx, sc, tiles, items_by_rank, world, T, rank, world, max(1, min(a.steps, 3)), 1)
     steps = max(1, min(a.steps, 3))
+    dt, _, _ = timed_steps(a, ctx, sc, tiles, items_by_rank, 1, T, rank, world, steps, 1)
     ctx.close()
-    return {"c2_weak": {"value": round(world * sc.xres * sc.yres * sc.spp * steps / dt / 1e6, 3),
-                        "unit": "Msamples/s", "ms_per_step": round(dt / steps * 1e3, 3), "frames_per_step": world,
-                        "scaling": "weak"}}
+    return {"c3_strong": {"value": round(sc.xres * sc.yres * sc.spp * steps / dt / 1e6, 3),
+                          "unit": "Msamples/s", "ms_per_step": round(dt / steps * 1e3, 3), "frames_per_step": 1,
+                          "tiles": len(tiles), "deal_balance": round(balance, 4), "scaling": "strong"}}
 
 
 def pmc_traffic(path, launch_ms, config):

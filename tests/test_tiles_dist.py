@@ -213,3 +213,17 @@ def test_deal_diagonal_partition():
         blk = [ty * nx + tx for ty in range(min(4, ny)) for tx in range(min(4, nx))]
         owners = {r for r, x in enumerate(d) for i in x if i in blk}
         assert len(owners) == min(world, len(blk))
+
+
+def test_bench_defaults_keep_the_metric_config():
+    """BASELINE.json's metric is quoted on skin.pbrt 1024^2 at 1/2/4/8 GPUs: every N defaults to C2
+    (weak scaling at N > 1, 128^2 tiles), so the driver's per-N values compare the same workload;
+    C3's one-frame strong scaling runs as the secondary figure or with --config c3 (64^2 tiles)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for n in (1, 2, 8):
+        a = bench.parse(["--gpus", str(n)])
+        assert (a.config, a.tile) == ("c2", 128)
+        assert bench.CONFIGS[a.config][3] == "weak"
+    a = bench.parse(["--gpus", "8", "--config", "c3"])
+    assert (a.config, a.tile) == ("c3", 64)
