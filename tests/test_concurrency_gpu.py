@@ -141,3 +141,63 @@ def test_concurrent_callers_bit_identical_to_serial(two):
             assert np.array_equal(mo, serial[k][1]), k
     # the two materials' gathers differ (so the test exercises both profiles)
     assert not np.array_equal(serial[0][1], serial[1][1])
+
+
+def test_octree_rebuild_while_rendering(mpss, oracle):
+    """mpss.h: a call that replaces the octree (mpss_set_irradiance_points) waits until the renders
+    in flight have queued their kernels, then for those kernels. 4 threads render strips on their own
+    streams while the main thread swaps the octree between two irradiance sets: no fault, and every
+    strip equals that strip rendered serially on one of the two octrees, bit for bit."""
+    import torch
+    from mpss import pbrtscene
+    sc = _two_material_scene(res=48, spp=4)
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=3)
+    pts = ctx.surface_points()
+    E1 = np.ascontiguousarray(ctx.irradiance())
+    E2 = np.ascontiguousarray(E1 * np.float32(0.5))
+    cloud = [np.ascontiguousarray(pts[k], np.float32) for k in ("p", "n")]
+    area = np.ascontiguousarray(pts["area"], np.float32)
+
+    def use(E):
+        ctx.set_irradiance_points(cloud[0], cloud[1], E, area)
+
+    strips = [(0, sc.xres, 12 * k, 12 * k + 12) for k in range(4)]
+    refs = []
+    for E in (E1, E2):
+        use(E)
+        refs.append([_render(torch, ctx, sc.spp, 7, *r).cpu().numpy() for r in strips])
+        torch.cuda.synchronize()
+    assert not np.array_equal(refs[0][1], refs[1][1])  # the two octrees render differently
+    results = [[] for _ in strips]
+    errors = []
+    start = threading.Barrier(len(strips) + 1)
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            start.wait()
+            with torch.cuda.stream(s):
+                for _ in range(6):
+                    out = _render(torch, ctx, sc.spp, 7, *strips[k], s)
+                    s.synchronize()
+                    results[k].append(out.cpu().numpy())
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(len(strips))]
+    for t in th:
+        t.start()
+    start.wait()
+    for i in range(4):
+        use(E1 if i % 2 else E2)
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    for k in range(len(strips)):
+        assert len(results[k]) == 6
+        for img in results[k]:
+            assert np.array_equal(img, refs[0][k]) or np.array_equal(img, refs[1][k]), k
+    use(E1)  # last: every render from now on sees E1
+    assert np.array_equal(_render(torch, ctx, sc.spp, 7, *strips[0]).cpu().numpy(), refs[0][0])
+    ctx.close()
