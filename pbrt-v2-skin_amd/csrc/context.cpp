@@ -206,12 +206,13 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
         }
         mat->rgb = true;
     }
+    const int distinct = m.rgb_profile ? 3 : NB;  // rgbprofile: 3 distinct channels (R, G, B)
     if (m.use_monte_carlo && !m.rgb_profile)
         build_profile_mc(lp, m.photons, 89, mat->profile);
     else if (cfg_.profile_on_host || sp.desired_length > 1024)
-        build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
+        build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile, 0, distinct);
     else
-        build_profile_gpu(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile);
+        build_profile_gpu(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile, 0, distinct);
     if (cfg_.profile_on_host)
         build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
     else

@@ -530,12 +530,20 @@ void profile_from_rings(const double *refl, int nseg, double extent, int target,
     rcp = (float)(target - 1) / last;
 }
 
-void build_profile(const LayerParams &lp, int desired_length, bool lerp_thin, ProfileTables &out, int nthreads) {
+void build_profile(const LayerParams &lp, int desired_length, bool lerp_thin, ProfileTables &out, int nthreads,
+                   int distinct) {
+    if (distinct < 1 || distinct > NB) throw Error(-1, "build_profile: distinct channels out of range");
     std::vector<std::vector<float>> tabs(NB);
-    parallel_for(NB, nthreads, [&](int sc) {
+    parallel_for(distinct, nthreads, [&](int sc) {
         channel_profile(lp, sc, desired_length, lerp_thin, tabs[sc], out.rcp[sc], out.spacing[sc],
                         out.total_reflectance[sc]);
     });
+    for (int c = distinct; c < NB; ++c) {
+        tabs[c] = tabs[c % distinct];
+        out.rcp[c] = out.rcp[c % distinct];
+        out.spacing[c] = out.spacing[c % distinct];
+        out.total_reflectance[c] = out.total_reflectance[c % distinct];
+    }
     out.length = (int)tabs[0].size();
     for (int c = 1; c < NB; ++c)
         if ((int)tabs[c].size() != out.length) throw Error(-2, "profile channel lengths differ");

@@ -39,11 +39,13 @@ struct RhoTable {
 };
 
 void skin_layer_params(const SkinParams &p, LayerParams &out);
+// distinct: channels 0..distinct-1 are built and channel c >= distinct copies channel c % distinct
+// (rgbprofile: lp's band c already holds component c % 3, so 3 builds give all 30 rows)
 void build_profile(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
-                   int nthreads = 0);
+                   int nthreads = 0, int distinct = NB);
 // The same profile built on the current HIP device (profile_gpu.hip); out is filled on the host.
 void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_on_thin_slab, ProfileTables &out,
-                       hipStream_t stream = 0);
+                       hipStream_t stream = 0, int distinct = NB);
 // The same rho_hd table on the current HIP device (rho_gpu.hip): bit-identical to build_rho_table
 // (one MT19937 stream per entry, terms Kahan-summed in sample order); rho_hh on the host.
 void build_rho_table_gpu(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,

@@ -295,7 +295,9 @@ unsigned round_up_pow2_u(unsigned v) {
 }  // namespace
 
 void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_thin, ProfileTables &out,
-                       hipStream_t stream) {
+                       hipStream_t stream, int distinct) {
+    if (distinct < 1 || distinct > NB) throw Error(-1, "build_profile_gpu: distinct channels out of range");
+    const int NC = distinct;  // channels built; channel c >= NC copies channel c % NC
     const int length = (int)round_up_pow2_u((unsigned)desired_length);
     const int N = 2 * length, M = 2 * N;
     int logM = 0;
@@ -303,9 +305,9 @@ void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_thin
     if (M > 4096) throw Error(-1, "build_profile_gpu: desiredlength above 1024 not supported on the GPU path");
     const int ext = length - 1;
     // per-channel setup (channel_profile / layer_grid, material.cpp)
-    std::vector<ChanSetup> cs(NB);
-    std::vector<float> steps(NB);
-    for (int sc = 0; sc < NB; ++sc) {
+    std::vector<ChanSetup> cs(NC);
+    std::vector<float> steps(NC);
+    for (int sc = 0; sc < NC; ++sc) {
         float mfp_total = 0.f;
         for (int l = 0; l < 2; ++l) mfp_total += 1.f / (lp.mua[l][sc] + lp.musp[l][sc]);
         const float mfp = mfp_total / (float)2;
@@ -347,14 +349,14 @@ void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_thin
     d_nsq.upload(ul.nsq.data(), ul.nsq.size());
     DevBuf<float> d_step, d_d, d_r, d_table;
     d_step.upload(steps.data(), steps.size());
-    d_d.alloc((size_t)NB * nent);
-    d_r.alloc((size_t)NB * nent);
-    d_table.alloc((size_t)NB * tl);
+    d_d.alloc((size_t)NC * nent);
+    d_r.alloc((size_t)NC * nent);
+    d_table.alloc((size_t)NC * tl);
     DevBuf<double> d_tot;
-    d_tot.alloc(NB);
+    d_tot.alloc(NC);
     // channels in batches that keep the 4 complex grids per channel within ~3 GB
     const size_t grid_bytes = (size_t)M * M * sizeof(double2);
-    const int batch = (int)std::max<size_t>(1, std::min<size_t>(NB, ((size_t)3 << 30) / (4 * grid_bytes)));
+    const int batch = (int)std::max<size_t>(1, std::min<size_t>(NC, ((size_t)3 << 30) / (4 * grid_bytes)));
     DevBuf<double2> grids;
     grids.alloc((size_t)batch * 4 * M * M);
     const int cols = std::max(1, std::min(4, 131072 / (M * (int)sizeof(double2))));
@@ -362,8 +364,8 @@ void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_thin
                                  cols * M * (int)sizeof(double2)));
     MPSS_HIP(hipFuncSetAttribute((const void *)fft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  M * (int)sizeof(double2)));
-    for (int c0 = 0; c0 < NB; c0 += batch) {
-        const int nch = std::min(batch, NB - c0);
+    for (int c0 = 0; c0 < NC; c0 += batch) {
+        const int nch = std::min(batch, NC - c0);
         MPSS_HIP(hipMemsetAsync(grids.ptr, 0, (size_t)nch * 4 * grid_bytes, stream));
         const int64_t cells = (int64_t)(ext + 1) * (ext + 1) * 2 * nch;
         hipLaunchKernelGGL(grid_fill_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, stream,
@@ -390,26 +392,28 @@ void build_profile_gpu(const LayerParams &lp, int desired_length, bool lerp_thin
         hipLaunchKernelGGL(total_kernel, dim3((unsigned)nch), dim3(256), 0, stream, grids.ptr, M, N, d_tot.ptr + c0);
         MPSS_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((tl * NB + 255) / 256)), dim3(256), 0, stream, d_d.ptr,
-                       d_r.ptr, nent, NB, tl, d_table.ptr);
+    hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((tl * NC + 255) / 256)), dim3(256), 0, stream, d_d.ptr,
+                       d_r.ptr, nent, NC, tl, d_table.ptr);
     MPSS_HIP(hipGetLastError());
     out.length = tl;
     out.table.resize((size_t)NB * tl);
-    std::vector<float> dlast(NB);
-    std::vector<double> tot(NB);
-    MPSS_HIP(hipMemcpyAsync(out.table.data(), d_table.ptr, sizeof(float) * out.table.size(), hipMemcpyDeviceToHost,
+    std::vector<float> dlast(NC);
+    std::vector<double> tot(NC);
+    MPSS_HIP(hipMemcpyAsync(out.table.data(), d_table.ptr, sizeof(float) * (size_t)NC * tl, hipMemcpyDeviceToHost,
                             stream));
-    MPSS_HIP(hipMemcpyAsync(tot.data(), d_tot.ptr, sizeof(double) * NB, hipMemcpyDeviceToHost, stream));
-    for (int c = 0; c < NB; ++c)
+    MPSS_HIP(hipMemcpyAsync(tot.data(), d_tot.ptr, sizeof(double) * NC, hipMemcpyDeviceToHost, stream));
+    for (int c = 0; c < NC; ++c)
         MPSS_HIP(hipMemcpyAsync(&dlast[c], d_d.ptr + (size_t)c * nent + nent - 1, sizeof(float), hipMemcpyDeviceToHost,
                                 stream));
     MPSS_HIP(hipStreamSynchronize(stream));
+    for (int c = NC; c < NB; ++c)
+        memcpy(&out.table[(size_t)c * tl], &out.table[(size_t)(c % NC) * tl], sizeof(float) * tl);
     for (int c = 0; c < NB; ++c) {
-        const float extent = dlast[c];
+        const float extent = dlast[c % NC];
         const float last = (float)(tl - 1) * extent / (float)(tl - 1);
         out.spacing[c] = last / (float)(tl - 1);  // multipole.cpp:274-275
         out.rcp[c] = (float)(tl - 1) / last;
-        out.total_reflectance[c] = (float)tot[c];
+        out.total_reflectance[c] = (float)tot[c % NC];
     }
 }
 
