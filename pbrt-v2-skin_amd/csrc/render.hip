@@ -1185,9 +1185,17 @@ __global__ __launch_bounds__(256) void direct_combine_kernel(RenderScene sc, Sam
                 Ld[c] += ed;
             }
         }
-        const Den dn = make_den((float)ns);
+        // L += Ld / nSamples. nsamples_round is a power of two (LDSampler::RoundSize), and x / 2^k and
+        // x * 2^-k are the same exact real rounded once, for every x (subnormal results included)
+        if ((ns & (ns - 1)) == 0) {
+            const float inv_ns = 1.f / (float)ns;
 #pragma unroll
-        for (int c = 0; c < NB; ++c) ld[c] += div_by(Ld[c], dn.d, dn.inv, dn.ok);
+            for (int c = 0; c < NB; ++c) ld[c] += Ld[c] * inv_ns;
+        } else {
+            const Den dn = make_den((float)ns);
+#pragma unroll
+            for (int c = 0; c < NB; ++c) ld[c] += div_by(Ld[c], dn.d, dn.inv, dn.ok);
+        }
     }
     float4 *row = reinterpret_cast<float4 *>(rec.ld + (size_t)slot * ROW);
 #pragma unroll

@@ -42,6 +42,7 @@ def main():
             "unit": "photons/s", "photons": n, "seconds": round(dt, 3), "events_per_s": round(g["events"] / dt, 1),
             "total_r": g["total_r"], "total_t": g["total_t"], "layers": layers, "mfp_range": mfpr,
             "segments": nseg}
+    line["roofline"] = mc_roofline(dt)
     if a.cpu_seconds > 0:
         import oracle_mc
         m = 20000
@@ -66,6 +67,45 @@ def main():
             f.write("Name\tTotal" + "".join("\t%g" % d for d in dist) + "\n")
             f.write("Monte-Carlo Reflectance\t%g\t" % g["total_r"] + "\t".join("%g" % v for v in g["reflectance"]) + "\n")
             f.write("Monte-Carlo Transmittance\t%g\t" % g["total_t"] + "\t".join("%g" % v for v in g["transmittance"]) + "\n")
+
+
+# VALU issue peak of MI355X: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 instruction (FP64
+# FMA runs at the FP32 rate: 78.6 TFLOP/s FP64 vector = 256 x 4 x 16 lanes x 2 x 2.4 GHz)
+VALU_PEAK_INST_S = 256 * 4 * 2.4e9 / 4
+
+
+def mc_roofline(seconds):
+    """The walk is FP64 arithmetic with LDS tallies: its bound is VALU issue. Instructions come from
+    the committed PMC summary of this command (profiles/*_c4_pmc.json, tools/gpu.sh pmc_mc), the time
+    from this run; none current -> achieved null."""
+    import glob
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_c4_pmc.json")):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        e = next((v for k, v in d.items() if "mc_profile_kernel" in k), None)
+        if not e or "SQ_INSTS_VALU" not in e:
+            continue
+        w = d.get("__meta__", {}).get("written", "")
+        if best is None or w > best[0]:
+            best = (w, f, e)
+    r = {"kernel": "mc_profile_kernel (FP64 layered random walk)", "bound": "valu", "achieved": None,
+         "peak": VALU_PEAK_INST_S / 1e9, "unit": "G wave64 VALU instructions/s", "frac": None, "traffic": None,
+         "peak_source": "256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles (MI355X_MICROARCH.md clocks and widths)",
+         "note": "issue-slot fraction: an FP64 transcendental (log / sqrt / sin / cos of the walk) counts once "
+                 "but holds its SIMD for several cycles"}
+    if best:
+        _, f, e = best
+        inst = e["SQ_INSTS_VALU"]["mean"] * e["SQ_INSTS_VALU"]["dispatches"]
+        # the PMC run times the warm-up walk too: scale its instruction count to the measured walk's
+        r["achieved"] = round(inst / seconds / 1e9, 2) if inst else None
+        r["frac"] = round(inst / seconds / VALU_PEAK_INST_S, 4) if inst else None
+        r["source"] = os.path.relpath(f, ROOT) + " (SQ_INSTS_VALU summed over the command's dispatches)"
+        if "fetch_bytes_corrected_mean" in e:
+            r["traffic"] = e["fetch_bytes_corrected_mean"] * e["FETCH_SIZE"]["dispatches"]
+    return r
 
 
 if __name__ == "__main__":

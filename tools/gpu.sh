@@ -11,6 +11,7 @@
 #   bench[=CFG]       bench.py --config CFG (c2 default), 5 steps  -> gpurun_out/TAG_bench_CFG.jsonl
 #   quick[=CFG]       bench.py, 3 steps, no CPU baseline           -> gpurun_out/TAG_bench_CFG.jsonl
 #   mc                tools/bench_mc.py (C4)                       -> gpurun_out/TAG_bench_c4_mc.jsonl
+#   pmc_mc            rocprofv3 --pmc SQ_INSTS_VALU of tools/bench_mc.py -> gpurun_out/prof_TAG_c4/pmc_1
 #   kt[=CFG]          rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG[_CFG]/kt
 #   pmc[=CFG]         rocprofv3 --pmc passes of the bench (one counter set per run, $PMC_SETS
 #                     overrides the default sets, one per line)   -> gpurun_out/prof_TAG[_CFG]/pmc_i
@@ -60,6 +61,11 @@ for step in "$@"; do
       echo "== mc"
       timeout -k 10 300 python tools/bench_mc.py > $log 2>&1 || fail mc $log
       grep '"metric"' $log > gpurun_out/${TAG}_bench_c4_mc.jsonl; cat gpurun_out/${TAG}_bench_c4_mc.jsonl ;;
+    pmc_mc)
+      d=gpurun_out/prof_${TAG}_c4
+      mkdir -p $d
+      echo "== pmc mc"
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES -d $d/pmc_1 -o run --output-format csv -- python3 tools/bench_mc.py --cpu-seconds 0 > $d/pmc_1.log 2>&1 || fail "pmc mc" $d/pmc_1.log 20 ;;
     kt)
       cfg=${arg:-c2}
       d=gpurun_out/prof_${TAG}$(sfx $cfg)
