@@ -404,6 +404,7 @@ void Context::build_octree_locked(int n, const float *p, const float *nrm, const
         build_octree_device(n, dp ? dp : up.ptr, dn ? dn : un.ptr, dE ? dE : uE.ptr, uA.ptr, bmin, bmax, dev_octree_);
     }
     have_octree_ = true;
+    dev_octree_.ensure_leaf_r2(max_error_);
     ensure_layouts();
 }
 

@@ -93,6 +93,8 @@ struct BandTree {
     const float *__restrict__ table;     // [NB][L] + 2 trailing zeros (DeviceProfile::upload)
     BandGroups groups;
     float grcp[kGroups][4];              // rcpDsqSpacing of each group slot (0 for an empty slot)
+    float grcp_max[kGroups];             // the largest of a group's rcp (its shortest reach)
+    const float *leaf_r2;                // DeviceOctree::leaf_r2 (nullable: no LDS-only point loops)
     int L, n_nodes, n_points;
     float max_error, prune_f;
 };
@@ -135,6 +137,7 @@ struct BandLane {
     uint32_t klim;    // min(KLDS, L - 2): s < klim <=> the pair (s, s + 1) is in the LDS copy
     uint32_t gspan;   // L - 1 - klim: s - klim < gspan (unsigned) <=> the pair is read from L2
     const float *lt;  // LDS rows (generic pointer)
+    lds_float *ltl;   // the same rows through the LDS address space (ds_read only)
     const float *tb[4];  // the bands' table rows
 };
 // Row length (floats) of a band's LDS near field.
@@ -177,6 +180,26 @@ __device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float
             hist[2] += s < 8192u;
             hist[3] += s < 16384u;
         }
+    }
+}
+
+// band_rd_fetch for a point the caller has proven inside the near field of all four bands (s <
+// klim: DeviceOctree::leaf_r2): the pairs come straight from LDS (ds_read), the vector-memory path
+// -- the gather's binding resource -- never sees them. Same f, same pairs, so the same terms.
+template <int KLDS>
+__device__ __forceinline__ void band_rd_fetch_lds(const BandLane &b, float d2, float f[4], RdPair v[4]) {
+    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
+    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
+    f[0] = f01.x;
+    f[1] = f01.y;
+    f[2] = f23.x;
+    f[3] = f23.y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t s = (uint32_t)f[j];
+        lds_float *q = b.ltl + j * near_row<KLDS>() + s;  // one ds_read2_b32 per band
+        v[j].a = q[0];
+        v[j].b = q[1];
     }
 }
 
@@ -258,7 +281,12 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
 #pragma unroll
     for (int j = 0; j < 4; ++j) b.tb[j] = VROWS ? in_vgprs(a.table + b.off[j]) : a.table + b.off[j];
     b.lt = lt;
+    b.ltl = (lds_float *)lt;
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
+    // a leaf whose points all lie within the near field of every band of the group, for any query that
+    // opens it: leaf_r2 * rcp_max < klim (with a 1e-5 margin for the roundings of d2 and f)
+    const float lds_r2_lim = (float)b.klim / (a.grcp_max[grp] * 1.00001f);
+    const cptr<float> leaf_r2 = as_const(a.leaf_r2);
     const float rcp_min = a.groups.rcp_min[grp];
     const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
     const cptr<float4> e_g = as_const(a.band_e + (size_t)grp * a.n_points);
@@ -305,6 +333,25 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 const int live = (int)h.pad;
                 if (COUNT) w_pts += live;
                 int i0 = 0;
+                if (!COUNT && KLDS > 0 && a.leaf_r2 && leaf_r2[node] < lds_r2_lim) {
+                    for (; i0 + 1 < live; i0 += 2) {
+                        const int ka = h.leaf_first + i0, kb = ka + 1;
+                        const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];
+                        const float4 ea = e_g[ka], eb = e_g[kb];
+                        if (!open) continue;
+                        const float ax = px - pa.x, ay = py - pa.y, az = pz - pa.z;
+                        const float bx2 = px - pb.x, by2 = py - pb.y, bz2 = pz - pb.z;
+                        const float d2a = ax * ax + ay * ay + az * az;
+                        const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
+                        float fa[4], fb[4];
+                        RdPair va[4], vb[4];
+                        band_rd_fetch_lds<KLDS>(b, d2a, fa, va);
+                        band_rd_fetch_lds<KLDS>(b, d2b, fb, vb);
+                        const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
+                        band_rd_combine<true>(fa, va, e0, pa.w, lacc);
+                        band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
+                    }
+                }
                 for (; i0 + 1 < live; i0 += 2) {
                         const int ka = h.leaf_first + i0, kb = ka + 1;
                         const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];

@@ -27,6 +27,15 @@ struct DeviceOctree {
     // one group-major layout per distinct band grouping in use; built eagerly and synchronously
     // (Context::set_irradiance_points / add material) so launches only read them
     std::vector<std::unique_ptr<BandLayout>> layouts;
+    // per node: for a leaf, the square of a radius around its centroid that holds every point of the
+    // leaf as seen from any query that opens it under max_error (DiffusionOctree Mo(): d^2 <= sumArea /
+    // maxError, or the query inside the leaf's box): max(sqrt(sumArea / maxError), diag) + diag,
+    // squared, rounded up; +inf for interior nodes and leaves without a finite centroid. Lets the
+    // sharded gather prove a leaf's point lookups lie in its LDS near field. Valid for
+    // leaf_r2_error == the gather's max_error.
+    DevBuf<float> leaf_r2;
+    float leaf_r2_error = -1.f;
+    void ensure_leaf_r2(float max_error);  // synchronous
     void upload(const FlatOctree &t);
     const BandLayout *find_layout(const BandGroups &g) const;
     // builds the layout if it is missing (synchronizes the device); the caller serializes calls

@@ -524,8 +524,14 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     bt.band_e = l.e.ptr;
     bt.table = p.table.ptr;
     bt.groups = p.groups;
-    for (int g = 0; g < kGroups; ++g)
-        for (int s = 0; s < 4; ++s) bt.grcp[g][s] = p.groups.band[g][s] >= 0 ? p.host_rcp[p.groups.band[g][s]] : 0.f;
+    for (int g = 0; g < kGroups; ++g) {
+        bt.grcp_max[g] = 0.f;
+        for (int s = 0; s < 4; ++s) {
+            bt.grcp[g][s] = p.groups.band[g][s] >= 0 ? p.host_rcp[p.groups.band[g][s]] : 0.f;
+            bt.grcp_max[g] = bt.grcp[g][s] > bt.grcp_max[g] ? bt.grcp[g][s] : bt.grcp_max[g];
+        }
+    }
+    bt.leaf_r2 = (t.leaf_r2.ptr && t.leaf_r2_error == max_error) ? t.leaf_r2.ptr : nullptr;
     bt.L = p.L;
     bt.n_nodes = t.n_nodes;
     bt.n_points = t.n_points;
@@ -586,6 +592,7 @@ void DeviceOctree::upload(const FlatOctree &t) {
             }
     }
     layouts.clear();
+    leaf_r2_error = -1.f;
     nodes.upload(hdr.data(), hdr.size());
     node_et.upload(t.node_et.data(), t.node_et.size());
     pt_hdr.upload(reinterpret_cast<const float4 *>(ph.data()), ph.size() / 4);
@@ -612,6 +619,35 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
     for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
     groups = make_band_groups(rcp_, snake);
+}
+
+namespace {
+__global__ void leaf_r2_kernel(const NodeHdr *__restrict__ nodes, int n, float max_error, float *__restrict__ r2) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const NodeHdr h = nodes[i];
+    float out = INFINITY;
+    if (h.leaf_first >= 0 && h.sum_area > 0.f && max_error > 0.f && isfinite(h.px) && isfinite(h.py) &&
+        isfinite(h.pz)) {
+        const double dx = (double)h.bmaxx - h.bminx, dy = (double)h.bmaxy - h.bminy, dz = (double)h.bmaxz - h.bminz;
+        const double diag = sqrt(dx * dx + dy * dy + dz * dz);
+        const double open = sqrt((double)h.sum_area / (double)max_error) * (1.0 + 1e-6);
+        const double R = (open > diag ? open : diag) + diag;
+        out = (float)(R * R * (1.0 + 1e-6));
+    }
+    r2[i] = out;
+}
+}  // namespace
+
+void DeviceOctree::ensure_leaf_r2(float max_error) {
+    if (leaf_r2.ptr && leaf_r2_error == max_error) return;
+    leaf_r2.alloc((size_t)(n_nodes > 0 ? n_nodes : 1));
+    if (n_nodes > 0)
+        hipLaunchKernelGGL(leaf_r2_kernel, dim3((unsigned)((n_nodes + 255) / 256)), dim3(256), 0, 0, nodes.ptr, n_nodes,
+                           max_error, leaf_r2.ptr);
+    MPSS_HIP(hipGetLastError());
+    MPSS_HIP(hipDeviceSynchronize());
+    leaf_r2_error = max_error;
 }
 
 const BandLayout *DeviceOctree::find_layout(const BandGroups &g) const {

@@ -370,6 +370,7 @@ void build_octree_device(int n, const float *P, const float *N, const float *E, 
         hipLaunchKernelGGL(preorder_level_kernel, dim3(grid_of(hi - lo)), dim3(256), 0, 0, lo, hi, nd);
     }
     t.layouts.clear();
+    t.leaf_r2_error = -1.f;
     t.nodes.alloc(n_nodes);
     t.node_et.alloc((size_t)n_nodes * ROW);
     t.pt_hdr.alloc(n);
