@@ -89,18 +89,23 @@ MPSS_HD V3 xform_normal(const float *minv, V3 n) {  // uses the inverse matrix, 
 // ---------------------------------------------------------------- low-discrepancy samples
 // montecarlo.h:278-302
 MPSS_HD float van_der_corput(uint32_t n, uint32_t scramble) {
-    n = (n << 16) | (n >> 16);
-    n = ((n & 0x00ff00ffu) << 8) | ((n & 0xff00ff00u) >> 8);
-    n = ((n & 0x0f0f0f0fu) << 4) | ((n & 0xf0f0f0f0u) >> 4);
-    n = ((n & 0x33333333u) << 2) | ((n & 0xccccccccu) >> 2);
-    n = ((n & 0x55555555u) << 1) | ((n & 0xaaaaaaaau) >> 1);
-    n ^= scramble;
+    n = __builtin_bitreverse32(n) ^ scramble;
     const float v = (float)((n >> 8) & 0xffffff) / (float)(1 << 24);
     return v < kOneMinusEps ? v : kOneMinusEps;
 }
+// Sobol2's generator has columns v_0 = 2^31, v_{i+1} = v_i ^ (v_i >> 1): column i is row i of Pascal's
+// triangle mod 2, top bit first. By Lucas' theorem, bit 31 - j of the XOR of the columns of n's set
+// bits is the parity of n's bits at the positions i that contain j (i & j == j) -- a superset-sum
+// transform of n in five shift-xor steps, then bit-reversed: the loop's value for every n, without
+// its n-dependent trip count (tests/test_sampler_replay.py checks the transform against the loop for
+// every 16-bit n; the GPU image tests against the oracle's loop).
 MPSS_HD float sobol2(uint32_t n, uint32_t scramble) {
-    for (uint32_t v = 1u << 31; n != 0; n >>= 1, v ^= v >> 1)
-        if (n & 1u) scramble ^= v;
+    n ^= (n >> 1) & 0x55555555u;
+    n ^= (n >> 2) & 0x33333333u;
+    n ^= (n >> 4) & 0x0f0f0f0fu;
+    n ^= (n >> 8) & 0x00ff00ffu;
+    n ^= (n >> 16) & 0x0000ffffu;
+    scramble ^= __builtin_bitreverse32(n);
     const float r = (float)((scramble >> 8) & 0xffffff) / (float)(1 << 24);
     return r < kOneMinusEps ? r : kOneMinusEps;
 }

@@ -202,3 +202,26 @@ def test_irradiance_scrambles_match_python(oracle):
                 ref[i, l] = rng.u32(), rng.u32()
                 rng.u32()
     assert np.array_equal(scr, ref)
+
+
+def test_sobol2_closed_form_equals_the_loop():
+    """pbrt_math.h sobol2: the superset-sum transform + bit reversal equals Sobol02's column loop
+    (montecarlo.h:292-302) for every 16-bit index and random 32-bit ones."""
+    def loop(n, scr):
+        v = 1 << 31
+        while n:
+            if n & 1:
+                scr ^= v
+            n >>= 1
+            v ^= v >> 1
+        return scr
+
+    def closed(n, scr):
+        for k, m in ((1, 0x55555555), (2, 0x33333333), (4, 0x0F0F0F0F), (8, 0x00FF00FF), (16, 0x0000FFFF)):
+            n ^= (n >> k) & m
+        return int("{:032b}".format(n)[::-1], 2) ^ scr
+
+    rng = np.random.default_rng(7)
+    ns = list(range(1 << 16)) + [int(x) for x in rng.integers(0, 1 << 32, 4096, dtype=np.uint64)]
+    scr = [int(x) for x in rng.integers(0, 1 << 32, len(ns), dtype=np.uint64)]
+    assert all(loop(n, s) == closed(n, s) for n, s in zip(ns, scr))
