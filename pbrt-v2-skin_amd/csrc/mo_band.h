@@ -287,7 +287,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     // opens it: leaf_r2 * rcp_max < klim (with a 1e-5 margin for the roundings of d2 and f)
     const float lds_r2_lim = (float)b.klim / (a.grcp_max[grp] * 1.00001f);
     const cptr<float> leaf_r2 = as_const(a.leaf_r2);
-    const float rcp_min = a.groups.rcp_min[grp];
+    // box2 * rcp_min >= prune_f as one compare: prune_f carries a 1e-4 margin over the profile end,
+    // far above the rounding of the quotient (rcp_min 0: pruning off, INF)
+    const float box_lim = a.prune_f / a.groups.rcp_min[grp];
     const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
     const cptr<float4> e_g = as_const(a.band_e + (size_t)grp * a.n_points);
     const cptr<NodeHdr> nodes = as_const(a.nodes);
@@ -298,6 +300,11 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         node = __builtin_amdgcn_readfirstlane(node);
         if (COUNT) ++w_nodes;
         const NodeHdr h = nodes[node];
+        // the whole 64-B header (one scalar-cache line) in one load, waited for once, instead of
+        // pieces loaded as the decisions below need them (each a further scalar-cache round trip)
+        asm volatile("" ::"s"(h.px), "s"(h.py), "s"(h.pz), "s"(h.sum_area), "s"(h.bminx), "s"(h.bminy),
+                     "s"(h.bminz), "s"(h.bmaxx), "s"(h.bmaxy), "s"(h.bmaxz), "s"(h.skip), "s"(h.leaf_first),
+                     "s"(h.flags), "s"(h.pad));
         const int skip = h.skip;
         bool open = false;
         if (node >= resume) {
@@ -308,7 +315,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             const float bz = fmaxf(fmaxf(h.bminz - pz, pz - h.bmaxz), 0.f);
             // exact-zero pruning with a 1e-4 margin (prune_f), so the test may round freely
             const float box2 = __builtin_fmaf(bz, bz, __builtin_fmaf(by, by, bx * bx));
-            if (box2 * rcp_min >= a.prune_f || (h.flags & NODE_BLACK)) {
+            if (box2 >= box_lim || (h.flags & NODE_BLACK)) {
                 resume = skip;
             } else {
                 const float dx = px - h.px, dy = py - h.py, dz = pz - h.pz;
@@ -356,6 +363,13 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const int ka = h.leaf_first + i0, kb = ka + 1;
                         const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];
                         const float4 ea = e_g[ka], eb = e_g[kb];
+                        // both points' headers and E in one scalar round trip: loaded later, the wait for
+                        // them would also wait out the table loads already in flight (a flat load counts in
+                        // lgkmcnt too) and split the pair's lookups into two round trips
+                        if (!COUNT)
+                            asm volatile("" ::"s"(pa.x), "s"(pa.y), "s"(pa.z), "s"(pa.w), "s"(pb.x), "s"(pb.y),
+                                         "s"(pb.z), "s"(pb.w), "s"(ea.x), "s"(ea.y), "s"(ea.z), "s"(ea.w),
+                                         "s"(eb.x), "s"(eb.y), "s"(eb.z), "s"(eb.w));
                         if (!open) continue;
                         if (COUNT) k_pts += 2;
                         const float ax = px - pa.x, ay = py - pa.y, az = pz - pa.z;
@@ -366,6 +380,12 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         RdPair va[4], vb[4];
                         band_rd_fetch<COUNT, KLDS>(b, d2a, fa, va, hist);
                         band_rd_fetch<COUNT, KLDS>(b, d2b, fb, vb, hist);
+                        // all eight lookups in flight before the first is consumed
+                        if (!COUNT)
+                            asm volatile("" ::"v"(va[0].a), "v"(va[0].b), "v"(va[1].a), "v"(va[1].b), "v"(va[2].a),
+                                         "v"(va[2].b), "v"(va[3].a), "v"(va[3].b), "v"(vb[0].a), "v"(vb[0].b),
+                                         "v"(vb[1].a), "v"(vb[1].b), "v"(vb[2].a), "v"(vb[2].b), "v"(vb[3].a),
+                                         "v"(vb[3].b));
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         band_rd_combine<true>(fa, va, e0, pa.w, lacc);
                         band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
