@@ -19,7 +19,8 @@ namespace mpss {
 
 namespace {
 
-constexpr int kMcMaxSegments = 4096;  // ComputeMonteCarloProfile tallies 4096 rings (multipole.cpp:322)
+constexpr int kMcMaxSegments = 4096;
+constexpr int kMcPool = 256;  // photon ids a wave takes from the global counter at a time  // ComputeMonteCarloProfile tallies 4096 rings (multipole.cpp:322)
 // pbrt's M_PI is the float literal 3.14159265358979323846f (core/pbrt.h:193-196); the walk and the
 // ring normalisation use it widened to double
 constexpr double kPbrtPi = (double)3.14159265358979323846f;
@@ -29,8 +30,10 @@ __device__ __forceinline__ void sample_sphere_d(double u1, double u2, double &x,
     z = 1. - 2. * u1;
     const double r = sqrt(fmax(0., 1. - z * z));
     const double phi = 2. * kPbrtPi * u2;
-    x = r * cos(phi);
-    y = r * sin(phi);
+    double sp, cp;
+    sincos(phi, &sp, &cp);  // one range reduction for both (the same values as cos / sin)
+    x = r * cp;
+    y = r * sp;
 }
 
 // FrDiel<double> (core/reflection.cpp:72-80) with etat = 1
@@ -62,18 +65,30 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
     McRng rng;
     rng.s = 0;
     unsigned long long nev = 0;
+    // the wave's own run of photon ids [pool, pool + pool_left), taken kMcPool at a time from the
+    // global counter: one atomic per kMcPool photons instead of one per refill (photons finish one
+    // by one, and a single counter serves only ~1e8 atomics/s)
+    uint64_t pool = 0;
+    int pool_left = 0;
     for (;;) {
-        // refill lanes whose photon has finished (one atomic per wave)
+        // refill lanes whose photon has finished
         if (!exhausted) {
             const uint64_t need = __builtin_amdgcn_ballot_w64(!alive);
             if (need) {
-                unsigned long long base = 0;
-                if (lane == (int)__builtin_ctzll(need))
-                    base = atomicAdd(a.next, (unsigned long long)__builtin_popcountll(need));
-                base = __shfl(base, (int)__builtin_ctzll(need));
-                if (!alive) {
-                    const uint64_t id = base + (uint64_t)__builtin_popcountll(need & ((1ull << lane) - 1ull));
-                    if (id < a.nphotons) {
+                if (pool_left == 0) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(a.next, (unsigned long long)kMcPool);
+                    base = __shfl(base, 0);
+                    pool = base;
+                    pool_left = base < a.nphotons ? (int)(a.nphotons - base < (uint64_t)kMcPool ? a.nphotons - base
+                                                                                                 : (uint64_t)kMcPool)
+                                                  : 0;
+                    if (pool_left == 0) exhausted = true;
+                }
+                const int rank = __builtin_popcountll(need & ((1ull << lane) - 1ull));
+                if (!alive && rank < pool_left) {
+                    const uint64_t id = pool + (uint64_t)rank;
+                    {
                         // TraceSinglePhoton setup (:233-241), then the outer loop's head (:245-248)
                         rng.init(a.seed, id);
                         ox = oy = oz = 0.;
@@ -87,7 +102,9 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                         alive = true;
                     }
                 }
-                if (base + (unsigned long long)__builtin_popcountll(need) >= a.nphotons) exhausted = true;
+                const int used = __builtin_popcountll(need) < pool_left ? __builtin_popcountll(need) : pool_left;
+                pool += (uint64_t)used;
+                pool_left -= used;
             }
         }
         if (__builtin_amdgcn_ballot_w64(alive) == 0) break;
@@ -122,11 +139,18 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                 }
             }
         }
+        // the step's attenuation: to the interface (a hit) or over the free flight (a scatter) --
+        // one exp for the wave, whichever branch each lane takes
+        double px = 0., py = 0., pz = 0., dist = 0.;
         if (hit) {
-            const double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            px = ox + dx * t;
+            py = oy + dy * t;
+            pz = oz + dz * t;
             const double ex = px - ox, ey = py - oy, ez = pz - oz;
-            const double dist = sqrt(ex * ex + ey * ey + ez * ez);
-            thr *= exp((double)-L.mua * dist);
+            dist = sqrt(ex * ex + ey * ey + ez * ez);
+        }
+        thr *= exp((double)-L.mua * (hit ? dist : len));
+        if (hit) {
             len = fmax(1e-7 * mfp, len - dist);
             const double cosi = fmin(fmax(dz, -1.), 1.);
             const bool up = dz < 0.;
@@ -185,7 +209,6 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
             ox = ox + dx * len;
             oy = oy + dy * len;
             oz = oz + dz * len;
-            thr *= exp((double)-L.mua * len);
             len = 0.;
             const double u1 = rng.next(), u2 = rng.next();
             sample_sphere_d(u1, u2, dx, dy, dz);

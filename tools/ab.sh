@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of two builds of libmpss.so (box-to-box spread is a few per cent, more than the
 # variants under test): ab/libmpss_A.so and ab/libmpss_B.so take turns as the in-tree library,
-# each running the quick bench of CFG, ROUNDS times; one line per run -> gpurun_out/TAG_ab.txt.
+# each running the quick bench of CFG (c4: tools/bench_mc.py), ROUNDS times; one line per run -> gpurun_out/TAG_ab.txt.
 #
 #   bash tools/ab.sh TAG [CFG] [ROUNDS]
 set -o pipefail
@@ -21,8 +21,13 @@ for r in $(seq 1 $ROUNDS); do
   for v in A B; do
     cp ab/libmpss_$v.so $lib
     log=gpurun_out/${TAG}_ab_${v}${r}.log
-    timeout -k 10 600 python -u bench.py --config $CFG "${steps[@]}" --no-cpu-baseline > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
-    python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["roofline"]["kernel_ms_per_step"])' $log $v$r | tee -a $out
+    if [ $CFG = c4 ]; then
+      timeout -k 10 300 python -u tools/bench_mc.py --cpu-seconds 0 > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
+      python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["seconds"], d["total_r"], d["total_t"])' $log $v$r | tee -a $out
+    else
+      timeout -k 10 600 python -u bench.py --config $CFG "${steps[@]}" --no-cpu-baseline > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
+      python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["roofline"]["kernel_ms_per_step"])' $log $v$r | tee -a $out
+    fi
   done
 done
 cp ab/libmpss_orig.so $lib
