@@ -99,7 +99,7 @@ def mc_roofline(seconds):
     if best:
         _, f, e = best
         inst = e["SQ_INSTS_VALU"]["mean"] * e["SQ_INSTS_VALU"]["dispatches"]
-        # the PMC run times the warm-up walk too: scale its instruction count to the measured walk's
+        # the PMC run counts the 1e5-photon warm-up walk too (0.1 % of the 1e8-photon walk's instructions)
         r["achieved"] = round(inst / seconds / 1e9, 2) if inst else None
         r["frac"] = round(inst / seconds / VALU_PEAK_INST_S, 4) if inst else None
         r["source"] = os.path.relpath(f, ROOT) + " (SQ_INSTS_VALU summed over the command's dispatches)"
