@@ -281,7 +281,7 @@ def main(a):
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
     # The gather's binding resource is the L2 request rate of its per-lane table gathers:
-    # the headline roofline is requests per second against the rate tools/microbench/l2_gather.hip
+    # the headline roofline is requests per second against the rate tools/microbench/l2_policy.hip
     # sustains. Its request count comes from the committed PMC pass of the same config and kernel
     # sources (TCP_TCC_READ_REQ per launch), its duration from this run's HIP events.
     pt = pmc_traffic(a.pmc_json, shade_launch_ms, a.config)

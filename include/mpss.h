@@ -196,6 +196,7 @@ int mpss_octree_info(mpss_ctx *ctx, uint32_t *n_nodes, uint32_t *max_depth, uint
 int mpss_octree_export(mpss_ctx *ctx, void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index);
 
 /* Mo for q shading points (p_dev: q*3 floats) with material's Rd profile; mo_dev: q*30 floats.
+ * 0 <= q <= 2^30 (q = 0: nothing is launched; larger: MPSS_ERR_INVALID).
  * counters_dev (nullable): q*4 int32 {nodes entered, leaf points evaluated} by the reference
  * recursion (exact_mo = 1 only; else 0), then the same two counts for the kernel's pruned traversal. */
 int mpss_mo_batch(mpss_ctx *ctx, uint32_t material_id, uint32_t q, const float *p_dev, float *mo_dev,

@@ -178,6 +178,7 @@ int mpss_set_irradiance_points(mpss_ctx *c, uint32_t n, const float *p, const fl
     return guarded([&] {
         require(c && p && nrm && E && area, "mpss_set_irradiance_points: null argument");
         require(n > 0, "mpss_set_irradiance_points: empty point set");
+        require(n <= (1u << 30), "mpss_set_irradiance_points: at most 2^30 points");
         reinterpret_cast<Context *>(c)->set_irradiance_points((int)n, p, nrm, E, area);
     });
 }
@@ -203,6 +204,7 @@ int mpss_mo_batch(mpss_ctx *c, uint32_t id, uint32_t q, const float *p_dev, floa
                   void *stream) {
     return guarded([&] {
         require(c && (q == 0 || (p_dev && mo_dev)), "mpss_mo_batch: null argument");
+        require(q <= (1u << 30), "mpss_mo_batch: at most 2^30 queries per call");
         reinterpret_cast<Context *>(c)->mo_batch(id, (int)q, p_dev, mo_dev, counters_dev, (hipStream_t)stream);
     });
 }

@@ -108,6 +108,37 @@ def test_mo_edge_cases(oracle, mpss, torch_dev, wide_profile):
     assert np.all(mo == 0) and np.all(cnt[:, 0] == 1)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_mo_batch_sizes(mpss, torch_dev, wide_profile, mode):
+    """q = 0 launches nothing and leaves the output alone; q above 2^30 and an empty point set
+    are refused (MPSS_ERR_INVALID) before any launch; one query and 64 + 1 queries (a wave plus a
+    one-lane tail) equal the same queries inside a larger batch."""
+    table, rcp = wide_profile
+    p, n, E, area = synth.ellipsoid_cloud(3000, radii=RADII, seed=31, black_frac=0.05)
+    ctx = mpss.Context(max_error=0.1, exact_mo=mode)
+    mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
+    with pytest.raises(mpss.MpssError):
+        ctx.set_irradiance_points(p[:0], n[:0], E[:0], area[:0])
+    ctx.set_irradiance_points(p, n, E, area)
+    q = synth.surface_queries(1100, radii=RADII, seed=37)
+    qd = torch_dev.from_numpy(q).cuda()
+    out = torch_dev.full((len(q), 30), -1.0, dtype=torch_dev.float32, device="cuda")
+    ctx.mo_batch(mid, 0, qd.data_ptr(), out.data_ptr())
+    torch_dev.cuda.synchronize()
+    assert bool((out == -1.0).all())
+    with pytest.raises(mpss.MpssError):
+        ctx.mo_batch(mid, (1 << 30) + 1, qd.data_ptr(), out.data_ptr())
+    ctx.mo_batch(mid, len(q), qd.data_ptr(), out.data_ptr())
+    torch_dev.cuda.synchronize()
+    full = out.cpu().numpy()
+    for lo, m in ((0, 1), (700, 65)):
+        part = torch_dev.zeros((m, 30), dtype=torch_dev.float32, device="cuda")
+        ctx.mo_batch(mid, m, qd[lo:lo + m].contiguous().data_ptr(), part.data_ptr())
+        torch_dev.cuda.synchronize()
+        assert np.array_equal(part.cpu().numpy(), full[lo:lo + m]), (lo, m)
+    ctx.close()
+
+
 def test_layeredskin_material_on_device(oracle, mpss, torch_dev):
     """mpss_add_layeredskin builds the tables itself; they must match the oracle's."""
     ctx = mpss.Context(max_error=0.1)
