@@ -76,14 +76,15 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
-                    help="BASELINE.json config (default: c2 on one GPU, c3 strong scaling on several)")
+                    help="BASELINE.json config (default c2, the metric's config, at every N: one frame per GPU "
+                         "per step; several GPUs add the C3 strong-scaling figure as `secondary`)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
                     help="weak: one frame per GPU per step; strong: one frame per step split over the GPUs "
                          "(default: the config's)")
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"))
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
-    ap.add_argument("--tile", type=int, default=None, help="tile size (default 128 on one GPU, 64 on several)")
+    ap.add_argument("--tile", type=int, default=None, help="tile size (default 128; 64 for c3 on several GPUs)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--batch-log2", type=int, default=None,
                     help="camera samples per render batch, log2 (mpss_config.max_batch_samples; default 2^24)")
