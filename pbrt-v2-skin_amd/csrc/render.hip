@@ -1394,6 +1394,27 @@ __global__ __launch_bounds__(256) void film_kernel(RenderScene sc, PieceList pl,
         const uint32_t need = (dx < 0 ? REC_XHI : dx > 0 ? REC_XLO : 0u) | (dy < 0 ? REC_YHI : dy > 0 ? REC_YLO : 0u);
         if (q == 0) {
             const int32_t *sl = rec.slot + li * tb.spp;
+            if ((tb.spp & 7) == 0) {
+                // 8 slots as two 16-byte loads: a lane's run of slots is contiguous, and the
+                // vector-memory path pays per cache line an instruction touches, so one wide load
+                // per line instead of four narrow ones (same slots, same order)
+                const int4 *sl4 = reinterpret_cast<const int4 *>(sl);
+                for (int s0 = 0; s0 < tb.spp; s0 += 8) {
+                    const int4 a4 = sl4[s0 >> 2], b4 = sl4[(s0 >> 2) + 1];
+                    const int32_t v[8] = {a4.x, a4.y, a4.z, a4.w, b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (v[k] >= 0) {
+                            const float4 x = rec.xyz[v[k]];
+                            X += 1.f * x.x;
+                            Y += 1.f * x.y;
+                            Z += 1.f * x.z;
+                        }
+                        W += 1.f;
+                    }
+                }
+                continue;
+            }
             for (int s0 = 0; s0 < tb.spp; s0 += 8) {
                 int32_t v[8];
 #pragma unroll
