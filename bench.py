@@ -149,7 +149,11 @@ def build_scene(a, label_cfg, local):
 
 
 def deal(ctx, sc, T, frames, world):
-    """Tiles of `frames` frames dealt over `world` ranks by estimated cost (identical on every rank)."""
+    """Tiles of `frames` frames dealt over `world` ranks (identical on every rank). One frame per
+    rank (weak scaling) gives each rank a whole frame: the frames cost the same, and one frame's
+    tiles render in one mpss_render_tiles call, one Mo() gather launch per step -- tiles of several
+    frames would cost one smaller launch per frame (one seed per call). Otherwise the tiles are
+    dealt by estimated cost."""
     import numpy as np
     from mpss import tiles as tl
     tiles = tl.tile_grid(sc.xres, sc.yres, T)
@@ -158,7 +162,11 @@ def deal(ctx, sc, T, frames, world):
     cost1 = tl.tile_cost_model(sss, surf, px)
     items_all = [(f, t) for f in range(frames) for t in range(len(tiles))]
     costs = [cost1[t] for _, t in items_all]
-    by_rank_idx = tl.deal_balanced(costs, world)
+    if frames == world and world > 1:
+        nt = len(tiles)
+        by_rank_idx = [list(range(r * nt, (r + 1) * nt)) for r in range(world)]
+    else:
+        by_rank_idx = tl.deal_balanced(costs, world)
     items_by_rank = [[items_all[i] for i in idx] for idx in by_rank_idx]
     return tiles, items_by_rank, tl.balance(costs, by_rank_idx), int((np.asarray(sss) > 0).sum())
 
@@ -334,8 +342,10 @@ def main(a):
                 "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh%s)" % (", subdivided" if subdiv else ""),
-                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles dealt by cost, RCCL film gather"
-                           % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T),
+                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles%s, RCCL film gather"
+                           % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T,
+                              ", a whole frame per GPU" if frames == world and world > 1 else
+                              (" dealt by cost" if world > 1 else "")),
                            "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3), "tile_deal_s": round(t_deal, 3),
