@@ -22,6 +22,10 @@ struct McScene {  // MiniScene (mcprofile.cpp:142-193)
     double depth[kMcMaxLayers + 1];  // interface depths: 0, d0, d0 + d1, ...
     double extent;                   // mfpRange * mean mfp
     int nsegments;
+    // per-layer constants of the walk, divided once on the host (the same IEEE double quotients)
+    double mfp[kMcMaxLayers];     // 1 / musp
+    double eta_dn[kMcMaxLayers];  // ior / ior of the layer below (1 past the last), the ray going down
+    double eta_up[kMcMaxLayers];  // ior / ior of the layer above (1 above the first), the ray going up
 };
 
 // Per-photon random stream ("replay mode"): splitmix64 seeded from (seed, photon),

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                         thr = 1.;
                         len = 0.;
                         layer = 0;
-                        mfp = 1. / (double)sc.layer[0].musp;
+                        mfp = sc.mfp[0];
                         len *= mfp;
                         alive = true;
                     }
@@ -125,8 +125,7 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                     hit = true;
                     iface = layer + 1;
                     t = (nd - oz) / ct;
-                    const double nior = (layer + 1 == sc.nlayers) ? 1. : (double)sc.layer[layer + 1].ior;
-                    inv = (double)L.ior / nior;
+                    inv = sc.eta_dn[layer];
                 }
             } else {
                 const double nd = sc.depth[layer];
@@ -134,8 +133,7 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                     hit = true;
                     iface = layer;
                     t = (nd - oz) / ct;
-                    const double nior = (layer == 0) ? 1. : (double)sc.layer[layer - 1].ior;
-                    inv = (double)L.ior / nior;
+                    inv = sc.eta_up[layer];
                 }
             }
         }
@@ -198,7 +196,7 @@ __global__ __launch_bounds__(256) void mc_profile_kernel(McArgs a) {
                     if (layer < 0 || layer >= sc.nlayers) {
                         dead = true;
                     } else {
-                        mfp = 1. / (double)sc.layer[layer].musp;  // next outer loop's head
+                        mfp = sc.mfp[layer];  // next outer loop's head
                         len *= mfp;
                     }
                 }
@@ -240,6 +238,11 @@ McScene make_mc_scene(const McLayer *layers, int n, double mfp_range, int nsegme
     }
     sc.extent = mfp_range * (mfp_total / (double)n);
     sc.nsegments = nsegments;
+    for (int i = 0; i < n; ++i) {
+        sc.mfp[i] = 1. / (double)layers[i].musp;
+        sc.eta_dn[i] = (double)layers[i].ior / (i + 1 == n ? 1. : (double)layers[i + 1].ior);
+        sc.eta_up[i] = (double)layers[i].ior / (i == 0 ? 1. : (double)layers[i - 1].ior);
+    }
     return sc;
 }
 
