@@ -102,6 +102,9 @@ typedef struct {
                                   next group with work left; 0: each stays on its own group (XCD) */
     int mo_near_field;         /* profile entries per band kept in LDS: 10236 (default; one workgroup
                                   per CU holds the whole 160 KB) or 5088 (two workgroups per CU) */
+    int tessellate_on_host;    /* 1: Preprocess tessellates on the host (threads over triangles,
+                                  scene.cpp); 0 (default): one GPU thread per triangle (render.hip
+                                  tess_kernel), the same points bit for bit (tessellate.h) */
 } mpss_config;
 
 enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };

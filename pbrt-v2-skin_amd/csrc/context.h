@@ -121,6 +121,7 @@ public:
     void set_camera(const float *r2c, const float *c2w, int xres, int yres);
     void set_surface_points(uint32_t n, const SurfacePoint *pts);
     void preprocess(uint32_t seed);
+    void tessellate_on_gpu();  // Preprocess point set, GPU build (render_host.hip)
     // FindPoissonPointDistribution (usepoissonpointfinder): fills points_ (render_host.hip)
     void find_poisson_points(uint32_t seed);
     void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);

@@ -42,14 +42,15 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 8; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 9; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
                                           // 6: GPU octree build (octree_on_host), mpss_octree_export;
                                           // 7: gather choices in mpss_config (mo_band_dealing,
                                           //    mo_work_stealing, mo_near_field), count_traversal 2;
                                           // 8: light spheres seen directly shaded (default matte),
-                                          //    rebuilds wait for in-flight render / mo_batch calls
+                                          //    rebuilds wait for in-flight render / mo_batch calls;
+                                          // 9: GPU tessellation (tessellate_on_host), size bounds
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -74,6 +75,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->mo_band_dealing = 0;
     c->mo_work_stealing = 1;
     c->mo_near_field = 10236;
+    c->tessellate_on_host = 0;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {

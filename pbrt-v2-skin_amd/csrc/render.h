@@ -170,6 +170,9 @@ struct PoissonWalk {
     int npaths;
 };
 __global__ void poisson_walk_kernel(RenderScene sc, PoissonWalk w, SurfacePoint *out, int *count);
+template <bool EMIT, bool INCENTER>
+__global__ void tess_kernel(RenderScene sc, int mesh, int ntri, int64_t base, float min_dist, int64_t *counts,
+                            const int64_t *offs, SurfacePoint *out);
 
 __global__ void irradiance_kernel(RenderScene sc, const float *sp_p, const float *sp_n, const float *sp_eps,
                                   const uint32_t *sp_mat, const float *sp_uv, int n, uint32_t seed, float *E_out);

@@ -17,6 +17,7 @@
 
 #include "../../data/spectral_bands.h"
 #include "geom.h"
+#include "tessellate.h"
 
 namespace mpss {
 
@@ -1453,6 +1454,44 @@ __global__ __launch_bounds__(256) void film_kernel(RenderScene sc, PieceList pl,
     o[2] = Z;
     o[3] = W;
 }
+
+// ------------------------------------------------------------------ Preprocess: tessellation
+// TessellateSurfacePoints on the GPU (tessellate.h, the host build's code), one thread per triangle
+// of one mesh: the counting pass writes each triangle's point count, the emitting pass its points
+// from out[offs[base + t]] in the reference's shader order. Points therefore land in triangle order,
+// as the host build and the reference (surfacepoints.cpp:328-332) emit them.
+// INCENTER is a template parameter, not a kernel argument: with the centroid/incentre choice left to a
+// run-time flag, this compiler (ROCm 7.2, gfx950) evaluated the incentre for the sub-triangles of one
+// of tess_matching's two shader call sites (tests/test_tessellate_gpu.py caught it); with the choice
+// fixed at compile time every point equals the host build's.
+template <bool EMIT, bool INCENTER>
+__global__ __launch_bounds__(64) void tess_kernel(RenderScene sc, int mesh, int ntri, int64_t base, float min_dist,
+                                                  int64_t *counts, const int64_t *offs, SurfacePoint *out) {
+    const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t >= ntri) return;
+    const RenderMesh &m = sc.meshes[mesh];
+    const TessTri tr = tess_tri(m.view, t, min_dist);
+    if (!EMIT) {
+        int64_t n = 0;
+        auto shader = [&](BC, BC, BC) { ++n; };
+        tessellator(tr.tfe0, tr.tfe1, tr.tfe2, tr.tfc, shader);
+        counts[base + t] = n;
+        return;
+    }
+    const RenderMaterial &mt = sc.materials[m.material];
+    const TexView *bt = mt.has_bump ? &mt.bump_tex : nullptr;
+    int64_t k = offs[base + t];
+    auto shader = [&](BC a, BC b, BC c) {
+        out[k++] = tess_point(m.view, t, tr, a, b, c, INCENTER, bt, m.material, min_dist);
+    };
+    tessellator(tr.tfe0, tr.tfe1, tr.tfe2, tr.tfc, shader);
+}
+template __global__ void tess_kernel<false, false>(RenderScene, int, int, int64_t, float, int64_t *, const int64_t *,
+                                                   SurfacePoint *);
+template __global__ void tess_kernel<true, false>(RenderScene, int, int, int64_t, float, int64_t *, const int64_t *,
+                                                  SurfacePoint *);
+template __global__ void tess_kernel<true, true>(RenderScene, int, int, int64_t, float, int64_t *, const int64_t *,
+                                                 SurfacePoint *);
 
 // ------------------------------------------------------------------ tile-cost probe
 // PerspectiveCamera::GenerateRay through the pixel centre and Scene::Intersect, as primary_kernel.

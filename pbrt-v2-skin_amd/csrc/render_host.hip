@@ -319,6 +319,55 @@ void Context::set_surface_points(uint32_t n, const SurfacePoint *pts) {
     have_points_ = n > 0;
 }
 
+// TessellateSurfacePointsRenderer's point set on the GPU (tess_kernel): per mesh a counting pass,
+// a prefix sum of the per-triangle counts on the host (one int64 per triangle), then the emitting
+// pass; the points come back to points_ (mpss_get_surface_points / the pointsfile read them there).
+void Context::tessellate_on_gpu() {
+    const RenderScene sc = render_scene();
+    std::vector<int64_t> base(scene_.meshes.size() + 1, 0);
+    for (size_t m = 0; m < scene_.meshes.size(); ++m)
+        base[m + 1] = base[m] + (int64_t)(scene_.meshes[m].idx.size() / 3);
+    const int64_t ntri = base.back();
+    points_.clear();
+    if (ntri == 0) return;
+    DevBuf<int64_t> cnt, off;
+    cnt.alloc((size_t)ntri);
+    off.alloc((size_t)ntri);
+    for (size_t m = 0; m < scene_.meshes.size(); ++m) {
+        const int nt = (int)(base[m + 1] - base[m]);
+        if (nt > 0)
+            hipLaunchKernelGGL((tess_kernel<false, false>), dim3((unsigned)((nt + 63) / 64)), dim3(64), 0, 0, sc,
+                               (int)m, nt, base[m], min_dist_, cnt.ptr, (const int64_t *)nullptr,
+                               (SurfacePoint *)nullptr);
+    }
+    MPSS_HIP(hipGetLastError());
+    std::vector<int64_t> h((size_t)ntri);
+    MPSS_HIP(hipMemcpy(h.data(), cnt.ptr, sizeof(int64_t) * (size_t)ntri, hipMemcpyDeviceToHost));
+    int64_t total = 0;
+    for (int64_t i = 0; i < ntri; ++i) {
+        const int64_t c = h[(size_t)i];
+        h[(size_t)i] = total;
+        total += c;
+    }
+    if (total > ((int64_t)1 << 30)) throw Error(MPSS_ERR_INVALID, "tessellation: more than 2^30 surface points");
+    if (total == 0) return;
+    MPSS_HIP(hipMemcpy(off.ptr, h.data(), sizeof(int64_t) * (size_t)ntri, hipMemcpyHostToDevice));
+    DevBuf<SurfacePoint> pts;
+    pts.alloc((size_t)total);
+    for (size_t m = 0; m < scene_.meshes.size(); ++m) {
+        const int nt = (int)(base[m + 1] - base[m]);
+        if (nt > 0) {
+            void (*emit)(RenderScene, int, int, int64_t, float, int64_t *, const int64_t *, SurfacePoint *) =
+                cfg_.incenter ? tess_kernel<true, true> : tess_kernel<true, false>;
+            hipLaunchKernelGGL(emit, dim3((unsigned)((nt + 63) / 64)), dim3(64), 0, 0, sc, (int)m, nt, base[m],
+                               min_dist_, cnt.ptr, (const int64_t *)off.ptr, pts.ptr);
+        }
+    }
+    MPSS_HIP(hipGetLastError());
+    points_.resize((size_t)total);
+    MPSS_HIP(hipMemcpy(points_.data(), pts.ptr, sizeof(SurfacePoint) * (size_t)total, hipMemcpyDeviceToHost));
+}
+
 // MultipoleSubsurfaceIntegrator::Preprocess (multipolesubsurface.cpp:170-238)
 void Context::preprocess(uint32_t seed) {
     activate();
@@ -333,8 +382,10 @@ void Context::preprocess(uint32_t seed) {
     if (!have_points_) {
         if (cfg_.use_poisson_point_finder)
             find_poisson_points(seed);
-        else
+        else if (cfg_.tessellate_on_host)
             tessellate_surface_points(scene_, min_dist_, cfg_.incenter != 0, points_, 0, host_bump_views().data());
+        else
+            tessellate_on_gpu();
     }
     const int n = (int)points_.size();
     if (n == 0) {

@@ -3,6 +3,7 @@
 #include "scene.h"
 
 #include "geom.h"
+#include "tessellate.h"
 #include "texture.h"
 
 #include <algorithm>
@@ -186,80 +187,7 @@ void build_bvh(SceneData &s) {
 }
 
 // ------------------------------------------------------------------------------- tessellation
-namespace {
-
-struct BC {
-    float b0, b1, b2;
-};
-const BC kCentroid = {1.f / 3.f, 1.f / 3.f, 1.f / 3.f};  // trianglemesh.cpp:185
-
-inline BC bc_lerp(float t, BC a, BC b) {  // BarycentricCoordinate::Lerp
-    return BC{lerpf_t(t, a.b0, b.b0), lerpf_t(t, a.b1, b.b1), lerpf_t(t, a.b2, b.b2)};
-}
-inline BC bc_eval(BC s, BC a, BC b, BC c) {  // BarycentricCoordinate::Evaluate(BC, BC, BC)
-    return BC{s.b0 * a.b0 + s.b1 * b.b0 + s.b2 * c.b0, s.b0 * a.b1 + s.b1 * b.b1 + s.b2 * c.b1,
-              s.b0 * a.b2 + s.b1 * b.b2 + s.b2 * c.b2};
-}
-inline V3 bc_point(BC s, V3 a, V3 b, V3 c) {  // BarycentricCoordinate::Evaluate(Point x3)
-    return (a * s.b0 + b * s.b1) + c * s.b2;
-}
-
-template <class Shader>
-void matching(BC b0I, BC b1I, int segsI, BC b0O, BC b1O, int segsO, Shader &shader) {  // :321-351
-    int ip = 0, op = 0;
-    while (ip < segsI || op < segsO) {
-        const BC bIn = segsI ? bc_lerp((float)ip / segsI, b0I, b1I) : b0I;
-        const BC bOut = bc_lerp((float)op / segsO, b0O, b1O);
-        const float sIn = (ip < segsI) ? fabsf((float)(ip + 1) + 1.f - (float)op / segsO * (segsI + 2)) : INFINITY;
-        const float sOut = (op < segsO) ? fabsf((float)ip + 1.f - (float)(op + 1) / segsO * (segsI + 2)) : INFINITY;
-        if (sIn < sOut) {
-            shader(bc_lerp((float)(ip + 1) / segsI, b0I, b1I), bIn, bOut);
-            ip++;
-        } else {
-            shader(bIn, bOut, bc_lerp((float)(op + 1) / segsO, b0O, b1O));
-            op++;
-        }
-    }
-}
-
-template <class Shader>
-void tessellator(float tfe0, float tfe1, float tfe2, float tfc, Shader &shader) {  // :265-318
-    const int e0 = std::max((int)ceilf(tfe0), 1), e1 = std::max((int)ceilf(tfe1), 1),
-              e2 = std::max((int)ceilf(tfe2), 1);
-    int ic = std::max((int)ceilf(tfc), 1);
-    if (e0 > 1 || e1 > 1 || e2 > 1) ic = std::max(ic, 2);
-    const BC b0{1.f, 0.f, 0.f}, b1{0.f, 1.f, 0.f}, b2{0.f, 0.f, 1.f}, bc = kCentroid;
-    const int rings = (ic + 1) / 2;
-    for (int r = 0; r < rings - 1; ++r) {
-        const int edgeInner = ic - (rings - r) * 2;
-        const BC o0 = bc_lerp((float)(r + 1) / rings, bc, b0), o1 = bc_lerp((float)(r + 1) / rings, bc, b1),
-                 o2 = bc_lerp((float)(r + 1) / rings, bc, b2);
-        if (edgeInner >= 0) {
-            const int edgeOuter = edgeInner + 2;
-            const BC i0 = bc_lerp((float)r / rings, bc, b0), i1 = bc_lerp((float)r / rings, bc, b1),
-                     i2 = bc_lerp((float)r / rings, bc, b2);
-            matching(i0, i1, edgeInner, o0, o1, edgeOuter, shader);
-            matching(i1, i2, edgeInner, o1, o2, edgeOuter, shader);
-            matching(i2, i0, edgeInner, o2, o0, edgeOuter, shader);
-        } else {
-            shader(o0, o1, o2);
-        }
-    }
-    const int edgeInner = ic - 2;
-    if (edgeInner >= 0) {
-        const float t = (float)(rings - 1) / rings;
-        const BC i0 = bc_lerp(t, bc, b0), i1 = bc_lerp(t, bc, b1), i2 = bc_lerp(t, bc, b2);
-        matching(i0, i1, edgeInner, b0, b1, e2, shader);
-        matching(i1, i2, edgeInner, b1, b2, e0, shader);
-        matching(i2, i0, edgeInner, b2, b0, e1, shader);
-    } else {
-        shader(b0, b1, b2);
-    }
-}
-
-inline V3 ld3(const std::vector<float> &a, int i) { return V3{a[3 * (size_t)i], a[3 * (size_t)i + 1], a[3 * (size_t)i + 2]}; }
-
-}  // namespace
+// (the per-triangle code is tessellate.h, shared with the GPU build)
 
 MeshView mesh_view(const Mesh &m) {
     return MeshView{m.P.data(), m.N.empty() ? nullptr : m.N.data(), m.S.empty() ? nullptr : m.S.data(),
@@ -287,45 +215,12 @@ void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter
             const Mesh &m = s.meshes[job.mesh];
             const MeshView mv = mesh_view(m);
             for (int t = job.t0; t < job.t1; ++t) {
-                const V3 v0 = ld3(m.P, m.idx[3 * t]), v1 = ld3(m.P, m.idx[3 * t + 1]), v2 = ld3(m.P, m.idx[3 * t + 2]);
-                const float le0 = length(v1 - v2), le1 = length(v2 - v0), le2 = length(v0 - v1);
-                float tfe0 = le0 / min_dist * 0.8f, tfe1 = le1 / min_dist * 0.8f, tfe2 = le2 / min_dist * 0.8f;
-                const float tfc = floorf((tfe0 + tfe1 + tfe2) / 3.f + .5f);
-                tfe0 = floorf(tfe0 + .5f);
-                tfe1 = floorf(tfe1 + .5f);
-                tfe2 = floorf(tfe2 + .5f);
+                const TessTri tr = tess_tri(mv, t, min_dist);
+                const TexView *bt = bump ? bump[m.material] : nullptr;
                 auto shader = [&](BC a, BC b, BC c) {
-                    const V3 s0 = bc_point(a, v0, v1, v2), s1 = bc_point(b, v0, v1, v2), s2 = bc_point(c, v0, v1, v2);
-                    BC bc;
-                    if (!incenter) {
-                        bc = bc_eval(kCentroid, a, b, c);
-                    } else {
-                        const float l0 = length(s1 - s2), l1 = length(s2 - s0), l2 = length(s0 - s1);
-                        const BC bic{l0 / (l0 + l1 + l2), l1 / (l0 + l1 + l2), l2 / (l0 + l1 + l2)};
-                        bc = bc_eval(bic, a, b, c);
-                    }
-                    SurfacePoint sp;
-                    const V3 p = bc_point(bc, v0, v1, v2);
-                    sp.p[0] = p.x; sp.p[1] = p.y; sp.p[2] = p.z;
-                    // GetDifferentialGeometries(bc) -> dgGeom, dgShading (no differentials); Bump with
-                    // no map copies dgShading (material.cpp:107-114)
-                    const ShadingFrame fr = tri_shading(mv, t, p, bc.b0, bc.b1, bc.b2);
-                    sp.u = fr.u;
-                    sp.v = fr.v;
-                    V3 n = fr.nn;
-                    const TexView *bt = bump ? bump[m.material] : nullptr;
-                    if (bt) {
-                        const UVDiff g{fr.u, fr.v, 0.f, 0.f, 0.f, 0.f};
-                        V3 dpdu_b;
-                        bump_frame(*bt, g, fr.ss, fr.ts, fr.dndu, fr.dndv, fr.nn, fr.ng, mv.flip, dpdu_b, n);
-                    }
-                    sp.n[0] = n.x; sp.n[1] = n.y; sp.n[2] = n.z;
-                    sp.material = m.material;
-                    sp.area = .5f * length(cross(s1 - s0, s2 - s0));
-                    sp.ray_eps = min_dist / 10.f;
-                    job.pts.push_back(sp);
+                    job.pts.push_back(tess_point(mv, t, tr, a, b, c, incenter, bt, m.material, min_dist));
                 };
-                tessellator(tfe0, tfe1, tfe2, tfc, shader);
+                tessellator(tr.tfe0, tr.tfe1, tr.tfe2, tr.tfc, shader);
             }
         }
     };

@@ -43,7 +43,7 @@ class Config(C.Structure):
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
                 ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int), ("sampler", C.c_int),
                 ("replay_cores", C.c_int), ("octree_on_host", C.c_int), ("mo_band_dealing", C.c_int),
-                ("mo_work_stealing", C.c_int), ("mo_near_field", C.c_int)]
+                ("mo_work_stealing", C.c_int), ("mo_near_field", C.c_int), ("tessellate_on_host", C.c_int)]
 
 SAMPLER_HASH, SAMPLER_REFERENCE = 0, 1
 
