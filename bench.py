@@ -2,15 +2,14 @@
 
 A step = the pixel loop of one skin.pbrt frame (SamplerRenderer::Render's task loop,
 samplerrenderer.cpp:191-217): every camera sample is traced, shaded (direct lighting + the
-Mo() octree gather) and splatted into the film; the film tiles of every rank reach rank 0
-through one RCCL gather per step.
+Mo() octree gather) and splatted into the film; at N > 1 the film tiles of every rank
+reach rank 0 through one RCCL gather per step.
 
 * Every N (default): config C2, skin.pbrt 1024x1024 at 64 spp -- BASELINE.json's metric is quoted on
   it "@ 1/2/4/8 MI355X", so `value` at every N is the same workload and the driver's per-N
-  efficiency compares like with like. At N > 1 a step renders N C2 frames (one frame's work per GPU:
-  weak scaling) whose 128x128 tiles are dealt over the ranks by estimated cost (mpss_tile_costs:
-  camera rays through the pixel centres that hit skin; the deal is computed identically on every
-  rank, mpss/tiles.py deal_balanced), then gathered on rank 0 by one RCCL gather per step.
+  efficiency compares like with like. At N > 1 a step renders N independent C2 frames, one whole
+  frame per GPU (seed + rank; weak scaling: no tile dealing, no load balancing), gathered on rank 0
+  by one RCCL gather per step. At N = 1 there is no process group and no gather.
 * N > 1 also reports, as `secondary.c3_strong`, north_star's tile scaling of ONE frame: config C3
   (2048x2048, 256 spp) split over the N GPUs as cost-dealt 64x64 tiles (strong scaling).
 * --config c3 / c5 select BASELINE.json's other configurations explicitly (their own scaling).
@@ -87,7 +86,10 @@ def parse(argv=None):
     ap.add_argument("--tile", type=int, default=None, help="tile size (default 128; 64 for c3 on several GPUs)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--batch-log2", type=int, default=None,
-                    help="camera samples per render batch, log2 (mpss_config.max_batch_samples; default 2^24)")
+                    help="camera samples per render batch, log2 (mpss_config.max_batch_samples; default 2^26)")
+    ap.add_argument("--common-grid", type=int, choices=(0, 1), default=1,
+                    help="mpss_config.mo_common_grid: 1 (default) the Mo() gather's far field from the band groups' "
+                         "resampled common-grid tables; 0 the per-band tables")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 strong-scaling figure at N > 1")
@@ -136,6 +138,7 @@ def build_scene(a, label_cfg, local):
         sc.meshes = [pbrtscene.subdivide_mesh(me, subdiv) for me in sc.meshes]
     t0 = time.perf_counter()
     kw = {} if a.batch_log2 is None else {"max_batch_samples": 1 << a.batch_log2}
+    kw["mo_common_grid"] = a.common_grid
     ctx = pbrtscene.build_context(sc, device=local, **kw)
     t_mat = time.perf_counter() - t0
     if pts is not None:
@@ -342,10 +345,11 @@ def main(a):
                 "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh%s)" % (", subdivided" if subdiv else ""),
-                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles%s, RCCL film gather"
+                "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles%s%s"
                            % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T,
-                              ", a whole frame per GPU" if frames == world and world > 1 else
-                              (" dealt by cost" if world > 1 else "")),
+                              ", independent whole frames, one per GPU" if frames == world and world > 1 else
+                              (" dealt by cost" if world > 1 else ""),
+                              ", one RCCL film gather per step" if world > 1 else ""),
                            "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3), "tile_deal_s": round(t_deal, 3),
@@ -362,6 +366,9 @@ def main(a):
                            "mo_lookup_near_fraction": [round(x / max(1, cnt["mo_lookups"]), 4)
                                                        for x in cnt["mo_lookups_near"]],
                            "mo_wave_iters": {"node": cnt["mo_wave_node_iters"], "point": cnt["mo_wave_point_iters"]},
+                           "mo_common_grid": bool(ctx.gather_info(0)["common_grid"]) if sc.materials else False,
+                           "mo_lane_records": {"rows": cnt["mo_row_lane_records"], "lds": cnt["mo_lds_lane_records"],
+                                                  "tables": cnt["mo_table_lane_records"]},
                            "mo_visits": {"node": cnt["mo_nodes"], "point": cnt["mo_points"],
                                          "lookups_in_profile": cnt["mo_lookups"]}},
                 "roofline": roofline, "cpu_baseline": cpu}

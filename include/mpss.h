@@ -95,7 +95,8 @@ typedef struct {
     int octree_on_host;        /* 1: build the irradiance octree on the host (serial Insert in point
                                   order, octree.cpp); 0 (default): level-synchronous build on the GPU
                                   (octree_gpu.hip), the same tree bit for bit */
-    /* Choices of the spectrally sharded gather (exact_mo = 0). None changes a result bit. */
+    /* Choices of the spectrally sharded gather (exact_mo = 0). None of these three changes a result bit
+       (mo_common_grid, below, does within its stated bound). */
     int mo_band_dealing;       /* 0 (default): the 30 bands dealt into 8 groups of adjacent profile
                                   reach; 1: snake rounds (every group one of the 8 longest reaches) */
     int mo_work_stealing;      /* 1 (default): a workgroup whose band group runs dry moves on to the
@@ -105,6 +106,15 @@ typedef struct {
     int tessellate_on_host;    /* 1: Preprocess tessellates on the host (threads over triangles,
                                   scene.cpp); 0 (default): one GPU thread per triangle (render.hip
                                   tess_kernel), the same points bit for bit (tessellate.h) */
+    int mo_common_grid;        /* 1 (default): the sharded gather (mo_near_field 10236) reads a band
+                                  group's lookups past the exact LDS near field, as far as the
+                                  resampling stays within 2e-6 of each band's own value (measured at
+                                  every band knot when the material is added), from ONE table of the
+                                  group's bands resampled onto its coarsest d^2 grid: two 16-byte loads
+                                  per lookup instead of four 8-byte lerp pairs; farther lookups read the
+                                  bands' own tables. Results differ from the per-band gather by at most
+                                  that relative error per term (mpss_get_gather_info). 0: per-band
+                                  tables everywhere (bit-identical to the packet kernel) */
 } mpss_config;
 
 enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };
@@ -159,6 +169,11 @@ int mpss_add_dipole_material(mpss_ctx *ctx, const float *sigma_a, const float *s
 /* Query sizes first with NULL buffers: *length and *n_rho are always written. */
 int mpss_get_material_tables(mpss_ctx *ctx, uint32_t material_id, float *rd_table, uint32_t *length, float *rcp,
                              float *rho_hd, uint32_t *n_rho, float *total_reflectance);
+/* How the sharded gather evaluates material `id` (mpss_config.mo_common_grid): *common_grid = 1 when
+ * its far field is read from the resampled group tables, 0 for per-band tables (or a material the
+ * sharded gather does not run: dipole, rgbprofile). rel_err / l1_err (nullable, 30 floats): the
+ * measured resampling error per band (see mo_common_grid), 0 without a common grid. */
+int mpss_get_gather_info(mpss_ctx *ctx, uint32_t id, int *common_grid, float *rel_err, float *l1_err);
 
 /* Texture "imagemap" (CreateImageSpectrumTexture / CreateImageFloatTexture, textures/imagemap.cpp:
  * 110-180) with the default "uv" mapping (UVMapping2D, core/texture.cpp:88-98). texels = the image
@@ -284,6 +299,10 @@ typedef struct {
     /* count_traversal: Rd table lookups inside the profile (lane x band), and how many of them
      * fall in the first 4096 / 8192 / 16384 entries of their band */
     int64_t mo_lookups, mo_lookups_near[3];
+    /* count_traversal with the common grid: lane-records (one record's lookups of one lane) read from
+     * the group rows (two 16-byte loads), from the LDS near field, from the bands' own tables (four
+     * 8-byte loads) */
+    int64_t mo_row_lane_records, mo_lds_lane_records, mo_table_lane_records;
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal (0, 1 or 2, as mpss_config) after creation
@@ -340,6 +359,17 @@ int mpss_host_dipole_rd(const float *sigma_a, const float *sigmap_s, float eta, 
 /* rho_hd table (n entries, sqrt_samples^2 samples each) and rho_hh. */
 int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, int sqrt_samples, float *hd,
                         float *hh);
+/* The common grid the sharded gather builds for a profile (mpss_config.mo_common_grid), on the host:
+ * table [30][L], rcp [30]; snake as mpss_config.mo_band_dealing. Outputs (each nullable): rows
+ * [n_rows][8] (the groups' pair rows: group g's row for u is row0[g] + u - ubase[g], holding
+ * R_0(u), R_0(u+1), ..., R_3(u), R_3(u+1)); *n_rows (call with rows NULL to size it); bands [8][4]
+ * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim [8]
+ * (lanes with u < u0lim read the exact LDS near field, u0lim <= u < u1lim the rows, u >= u1lim the
+ * bands' own tables); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over
+ * the knots each band reads from the rows); *ok = 1 when some group has rows. */
+int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
+                          int32_t *bands, float *rg, float *u0lim, float *u1lim, uint32_t *row0, uint32_t *ubase,
+                          float *rel_err, float *l1_err, int *ok);
 /* Octree build + pre-order export (sizes first with NULL outputs). */
 int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
                             uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,

@@ -14,6 +14,8 @@ Context::Context(const mpss_config &cfg) : cfg_(cfg) {
                                           " out of range (" + std::to_string(ndev) + " HIP devices)");
     if (cfg.mo_near_field != 10236 && cfg.mo_near_field != 5088)
         throw Error(MPSS_ERR_INVALID, "mpss_create: mo_near_field must be 10236 or 5088");
+    if (cfg.mo_common_grid != 0 && cfg.mo_common_grid != 1)
+        throw Error(MPSS_ERR_INVALID, "mpss_create: mo_common_grid must be 0 or 1");
     if (cfg.mo_band_dealing != 0 && cfg.mo_band_dealing != 1)
         throw Error(MPSS_ERR_INVALID, "mpss_create: mo_band_dealing must be 0 or 1");
     max_error_ = cfg.max_error;
@@ -68,21 +70,25 @@ RenderWorkspace *Context::acquire_ws() {
 // at most kMaxIdleWorkspaces: a burst of concurrent callers does not pin its peak memory (a full C2
 // batch workspace is several GB) for the context's lifetime; the oldest idle one is freed first.
 constexpr size_t kMaxIdleWorkspaces = 4;
-void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) {
+hipError_t Context::release_ws_nothrow(RenderWorkspace *ws, hipStream_t stream) noexcept {
     const hipError_t e = hipEventRecord(ws->done, stream);
     ws->pending = e == hipSuccess;
     std::unique_ptr<RenderWorkspace> drop;
-    {
+    try {
         std::lock_guard<std::mutex> g(mu_);
         ws_free_.emplace_back(ws);
         if (ws_free_.size() > kMaxIdleWorkspaces) {
             drop = std::move(ws_free_.front());
             ws_free_.erase(ws_free_.begin());
         }
+    } catch (...) {  // the pool could not take it back: free it here
+        if (!drop) drop.reset(ws);
     }
     drop.reset();  // waits for its last kernels, outside the lock
-    MPSS_HIP(e);
+    return e;
 }
+
+void Context::release_ws(RenderWorkspace *ws, hipStream_t stream) { MPSS_HIP(release_ws_nothrow(ws, stream)); }
 
 // mu_ held (by the caller's lock on it): wait out every in-flight render_tiles / mo_batch, then
 // their kernels, before device state they read is replaced.
@@ -131,10 +137,7 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         }
         ++inflight_;  // until the kernels are queued (an octree rebuild waits for it)
     }
-    struct Done {
-        Context *c;
-        ~Done() { c->end_inflight(); }
-    } done{this};
+    InflightGuard guard{this, ws, stream};
     if (mode == -1) {
         launch_mo_dipole(dev_octree_, m->dev_dipole.ptr, max_error_, q, p_dev, out_dev, NB, counters_dev, stream);
         return;
@@ -153,19 +156,26 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
             ws->perm_n = need;
         }
         perm = ws->perm.ptr;
+        if (ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
     }
-    if (ws && ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
-    try {
-        launch_mo_gather(dev_octree_, layout, m->dev_profile, max_error_, q, p_dev, out_dev, NB, counters_dev,
-                         ws ? ws->work.ptr : nullptr, perm, mode, opts, stream);
-    } catch (...) {
-        if (ws) release_ws(ws, stream);
-        throw;
-    }
-    if (ws) release_ws(ws, stream);
+    launch_mo_gather(dev_octree_, layout, m->dev_profile, max_error_, q, p_dev, out_dev, NB, counters_dev,
+                     ws ? ws->work.ptr : nullptr, perm, mode, opts, stream);
+    guard.release();
 }
 
 void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }
+
+void Context::gather_info(uint32_t id, int *common_grid, float *rel_err, float *l1_err) const {
+    const Material &m = material(id);  // (takes mu_; materials are never replaced)
+    const bool band = !m.dipole && !m.rgb;
+    const bool on = band && cfg_.exact_mo == 0 && cfg_.mo_common_grid != 0 && cfg_.mo_near_field == 10236 &&
+                    m.dev_profile.cg.on;
+    *common_grid = on ? 1 : 0;
+    for (int c = 0; c < NB; ++c) {
+        if (rel_err) rel_err[c] = band ? m.dev_profile.cg_rel_err[c] : 0.f;
+        if (l1_err) l1_err[c] = band ? m.dev_profile.cg_l1_err[c] : 0.f;
+    }
+}
 
 // Material ids travel in 8 bits of the render path's per-sample records (render.h REC_MAT_SHIFT).
 constexpr size_t kMaxMaterials = 256;

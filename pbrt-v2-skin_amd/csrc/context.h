@@ -95,6 +95,7 @@ public:
     // the single-dipole Rd of the dipolesubsurface integrator (dipole.h); usable with mo_batch
     uint32_t add_dipole_material(const float *sigma_a, const float *sigmap_s, float eta);
     const Material &material(uint32_t id) const;
+    void gather_info(uint32_t id, int *common_grid, float *rel_err, float *l1_err) const;
     void set_irradiance_points(int n, const float *p, const float *nrm, const float *E, const float *area);
     const DeviceOctree &octree() const;
     void export_octree(void *nodes, float *node_et, float *pt_hdr, float *pt_e, int32_t *pt_index);
@@ -107,6 +108,7 @@ public:
         o.near_field = cfg_.mo_near_field;
         o.steal = cfg_.mo_work_stealing != 0;
         o.count_noprune = cfg_.count_traversal == 2;
+        o.common_grid = cfg_.mo_common_grid != 0;
         return o;
     }
     const mpss_config &config() const { return cfg_; }
@@ -173,6 +175,24 @@ private:
     std::vector<std::unique_ptr<RenderWorkspace>> ws_free_;
     RenderWorkspace *acquire_ws();
     void release_ws(RenderWorkspace *ws, hipStream_t stream);
+    hipError_t release_ws_nothrow(RenderWorkspace *ws, hipStream_t stream) noexcept;  // for unwinding paths
+    // One in-flight call (inflight_ already counted under mu_): on every way out of the call, exceptions
+    // included, its workspace returns to the pool and the count drops (so quiesce_locked never waits
+    // for a call that has failed). mu_ must not be held when the guard dies.
+    struct InflightGuard {
+        Context *c;
+        RenderWorkspace *ws;
+        hipStream_t stream;
+        void release() {  // the normal path: hands the workspace back, throwing on a HIP error
+            RenderWorkspace *w = ws;
+            ws = nullptr;
+            if (w) c->release_ws(w, stream);
+        }
+        ~InflightGuard() {
+            if (ws) (void)c->release_ws_nothrow(ws, stream);
+            c->end_inflight();
+        }
+    };
     // every BSSRDF material's band layout exists on the device octree (mu_ held)
     void ensure_layouts();
     // p, nrm, E, area: host arrays; dp / dn / dE (nullable): the same on the device, when the caller

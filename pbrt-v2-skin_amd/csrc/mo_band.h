@@ -85,6 +85,35 @@ inline bool same_groups(const BandGroups &a, const BandGroups &b) {
     return true;
 }
 
+// The common grid of a band group (mpss_config.mo_common_grid; DeviceProfile::build_common): a
+// lookup of all <= 4 bands of the group past their LDS near fields from ONE interleaved table. The
+// group's tables are resampled onto the grid of its longest-reach band (rg = its rcpDsqSpacing, for
+// which the resampling is the identity), u = d2 * rg, and stored as 32-byte pair rows
+// {R_0(u), R_0(u+1), R_1(u), R_1(u+1)}, {R_2(u), R_2(u+1), R_3(u), R_3(u+1)}: a lookup is two 16-byte
+// loads from one 32-byte-aligned sector per lane instead of four 8-byte lerp pairs from four
+// unrelated offsets (the gather is bound by the L2 request rate of these per-lane loads, DESIGN.md
+// §4). Each lane takes one of three paths by u:
+//   u < u0lim          every band's exact pair from its LDS near field (as the per-band gather);
+//   u0lim <= u < u1lim the group rows -- only where the resampling is accurate: build_common measures
+//                      the error at every band's own grid knots and ends the range before the first
+//                      knot off by more than kCgRelTol of the band's local value (the tables' far
+//                      tails carry the MPC resampler's kinks and float noise a coarser grid cannot
+//                      follow);
+//   u >= u1lim         every band's exact pair from its own table in HBM/L2 (as the per-band gather).
+struct CommonGrid {
+    const float4 *tab;          // pair rows, two float4 each; group g's row for u at 2 * (row0[g] + u - ubase[g])
+    uint32_t row0[kGroups];     // group g's first pair row
+    uint32_t ubase[kGroups];    // the u of that row
+    float rg[kGroups];          // the group's grid: u = d2 * rg (its smallest rcp)
+    float u0lim[kGroups];       // u < u0lim => every band's pair (s, s + 1) lies in its LDS near field
+    float u1lim[kGroups];       // u0lim <= u < u1lim: the pair rows (u1lim = u0lim: none)
+    float tau[kGroups][4];      // d2 >= tau <=> fl(d2 * rcp) >= L - 1: the band is past its profile end
+    uint32_t lrow[kGroups][4];  // float offset of slot j's near-field row in LDS (entries 0..klim_j)
+    int lcnt[kGroups][4];       // its length, klim_j + 1 floats (2 zeros for an empty slot)
+    float lds_r2[kGroups];      // a leaf with leaf_r2 below this is read from LDS only (0: never)
+    int on;                     // 1: some group has a non-empty row range (the three-path gather runs)
+};
+
 struct BandTree {
     const NodeHdr *__restrict__ nodes;
     const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
@@ -97,6 +126,7 @@ struct BandTree {
     const float *leaf_r2;                // DeviceOctree::leaf_r2 (nullable: no LDS-only point loops)
     int L, n_nodes, n_points;
     float max_error, prune_f;
+    CommonGrid cg;
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
@@ -160,7 +190,7 @@ __host__ __device__ constexpr int near_row() {
 // (how much a near-field copy of that many entries per band in LDS would absorb).
 // The fetch half: f per band and the four pair loads (issued, not consumed).
 template <bool COUNT, int KLDS>
-__device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float f[4], RdPair v[4], int hist[4]) {
+__device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float f[4], RdPair v[4], int hist[7]) {
     const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
     const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
     f[0] = f01.x;
@@ -214,11 +244,19 @@ __device__ __forceinline__ const float *in_vgprs(const float *p) {
     return (const float *)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
-// The combine half: lerp, the Mo() products and the running sums (one point or node).
+// The Mo() products and the running sums of one record's four Rd values: acc += (Rd * e) (* w).
 template <bool POINT>
-__device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
-                                                f2v acc[2]) {
-    float rd[4];
+__device__ __forceinline__ void band_rd_products(const float rd[4], const float e[4], float w, f2v acc[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f2v val = f2v{rd[2 * h], rd[2 * h + 1]} * f2v{e[2 * h], e[2 * h + 1]};
+        if (POINT) val = val * f2v{w, w};
+        acc[h] += val;
+    }
+}
+
+// sampleProfile's lerp of the four pairs: rd[j] = (1 - t) * T[s] + t * T[s + 1], t = fract(f[j]).
+__device__ __forceinline__ void band_rd_lerp(const float f[4], const RdPair v[4], float rd[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const float t = __builtin_amdgcn_fractf(f[j]);  // == f - (float)(uint)f for 0 <= f < 2^24
@@ -228,17 +266,152 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
         // into a v_pk_add_f32 fed by three v_mov_b32 swizzles)
         asm("v_add_f32 %0, %1, %2" : "=v"(rd[j]) : "v"(p.x), "v"(p.y));
     }
+}
+
+// The combine half: lerp, the Mo() products and the running sums (one point or node).
+template <bool POINT>
+__device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
+                                                f2v acc[2]) {
+    float rd[4];
+    band_rd_lerp(f, v, rd);
+    band_rd_products<POINT>(rd, e, w, acc);
+}
+
+// ---- the common-grid gather (CommonGrid) ----
+// The lane's (wave-uniform) view of its group's grid.
+struct CgLane {
+    const float4 *tab;    // the pair rows, indexed by u0 + rowoff
+    uint32_t rowoff;      // row0 - ubase (mod 2^32)
+    float rg, u0lim, u1lim;
+    float tau[4];
+    float tau_min;        // the group's first profile end
+    uint32_t lrow[4];     // LDS float offsets of the slots' exact near-field rows
+    uint32_t off[4];      // c_j * L: the bands' own tables (the u >= u1lim path)
+    uint32_t lm2;         // L - 2: the last pair of a band's table
+};
+
+// One record's lookups: band j's pair (T[s], T[s + 1]) -- or (R(u0), R(u0 + 1)) on the group rows --
+// in lanes {2j, 2j + 1} of the tuples p01 (bands 0, 1) and p23 (bands 2, 3), its lerp parameter in
+// f[j] (d2 * rcp_j, or u on the group rows). Every path writes the two 128-bit tuples whole (a row
+// half is one 16-byte load, an LDS or table pair fills one half), so the three paths share registers
+// without moves -- a move after a load would wait for it to return.
+// (Returned as a value: stores through a reference in the arms of the branch get sunk into one store
+// to a phi of their addresses, which keeps the record in scratch memory.)
+typedef float f4v __attribute__((ext_vector_type(4)));
+struct CgRec {
+    float f[4];
+    f4v p01, p23;
+};
+typedef const __attribute__((address_space(1))) float gfloat;
+typedef const __attribute__((address_space(1))) f4v gf4v;
+typedef const __attribute__((address_space(1))) f2v gf2v __attribute__((aligned(4)));
+
+template <bool COUNT>
+__device__ __forceinline__ void cg_count(const BandLane &b, const CgLane &c, float d2, int path, int hist[7]) {
+    if (!COUNT) return;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        f2v val = f2v{rd[2 * h], rd[2 * h + 1]} * f2v{e[2 * h], e[2 * h + 1]};
-        if (POINT) val = val * f2v{w, w};
-        acc[h] += val;
+    for (int j = 0; j < 4; ++j) {
+        if (!(b.rcp[j] > 0.f) || !(d2 < c.tau[j])) continue;
+        const uint32_t s = (uint32_t)(d2 * b.rcp[j]);
+        ++hist[0];
+        hist[1] += s < 4096u;
+        hist[2] += s < 8192u;
+        hist[3] += s < 16384u;
     }
+    hist[4 + path] += 1;  // 4: group rows, 5: LDS, 6: the bands' own tables
+}
+
+__device__ __forceinline__ f2v lds_pair(const BandLane &b, uint32_t k) {
+    lds_float *q = b.ltl + k;
+    return f2v{q[0], q[1]};
+}
+
+template <bool COUNT>
+__device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, const float *table, float d2,
+                                          int hist[7]) {
+    CgRec r;
+    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
+    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
+    r.f[0] = f01.x;
+    r.f[1] = f01.y;
+    r.f[2] = f23.x;
+    r.f[3] = f23.y;
+    const float u = d2 * c.rg;
+    // Three sequential masked steps, LDS first: a later step's loads may overwrite registers an
+    // earlier step's loads target only once those have returned, and LDS returns first (the
+    // opposite order made every LDS lane wait for the global loads). The two global steps write in
+    // issue order (vector memory returns in order), so the second does not wait for the first.
+    const int path = u < c.u0lim ? 1 : (u < c.u1lim ? 0 : 2);
+    // both global steps' addresses up front, so the allocator cannot place one step's address in
+    // registers the other step's loads are still filling (that would wait for those loads)
+    gf4v *row = (gf4v *)(c.tab + 2u * ((uint32_t)u + c.rowoff));
+    gfloat *tp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
+        tp[j] = (gfloat *)(table + c.off[j] + (sj < c.lm2 ? sj : c.lm2));
+    }
+    asm volatile("" : "+v"(row), "+v"(tp[0]), "+v"(tp[1]), "+v"(tp[2]), "+v"(tp[3]));
+    if (path == 1) {  // s_j < klim_j for every band: inside its LDS row
+        const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
+        const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
+        r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
+        r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+    }
+    // (keeps the LDS step ahead of the global ones: the compiler otherwise orders the three steps its
+    // own way and puts the LDS step last)
+    asm volatile("" : "+v"(r.p01), "+v"(r.p23)::"memory");
+    if (path == 0) {
+        r.p01 = row[0];
+        r.p23 = row[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.f[j] = u;
+    }
+    if (path == 2) {
+        const f2v q0 = *(gf2v *)tp[0], q1 = *(gf2v *)tp[1], q2 = *(gf2v *)tp[2], q3 = *(gf2v *)tp[3];
+        r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
+        r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+    }
+    cg_count<COUNT>(b, c, d2, path, hist);
+    return r;
+}
+
+// A record the caller has proven near for every lane (leaf_r2 < CommonGrid::lds_r2): LDS only.
+__device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &c, float d2) {
+    CgRec r;
+    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
+    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
+    r.f[0] = f01.x;
+    r.f[1] = f01.y;
+    r.f[2] = f23.x;
+    r.f[3] = f23.y;
+    const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
+    const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
+    r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
+    r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+    return r;
+}
+
+// sampleProfile's lerp with t = fract(f[j]) -- the LDS and own-table paths' exactly as the per-band
+// gather's, the group rows' on the group grid -- then its range test (multipole.cpp:65-66) as
+// d2 >= tau: only lanes off the LDS path can be past a band's end, and only at the group's reach, so
+// the test runs when some lane of the wave is past the group's first end.
+template <bool POINT>
+__device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
+                                           f2v acc[2]) {
+    float rd[4];
+    const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
+    band_rd_lerp(r.f, v, rd);
+    if (__builtin_amdgcn_ballot_w64(d2 >= c.tau_min) != 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
+    }
+    band_rd_products<POINT>(rd, e, w, acc);
 }
 
 template <bool POINT, bool COUNT, int KLDS>
 __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   int hist[4]) {
+                                                   int hist[7]) {
     float f[4];
     RdPair v[4];
     band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
@@ -263,10 +436,13 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 // A leaf's points are taken two at a time -- both points' eight pair loads issued before either's
 // terms are formed (the same terms, summed in the same order), so a wave waits out one L2 round
 // trip per two points.
-template <bool COUNT, int KLDS, bool VROWS>
+// CG: far lookups from the group's common grid (CommonGrid; the LDS holds the exact near field in
+// CommonGrid::lrow's per-slot rows), else every band from its own table (bit-identical to the packet
+// kernel).
+template <bool COUNT, int KLDS, bool VROWS, bool CG = false>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
-                                                 int hist[4], const float *lt) {
+                                                 int hist[7], const float *lt) {
     BandLane b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -282,10 +458,26 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     for (int j = 0; j < 4; ++j) b.tb[j] = VROWS ? in_vgprs(a.table + b.off[j]) : a.table + b.off[j];
     b.lt = lt;
     b.ltl = (lds_float *)lt;
+    CgLane cl;
+    if (CG) {
+        cl.tab = a.cg.tab;
+        cl.rowoff = a.cg.row0[grp] - a.cg.ubase[grp];
+        cl.rg = a.cg.rg[grp];
+        cl.u0lim = a.cg.u0lim[grp];
+        cl.u1lim = a.cg.u1lim[grp];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cl.tau[j] = a.cg.tau[grp][j];
+            cl.lrow[j] = a.cg.lrow[grp][j];
+            cl.off[j] = b.off[j];
+        }
+        cl.lm2 = (uint32_t)a.L - 2u;
+        cl.tau_min = fminf(fminf(cl.tau[0], cl.tau[1]), fminf(cl.tau[2], cl.tau[3]));
+    }
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     // a leaf whose points all lie within the near field of every band of the group, for any query that
     // opens it: leaf_r2 * rcp_max < klim (with a 1e-5 margin for the roundings of d2 and f)
-    const float lds_r2_lim = (float)b.klim / (a.grcp_max[grp] * 1.00001f);
+    const float lds_r2_lim = CG ? a.cg.lds_r2[grp] : (float)b.klim / (a.grcp_max[grp] * 1.00001f);
     const cptr<float> leaf_r2 = as_const(a.leaf_r2);
     // box2 * rcp_min >= prune_f as one compare: prune_f carries a 1e-4 margin over the profile end,
     // far above the rounding of the quotient (rcp_min 0: pruning off, INF)
@@ -326,7 +518,12 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
-                    band_rd_accumulate<false, COUNT, KLDS>(b, d2, e, 1.f, acc, hist);
+                    if (CG) {
+                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        cg_combine<false>(cl, r, d2, e, 1.f, acc);
+                    } else {
+                        band_rd_accumulate<false, COUNT, KLDS>(b, d2, e, 1.f, acc, hist);
+                    }
                 } else {
                     open = true;
                 }
@@ -350,11 +547,17 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float bx2 = px - pb.x, by2 = py - pb.y, bz2 = pz - pb.z;
                         const float d2a = ax * ax + ay * ay + az * az;
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
+                        const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
+                        if (CG) {
+                            const CgRec ra = cg_fetch_near(b, cl, d2a), rb = cg_fetch_near(b, cl, d2b);
+                            cg_combine<true>(cl, ra, d2a, e0, pa.w, lacc);
+                            cg_combine<true>(cl, rb, d2b, e1, pb.w, lacc);
+                            continue;
+                        }
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
                         band_rd_fetch_lds<KLDS>(b, d2a, fa, va);
                         band_rd_fetch_lds<KLDS>(b, d2b, fb, vb);
-                        const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         band_rd_combine<true>(fa, va, e0, pa.w, lacc);
                         band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
                     }
@@ -376,6 +579,14 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float bx2 = px - pb.x, by2 = py - pb.y, bz2 = pz - pb.z;
                         const float d2a = ax * ax + ay * ay + az * az;
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
+                        if (CG) {
+                            const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
+                            const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
+                            const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
+                            cg_combine<true>(cl, ra, d2a, e0, pa.w, lacc);
+                            cg_combine<true>(cl, rb, d2b, e1, pb.w, lacc);
+                            continue;
+                        }
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
                         band_rd_fetch<COUNT, KLDS>(b, d2a, fa, va, hist);
@@ -399,7 +610,12 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float d2 = ex * ex + ey * ey + ez * ez;
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
-                    band_rd_accumulate<true, COUNT, KLDS>(b, d2, e, ph.w, lacc, hist);
+                    if (CG) {
+                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        cg_combine<true>(cl, r, d2, e, ph.w, lacc);
+                    } else {
+                        band_rd_accumulate<true, COUNT, KLDS>(b, d2, e, ph.w, lacc, hist);
+                    }
                 }
                 acc[0] += lacc[0];
                 acc[1] += lacc[1];

@@ -55,9 +55,27 @@ struct DeviceProfile {
     int L = 0;
     float host_rcp[NB];
     BandGroups groups{};   // band -> XCD group assignment for this profile
+    // The common grid of each band group (mo_band.h CommonGrid), built by upload() for the 10236-entry
+    // LDS layout: ctab holds the groups' pair rows (two float4 per row); cg.on = 1 when some group has
+    // an accurate row range.
+    DevBuf<float4> ctab;
+    CommonGrid cg{};
+    float cg_rel_err[NB] = {};  // per band: max |R - T| / |T| over its knots read from the group rows
+    float cg_l1_err[NB] = {};   // per band: sum of |R - T| over those knots / sum of |T| over the table
     // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
     void upload(const float *table, int L, const float *rcp, bool snake = false);
+    void build_common(const float *table);  // (upload calls it; host table [NB][L])
 };
+
+// The common grid's bound on the resampling error of a lookup relative to the band's own value there
+// (DeviceProfile::build_common; the group rows cover only the range where every band is within it).
+constexpr double kCgRelTol = 2e-6;
+
+// The host half of DeviceProfile::build_common: the layout (cg, without tab), the pair rows h (two
+// float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group
+// has rows.
+bool build_common_grid(const float *tab, int L, const float *rcp, const BandGroups &groups, CommonGrid &cg,
+                       std::vector<float4> &h, float rel_err[NB], float l1_err[NB]);
 
 // Choices of the sharded gather (mpss_config.mo_near_field / mo_work_stealing; count_noprune =
 // mpss_config.count_traversal == 2, instrumented passes only).
@@ -65,6 +83,7 @@ struct GatherOpts {
     int near_field = 10236;
     bool steal = true;
     bool count_noprune = false;
+    bool common_grid = true;  // mpss_config.mo_common_grid (needs near_field 10236 and DeviceProfile::cg.on)
 };
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.
@@ -94,8 +113,10 @@ void launch_mo_rgb(const DeviceOctree &t, const float *table3, const float *rcp3
 // Traversal statistics of the sharded gather (count variant): per group g, counts[kStatStride*g + k]
 // for k = 0 node visits, 1 point visits (summed over queries), 2 wave node iterations, 3 wave
 // point iterations (summed over waves; 64 x these / the visits = 1 / lane efficiency), 4 table
-// lookups inside the profile (lane x band), 5..7 those at entries < 4096, 8192, 16384.
-constexpr int kStatStride = 8;
+// lookups inside the profile (lane x band), 5..7 those at entries < 4096, 8192, 16384; common grid
+// only: 8 lane-records read from the group rows (two 16-byte loads each), 9 from the LDS near field,
+// 10 from the bands' own tables (four 8-byte loads).
+constexpr int kStatStride = 11;
 
 // Spectrally sharded gather for the render path: queries4[i] = {p, *}, i < *count_dev (<= nq_max);
 // out4[i * 8 + g] = the 4 bands of group g (BandGroups::pos gives a band's float offset).

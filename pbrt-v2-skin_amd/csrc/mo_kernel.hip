@@ -29,6 +29,7 @@
 #include "mo_packet.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -373,7 +374,7 @@ constexpr int wave_kernel_wpe() {
     return KLDS > 5088 ? 4 : 8;
 }
 
-template <bool COUNT, int KLDS, bool STEAL>
+template <bool COUNT, int KLDS, bool STEAL, bool CG>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS>(), wave_kernel_wpe<KLDS>())))
 void mo_band_wave_kernel(BandArgs a) {
     constexpr int ROWF = near_row<KLDS>();
@@ -406,7 +407,15 @@ void mo_band_wave_kernel(BandArgs a) {
             // most once after it was found dry)
         }
     }
-    if (KLDS > 0) {
+    if (CG) {
+        // slot j's exact near field: entries 0..klim_j of its band (CommonGrid::lrow, lcnt = klim_j + 1)
+        for (int j = 0; j < 4; ++j) {
+            const int c = a.t.groups.band[grp][j];
+            const int o = (int)a.t.cg.lrow[grp][j];
+            const int n = a.t.cg.lcnt[grp][j];
+            for (int k = tid; k < n; k += 1024) lt[o + k] = c >= 0 ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+        }
+    } else if (KLDS > 0) {
         // entries 0..kmax of each band, kmax = min(KLDS, L - 2), zeros after (the last two floats of
         // a row are the zero pair of the lanes past the profile end)
         const int kmax = KLDS < a.t.L - 2 ? KLDS : a.t.L - 2;
@@ -426,8 +435,8 @@ void mo_band_wave_kernel(BandArgs a) {
         float px = 0.f, py = 0.f, pz = 0.f;
         const bool live = q >= 0 && band_query(a, q, px, py, pz);
         float acc[4];
-        int kn = 0, kp = 0, wn = 0, wp = 0, hist[4] = {0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, VROWS>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
+        int kn = 0, kp = 0, wn = 0, wp = 0, hist[7] = {0, 0, 0, 0, 0, 0, 0};
+        mo_band_traverse<COUNT, KLDS, VROWS && !CG, CG>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
         if (live) {
             if (a.out4) {
                 a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
@@ -452,7 +461,7 @@ void mo_band_wave_kernel(BandArgs a) {
                     atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
                 }
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 7; ++k)
                     if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
             }
         }
@@ -467,12 +476,12 @@ void mo_band_wave_kernel(BandArgs a) {
 // 41.2 ms per launch, profiles/r02j_variants.txt). opts.count_noprune (instrumented pass only):
 // the reach pruning off, so each group walks exactly the records the reference's Mo() recursion
 // reads (bench.py's SURVEY 8d algorithmic bytes).
-template <bool COUNT, int KLDS>
+template <bool COUNT, int KLDS, bool CG = false>
 void launch_wave(const BandArgs &a, dim3 grid, bool steal, hipStream_t stream) {
     if (steal)
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true>), grid, dim3(1024), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true, CG>), grid, dim3(1024), 0, stream, a);
     else
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false>), grid, dim3(1024), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false, CG>), grid, dim3(1024), 0, stream, a);
 }
 
 void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, const GatherOpts &opts,
@@ -493,7 +502,12 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, cons
     const bool wide = opts.near_field == 10236;
     const int cap = wide ? 32 : 64;  // resident workgroups per group: 1 or 2 per CU of an XCD
     const dim3 grid((unsigned)((chunks < cap ? chunks : cap) * kGroups));
-    if (count && wide)
+    const bool cg = wide && opts.common_grid && a.t.cg.on && a.t.cg.tab;
+    if (cg && count)
+        launch_wave<true, 10236, true>(a, grid, opts.steal, stream);
+    else if (cg)
+        launch_wave<false, 10236, true>(a, grid, opts.steal, stream);
+    else if (count && wide)
         launch_wave<true, 10236>(a, grid, opts.steal, stream);
     else if (count)
         launch_wave<true, 5088>(a, grid, opts.steal, stream);
@@ -532,6 +546,9 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
         }
     }
     bt.leaf_r2 = (t.leaf_r2.ptr && t.leaf_r2_error == max_error) ? t.leaf_r2.ptr : nullptr;
+    bt.cg = p.cg;
+    if (!bt.leaf_r2)
+        for (int g = 0; g < kGroups; ++g) bt.cg.lds_r2[g] = 0.f;
     bt.L = p.L;
     bt.n_nodes = t.n_nodes;
     bt.n_points = t.n_points;
@@ -619,6 +636,180 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
     for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
     groups = make_band_groups(rcp_, snake);
+    build_common(tab);
+}
+
+// The common grid (mo_band.h CommonGrid), on the host from the band tables:
+//   * group g's grid is its longest-reach band's own (rg = the smallest rcp), u = d2 * rg;
+//   * the LDS budget of the wide kernel (4 x 10239 floats) is split so that every slot's exact near
+//     field ends at the same distance: klim_j ~ K0 * rcp_j / rg, and u0lim = min_j klim_j rg / rcp_j
+//     (less a 2^-18 margin) guarantees s_j = fl(d2 rcp_j) < klim_j for every lane with u < u0lim;
+//   * R_j(u) = band j's lerp at f = u * rcp_j / rg in double (its last segment continued one row past
+//     its end, 0 after); on the group rows a lane computes (1 - t) R_j(u0) + t R_j(u0 + 1);
+//   * the row range: the far path reads R where the band gather reads T, both piecewise linear, so the
+//     largest error lies on a knot of one of the two grids, and at the group grid's knots R is T's own
+//     lerp; every band knot s >= u0lim rcp_j / rg - 1 is compared (R's lerp at u = s rg / rcp_j against
+//     T[s]), and the rows end one cell before the first knot whose error exceeds kCgRelTol of |T[s]|
+//     (unfloored: a zero or a sign change ends it) -- past it every lookup reads the exact tables;
+//   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
+//   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
+constexpr int kCgMaxRows = 65536;
+
+bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
+                       std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB]) {
+    cg = CommonGrid{};
+    h.clear();
+    for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
+    constexpr int kLdsFloats = 4 * near_row<10236>();
+    if (L < 4) return false;
+    for (int c = 0; c < NB; ++c)
+        if (!(host_rcp[c] > 0.f) || !std::isfinite(host_rcp[c])) return false;  // no uniform grid to resample
+    bool any = false;
+    for (int g = 0; g < kGroups; ++g) {
+        float rg = INFINITY;
+        int nfull = 0;
+        for (int j = 0; j < 4; ++j)
+            if (groups.band[g][j] >= 0) {
+                rg = std::min(rg, host_rcp[groups.band[g][j]]);
+                ++nfull;
+            }
+        cg.row0[g] = (uint32_t)(h.size() / 2);
+        if (nfull == 0) {  // an unused group: no wave ever walks it
+            for (int j = 0; j < 4; ++j) {
+                cg.lrow[g][j] = (uint32_t)(2 * j);
+                cg.lcnt[g][j] = 2;
+            }
+            continue;
+        }
+        double r[4] = {0.0, 0.0, 0.0, 0.0}, rsum = 0.0;
+        for (int j = 0; j < 4; ++j)
+            if (groups.band[g][j] >= 0) {
+                r[j] = (double)host_rcp[groups.band[g][j]] / (double)rg;
+                rsum += r[j];
+            }
+        // near-field split: sum_j (klim_j + 1) <= kLdsFloats (empty slots: 2 zero floats)
+        int K0 = (int)std::floor((kLdsFloats - 3.0 * nfull - 2.0 * (4 - nfull) - 8.0) / rsum);
+        int klim[4], total;
+        for (;;) {
+            total = 0;
+            for (int j = 0; j < 4; ++j) {
+                if (groups.band[g][j] < 0) {
+                    klim[j] = 1;
+                } else {
+                    const double want = std::ceil((double)K0 * r[j] * (1.0 + 1e-6)) + 1.0;
+                    klim[j] = (int)std::min<double>(want, (double)(L - 2));
+                }
+                total += klim[j] + 1;
+            }
+            if (total <= kLdsFloats || K0 <= 1) break;
+            --K0;
+        }
+        if (total > kLdsFloats) return false;
+        uint32_t off = 0;
+        double u0 = INFINITY;
+        for (int j = 0; j < 4; ++j) {
+            cg.lrow[g][j] = off;
+            cg.lcnt[g][j] = klim[j] + 1;
+            off += (uint32_t)(klim[j] + 1);
+            if (groups.band[g][j] >= 0) u0 = std::min(u0, (double)klim[j] / r[j] * (1.0 - 0x1p-18));
+        }
+        float u0f = (float)u0;
+        if ((double)u0f > u0) u0f = std::nextafter(u0f, 0.f);
+        cg.u0lim[g] = u0f;
+        cg.rg[g] = rg;
+        // a leaf is LDS-only when every lane's u < u0lim: leaf_r2 * rg below u0lim, with a 1e-5 margin
+        // for the rounding of the lanes' d2 (as the band gather's lds_r2_lim)
+        cg.lds_r2[g] = (float)((double)u0f / ((double)rg * 1.00001));
+        for (int j = 0; j < 4; ++j) {
+            const int c = groups.band[g][j];
+            if (c < 0) {
+                cg.tau[g][j] = INFINITY;  // (its sum is never stored)
+                continue;
+            }
+            const float rc = host_rcp[c];
+            const float endf = (float)(L - 1);
+            float x = (float)((double)(L - 1) / (double)rc);
+            auto past = [&](float d2) {
+                volatile float f = d2 * rc;  // the float product of sampleProfile (multipole.cpp:63)
+                return f >= endf;
+            };
+            while (x > 0.f && past(x)) x = std::nextafter(x, 0.f);
+            while (!past(x)) x = std::nextafter(x, INFINITY);
+            cg.tau[g][j] = x;
+        }
+        // R_j(u): band j on the group grid (double lerp, rounded once)
+        auto R = [&](int j, int64_t u) -> float {
+            const int c = groups.band[g][j];
+            if (c < 0 || u >= (int64_t)L) return 0.f;
+            const double f = (double)u * r[j];
+            if (f - r[j] > (double)(L - 1)) return 0.f;  // past the row after the band's end
+            const int sidx = std::min((int)std::floor(f), L - 2);
+            const double t = f - sidx;
+            const float *T = tab + (size_t)c * L;
+            return (float)((1.0 - t) * (double)T[sidx] + t * (double)T[sidx + 1]);
+        };
+        // the accurate range: the rows end a cell before the first band knot off by > kCgRelTol
+        const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor((double)u0f) - 1);
+        double ubad = (double)(L - 1);
+        for (int j = 0; j < 4; ++j) {
+            const int c = groups.band[g][j];
+            if (c < 0) continue;
+            const float *T = tab + (size_t)c * L;
+            double l1 = 0.0, emax = 0.0, esum = 0.0;
+            for (int k = 0; k < L; ++k) l1 += std::fabs(T[k]);
+            const int s_lo = std::max(0, (int)std::floor((double)u0f * r[j]) - 1);
+            for (int k = s_lo; k < L - 1; ++k) {
+                const double u = (double)k / r[j];
+                if (u >= ubad) break;
+                const int64_t ui = (int64_t)std::floor(u);
+                const double t = u - (double)ui;
+                const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
+                const double err = std::fabs(approx - (double)T[k]);
+                const bool sign_ok = T[k] != 0.f && (T[k] > 0.f) == (T[k + 1] > 0.f) && T[k + 1] != 0.f;
+                if (!sign_ok || err > kCgRelTol * std::fabs((double)T[k])) {
+                    ubad = std::min(ubad, u);
+                    break;
+                }
+                emax = std::max(emax, err / std::fabs((double)T[k]));
+                esum += err;
+            }
+            cg_rel_err[c] = (float)emax;
+            cg_l1_err[c] = (float)(l1 > 0.0 ? esum / l1 : 0.0);
+        }
+        int64_t u1 = (int64_t)std::floor(ubad) - 1;
+        u1 = std::min<int64_t>(u1, ubase + kCgMaxRows);
+        u1 = std::min<int64_t>(u1, (int64_t)L - 1);
+        if (u1 <= (int64_t)u0f + 1) {  // no accurate range: the exact tables past the near field
+            cg.ubase[g] = (uint32_t)ubase;
+            cg.u1lim[g] = u0f;
+            continue;
+        }
+        cg.ubase[g] = (uint32_t)ubase;
+        cg.u1lim[g] = (float)u1;  // lanes with u < u1 read rows u0 <= u1 - 1 (values R(u0), R(u0 + 1))
+        for (int64_t u = ubase; u < u1; ++u) {
+            float v[4][2];
+            for (int j = 0; j < 4; ++j) {
+                v[j][0] = R(j, u);
+                v[j][1] = R(j, u + 1);
+            }
+            h.push_back(make_float4(v[0][0], v[0][1], v[1][0], v[1][1]));
+            h.push_back(make_float4(v[2][0], v[2][1], v[3][0], v[3][1]));
+        }
+        any = true;
+    }
+    cg.on = any ? 1 : 0;
+    return any;
+}
+
+void DeviceProfile::build_common(const float *tab) {
+    ctab.release();
+    std::vector<float4> h;
+    if (!build_common_grid(tab, L, host_rcp, groups, cg, h, cg_rel_err, cg_l1_err)) {
+        cg.on = 0;  // the per-band tables stay in use
+        return;
+    }
+    ctab.upload(h.data(), h.size());
+    cg.tab = ctab.ptr;
 }
 
 namespace {
@@ -629,10 +820,18 @@ __global__ void leaf_r2_kernel(const NodeHdr *__restrict__ nodes, int n, float m
     float out = INFINITY;
     if (h.leaf_first >= 0 && h.sum_area > 0.f && max_error > 0.f && isfinite(h.px) && isfinite(h.py) &&
         isfinite(h.pz)) {
+        // A query opens the leaf only if |q - c| <= open (dw >= max_error) or q lies in the box. Every point
+        // lies in the box, so |q - p_i| <= open + (c's farthest box corner) or <= diag. The centroid c is
+        // luminance-weighted and need not lie in the box (mixed-sign E, or a zero weight sum leaving c at
+        // the origin), hence the farthest corner from c rather than the diagonal.
         const double dx = (double)h.bmaxx - h.bminx, dy = (double)h.bmaxy - h.bminy, dz = (double)h.bmaxz - h.bminz;
         const double diag = sqrt(dx * dx + dy * dy + dz * dz);
+        const double fx = fmax(fabs((double)h.px - h.bminx), fabs((double)h.px - h.bmaxx));
+        const double fy = fmax(fabs((double)h.py - h.bminy), fabs((double)h.py - h.bmaxy));
+        const double fz = fmax(fabs((double)h.pz - h.bminz), fabs((double)h.pz - h.bmaxz));
+        const double corner = sqrt(fx * fx + fy * fy + fz * fz);
         const double open = sqrt((double)h.sum_area / (double)max_error) * (1.0 + 1e-6);
-        const double R = (open > diag ? open : diag) + diag;
+        const double R = (open + corner > diag ? open + corner : diag);
         out = (float)(R * R * (1.0 + 1e-6));
     }
     r2[i] = out;

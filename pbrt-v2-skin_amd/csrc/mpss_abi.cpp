@@ -8,6 +8,7 @@
 #include "context.h"
 #include "material.h"
 #include "mc_profile.h"
+#include "mo_kernel.h"
 #include "spectral.h"
 
 using namespace mpss;
@@ -42,7 +43,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 9; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 10; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
                                           // 6: GPU octree build (octree_on_host), mpss_octree_export;
@@ -51,6 +52,8 @@ int mpss_abi_version(void) { return 9; }  // 2: poisson point finder, infinite l
                                           // 8: light spheres seen directly shaded (default matte),
                                           //    rebuilds wait for in-flight render / mo_batch calls;
                                           // 9: GPU tessellation (tessellate_on_host), size bounds
+                                          // 10: mo_common_grid, mpss_get_gather_info, common-grid
+                                          //     lane-record counts in mpss_render_stats
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -76,6 +79,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->mo_work_stealing = 1;
     c->mo_near_field = 10236;
     c->tessellate_on_host = 0;
+    c->mo_common_grid = 1;
 }
 
 int mpss_create(const mpss_config *cfg, mpss_ctx **out) {
@@ -172,6 +176,45 @@ int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len,
         if (rcp) memcpy(rcp, m.profile.rcp, sizeof(float) * NB);
         if (rho) memcpy(rho, m.rho.hd.data(), sizeof(float) * m.rho.hd.size());
         if (total) memcpy(total, m.profile.total_reflectance, sizeof(float) * NB);
+    });
+}
+
+int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
+                          int32_t *bands, float *rg, float *u0lim, float *u1lim, uint32_t *row0, uint32_t *ubase,
+                          float *rel_err, float *l1_err, int *ok) {
+    return guarded([&] {
+        require(table && rcp && ok, "mpss_host_common_grid: null argument");
+        require(L >= 2 && L < (1u << 24), "mpss_host_common_grid: L out of range");
+        const BandGroups g = make_band_groups(rcp, snake != 0);
+        CommonGrid cg;
+        std::vector<float4> h;
+        float rel[NB], l1[NB];
+        *ok = build_common_grid(table, (int)L, rcp, g, cg, h, rel, l1) ? 1 : 0;
+        if (n_rows) {
+            if (rows) require(*n_rows >= h.size() / 2, "mpss_host_common_grid: rows too small");
+            *n_rows = (uint32_t)(h.size() / 2);
+        }
+        if (rows) memcpy(rows, h.data(), sizeof(float4) * h.size());
+        for (int k = 0; k < kGroups; ++k) {
+            for (int j = 0; j < 4; ++j)
+                if (bands) bands[4 * k + j] = g.band[k][j];
+            if (rg) rg[k] = cg.rg[k];
+            if (u0lim) u0lim[k] = cg.u0lim[k];
+            if (u1lim) u1lim[k] = cg.u1lim[k];
+            if (row0) row0[k] = cg.row0[k];
+            if (ubase) ubase[k] = cg.ubase[k];
+        }
+        for (int c = 0; c < NB; ++c) {
+            if (rel_err) rel_err[c] = rel[c];
+            if (l1_err) l1_err[c] = l1[c];
+        }
+    });
+}
+
+int mpss_get_gather_info(mpss_ctx *c, uint32_t id, int *common_grid, float *rel_err, float *l1_err) {
+    return guarded([&] {
+        require(c && common_grid, "mpss_get_gather_info: null argument");
+        reinterpret_cast<Context *>(c)->gather_info(id, common_grid, rel_err, l1_err);
     });
 }
 

@@ -654,10 +654,11 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     RenderWorkspace *ws = acquire_ws();
     ++inflight_;  // until this call's kernels are queued (see quiesce_locked)
     lk.unlock();
+    InflightGuard guard{this, ws, stream};  // every way out: workspace back to the pool, inflight_ down
 
     std::vector<Timed> timed;
     int64_t n_samples = 0, n_sss = 0;
-    try {
+    {
         if (ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));
         // a workspace buffer is reallocated only once its previous user's kernels are done
         auto grow = [&](auto &buf, int64_t &have, int64_t want, size_t per) {
@@ -854,17 +855,12 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             if (counting) n_sss += nh_dev;
             pi = pe;
         }
-    } catch (...) {
-        release_ws(ws, stream);
-        end_inflight();
-        throw;
     }
-    release_ws(ws, stream);
-    lk.lock();
+    guard.release();
+    std::lock_guard<std::mutex> g(mu_);  // (released before the guard's end_inflight takes mu_)
     timed_.insert(timed_.end(), timed.begin(), timed.end());
     stats_.samples += n_samples;
     stats_.sss_samples += n_sss;
-    if (--inflight_ == 0) idle_.notify_all();
 }
 
 // Tile-cost probe (mpss_tile_costs): classes per pixel centre, summed per rectangle on the host.
@@ -946,6 +942,9 @@ mpss_render_stats Context::render_stats() {
             out.mo_wave_point_iters += (int64_t)c[kStatStride * g2 + 3];
             out.mo_lookups += (int64_t)c[kStatStride * g2 + 4];
             for (int k = 0; k < 3; ++k) out.mo_lookups_near[k] += (int64_t)c[kStatStride * g2 + 5 + k];
+            out.mo_row_lane_records += (int64_t)c[kStatStride * g2 + 8];
+            out.mo_lds_lane_records += (int64_t)c[kStatStride * g2 + 9];
+            out.mo_table_lane_records += (int64_t)c[kStatStride * g2 + 10];
         }
     }
     return out;

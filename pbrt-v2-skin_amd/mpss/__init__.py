@@ -43,7 +43,8 @@ class Config(C.Structure):
                 ("kernel_timing", C.c_int), ("count_traversal", C.c_int), ("profile_on_host", C.c_int),
                 ("max_batch_samples", C.c_int64), ("use_poisson_point_finder", C.c_int), ("sampler", C.c_int),
                 ("replay_cores", C.c_int), ("octree_on_host", C.c_int), ("mo_band_dealing", C.c_int),
-                ("mo_work_stealing", C.c_int), ("mo_near_field", C.c_int), ("tessellate_on_host", C.c_int)]
+                ("mo_work_stealing", C.c_int), ("mo_near_field", C.c_int), ("tessellate_on_host", C.c_int),
+                ("mo_common_grid", C.c_int)]
 
 SAMPLER_HASH, SAMPLER_REFERENCE = 0, 1
 
@@ -56,7 +57,8 @@ class RenderStats(C.Structure):
                 ("mo_nodes", C.c_int64), ("mo_points", C.c_int64), ("group_nodes", C.c_int64 * 8),
                 ("group_points", C.c_int64 * 8), ("group_bands", (C.c_int32 * 4) * 8), ("ms_direct", C.c_double),
                 ("n_direct", C.c_int64), ("mo_wave_node_iters", C.c_int64), ("mo_wave_point_iters", C.c_int64),
-                ("mo_lookups", C.c_int64), ("mo_lookups_near", C.c_int64 * 3)]
+                ("mo_lookups", C.c_int64), ("mo_lookups_near", C.c_int64 * 3), ("mo_row_lane_records", C.c_int64),
+                ("mo_lds_lane_records", C.c_int64), ("mo_table_lane_records", C.c_int64)]
 
 
 class LayeredSkin(C.Structure):
@@ -96,6 +98,7 @@ _sig("mpss_set_material_tables", C.c_int, [vp, f32p, u32, f32p, f32p, u32, vp, C
 _sig("mpss_add_dipole_material", C.c_int, [vp, f32p, f32p, C.c_float, u32p])
 _sig("mpss_host_dipole_rd", C.c_int, [f32p, f32p, C.c_float, u32, vp, vp, vp])
 _sig("mpss_get_material_tables", C.c_int, [vp, u32, vp, u32p, vp, vp, u32p, vp])
+_sig("mpss_get_gather_info", C.c_int, [vp, u32, C.POINTER(C.c_int), vp, vp])
 _sig("mpss_set_irradiance_points", C.c_int, [vp, u32, f32p, f32p, f32p, f32p])
 _sig("mpss_octree_info", C.c_int, [vp, u32p, u32p, u32p])
 _sig("mpss_octree_export", C.c_int, [vp, vp, vp, vp, vp, vp])
@@ -134,6 +137,7 @@ _sig("mpss_host_imagemap_lookup", C.c_int, [C.POINTER(Imagemap), u32, f32p, f32p
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
+_sig("mpss_host_common_grid", C.c_int, [f32p, u32, f32p, C.c_int, vp, u32p] + [vp] * 8 + [C.POINTER(C.c_int)])
 _sig("mpss_host_octree_export", C.c_int, [u32, f32p, f32p, f32p, f32p, u32p] + [vp] * 8)
 
 
@@ -303,6 +307,27 @@ def host_rho_table(roughness, eta, n=1025, sqrt_samples=256, double_ref_sslf=Fal
     return hd, hh.value
 
 
+def host_common_grid(table, rcp, snake=False):
+    """The sharded gather's common grid for a profile (mpss_host_common_grid): dict of rows
+    (n_rows, 8), bands (8, 4), rg, u0lim, u1lim, row0, ubase (8,), rel_err / l1_err (30,), ok."""
+    table = np.ascontiguousarray(table, np.float32)
+    rcp = np.ascontiguousarray(rcp, np.float32)
+    L = table.shape[1]
+    n = C.c_uint32(0)
+    nul = [None] * 8
+    ok = C.c_int()
+    check(_lib.mpss_host_common_grid(table, L, rcp, int(snake), None, C.byref(n), *nul, C.byref(ok)))
+    out = dict(rows=np.zeros((n.value, 8), np.float32), bands=np.zeros((8, 4), np.int32),
+               rg=np.zeros(8, np.float32), u0lim=np.zeros(8, np.float32), u1lim=np.zeros(8, np.float32),
+               row0=np.zeros(8, np.uint32), ubase=np.zeros(8, np.uint32), rel_err=np.zeros(NB, np.float32),
+               l1_err=np.zeros(NB, np.float32))
+    check(_lib.mpss_host_common_grid(table, L, rcp, int(snake), out["rows"].ctypes.data, C.byref(n),
+                                     *[out[k].ctypes.data for k in ("bands", "rg", "u0lim", "u1lim", "row0", "ubase",
+                                                                    "rel_err", "l1_err")], C.byref(ok)))
+    out["ok"] = bool(ok.value)
+    return out
+
+
 def host_octree_export(p, n, E, area):
     p, n, E, area = [np.ascontiguousarray(x, np.float32) for x in (p, n, E, area)]
     nn = C.c_uint32()
@@ -367,6 +392,14 @@ class Context:
         check(_lib.mpss_get_material_tables(self.h, mid, tab.ctypes.data, C.byref(L), rcp.ctypes.data,
                                             rho.ctypes.data, C.byref(nr), tot.ctypes.data))
         return tab, rcp, rho, tot
+
+    def gather_info(self, mid):
+        """mpss_get_gather_info: {common_grid: bool, rel_err: (30,), l1_err: (30,)}."""
+        on = C.c_int()
+        rel = np.zeros(NB, np.float32)
+        l1 = np.zeros(NB, np.float32)
+        check(_lib.mpss_get_gather_info(self.h, mid, C.byref(on), rel.ctypes.data, l1.ctypes.data))
+        return dict(common_grid=bool(on.value), rel_err=rel, l1_err=l1)
 
     def set_irradiance_points(self, p, n, E, area):
         p, n, E, area = [np.ascontiguousarray(x, np.float32) for x in (p, n, E, area)]

@@ -16,7 +16,7 @@ def test_library_exports_header_symbols(mpss):
 
 
 def test_abi_version_and_errors(mpss):
-    assert mpss.lib().mpss_abi_version() == 9
+    assert mpss.lib().mpss_abi_version() == 10
     # a null-argument call must fail with a message, not crash
     rc = mpss.lib().mpss_create(None, None)
     assert rc == -1
@@ -30,6 +30,7 @@ def test_defaults_match_reference_factories(mpss):
         (5, 0.05, 0.25, 0.5)
     # the sharded gather's choices (none changes a result bit; tests/test_mo_gpu.py)
     assert (c.mo_band_dealing, c.mo_work_stealing, c.mo_near_field) == (0, 1, 10236)
+    assert c.mo_common_grid == 1  # the far field from the resampled group tables (within its checked bound)
     assert (c.octree_on_host, c.tessellate_on_host, c.profile_on_host) == (0, 0, 0)  # Preprocess on the GPU
     m = mpss.default_skin()
     # CreateLayeredSkinMaterial, layeredskin.cpp:234-257

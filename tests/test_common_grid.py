@@ -1,0 +1,142 @@
+"""The common grid of the sharded Mo() gather (mpss_config.mo_common_grid; mo_band.h CommonGrid),
+host half, on the CPU: the LDS split, the resampled pair rows and the range they serve, against a
+numpy restatement of multipole.cpp:60-73's sampleProfile (every served knot within 2e-6 of the
+band's own value).
+
+The gather itself (LDS and own-table lanes bit-identical to the per-band gather, row lanes within
+the bound) is checked on the GPU by tests/test_mo_gpu.py and the image tests."""
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.npz")
+LDS_FLOATS = 4 * (10236 + 3)
+
+
+def _groups(rcp):
+    """make_band_groups (mo_band.h): bands by increasing rcp, runs of 4, 4, 4, 4, 4, 4, 3, 3."""
+    order = np.argsort(rcp, kind="stable")
+    return [list(order[i * 4:(i + 1) * 4]) for i in range(6)] + [list(order[24:27]), list(order[27:30])]
+
+
+def _band_at(T, f, L):
+    """Band lerp at fractional index f (double), the last segment continued one row past the end."""
+    s = np.minimum(np.floor(f).astype(np.int64), L - 2)
+    t = f - s
+    return (1.0 - t) * T[s] + t * T[s + 1]
+
+
+def _R(T, r, u, L):
+    """Band table T on a group grid of relative spacing r at integer u (build_common's R_j(u))."""
+    f = u * r
+    v = _band_at(T, f, L)
+    return np.where((f - r > L - 1) | (u >= L), 0.0, v)
+
+
+def _check_layout(tab, rcp, cg, tol=2e-6):
+    """Groups, the LDS split, the pair rows against numpy, and that every band knot the rows serve
+    is within tol of the band's own value (unfloored)."""
+    L = tab.shape[1]
+    T64 = tab.astype(np.float64)
+    for g, bands in enumerate(_groups(rcp)):
+        slots = cg["bands"][g]
+        assert sorted(b for b in slots if b >= 0) == sorted(int(b) for b in bands)
+        rg = np.float32(rcp[bands].min())
+        assert cg["rg"][g] == rg
+        r = np.array([np.float64(rcp[c]) / np.float64(rg) if c >= 0 else 0.0 for c in slots])
+        # every lane with u < u0lim has s_j < klim_j for every band: the split fits the LDS
+        need = sum(int(np.ceil(cg["u0lim"][g] * rj)) + 2 for rj in r if rj > 0)
+        assert 0 < need <= LDS_FLOATS
+        u0, u1, ub, r0 = cg["u0lim"][g], cg["u1lim"][g], int(cg["ubase"][g]), int(cg["row0"][g])
+        if u1 <= u0:
+            continue
+        assert ub == max(0, int(np.floor(u0)) - 1)
+        n = int(u1) - ub
+        rows = cg["rows"][r0:r0 + n].astype(np.float64)
+        assert len(rows) == n
+        u = np.arange(ub, ub + n, dtype=np.float64)
+        for j, c in enumerate(slots):
+            if c < 0:
+                assert np.all(rows[:, 2 * j:2 * j + 2] == 0)
+                continue
+            want0 = _R(T64[c], r[j], u, L).astype(np.float32)
+            want1 = _R(T64[c], r[j], u + 1, L).astype(np.float32)
+            np.testing.assert_array_equal(rows[:, 2 * j].astype(np.float32), want0)
+            np.testing.assert_array_equal(rows[:, 2 * j + 1].astype(np.float32), want1)
+            # the knots the rows serve: u in [u0lim, u1lim)
+            k = np.arange(int(np.floor(u0 * r[j])), L - 1)
+            uk = k / r[j]
+            sel = (uk >= u0) & (uk < u1)
+            k, uk = k[sel], uk[sel]
+            ui = np.floor(uk).astype(np.int64) - ub
+            t = uk - np.floor(uk)
+            approx = (1 - t) * rows[ui, 2 * j] + t * rows[ui, 2 * j + 1]
+            err = np.abs(approx - T64[c, k])
+            assert np.all(err <= tol * np.abs(T64[c, k]) * (1 + 1e-9)), (g, c, (err / np.abs(T64[c, k])).max())
+
+
+def test_common_grid_of_golden_profile(mpss):
+    """desiredlength 64 skin profile (tests/golden): layout and pair rows vs numpy, the served range
+    within the bound."""
+    z = np.load(GOLDEN)
+    tab, rcp = z["profile_64"], z["profile_64_rcp"]
+    cg = mpss.host_common_grid(tab, rcp)
+    _check_layout(tab, rcp, cg)
+    assert cg["rel_err"].max() <= 2e-6
+
+
+def test_common_grid_of_the_benched_skin_profile(mpss):
+    """C2's material (skin.pbrt, desiredlength 512): rows for 7 of the 8 groups, over more than one
+    doubling of distance past the near field for each."""
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"))
+    m = sc.materials[0]
+    kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo", "albedo_tex", "bump_tex")}
+    tab, rcp, _ = mpss.host_build_profile(*mpss.host_skin_layers(mpss.default_skin(**kw)), 512)
+    cg = mpss.host_common_grid(tab, rcp)
+    assert cg["ok"]
+    span = np.log2(np.maximum(cg["u1lim"], 1) / cg["u0lim"])
+    assert (span > 1.0).sum() >= 7, span
+    assert cg["rel_err"].max() <= 2e-6 and cg["l1_err"].max() <= 1e-8
+    assert len(cg["rows"]) <= 8 * 65536
+    _check_layout(tab, rcp, cg)
+
+
+def test_common_grid_of_a_rough_table(mpss):
+    """A table that is rough on the groups' grids: whatever rows are built serve only knots within
+    the bound (here none past the near field)."""
+    rng = np.random.default_rng(5)
+    L = 4096
+    x = np.arange(L) / L
+    tab = np.stack([np.exp(-x * (3 + c)) * (1 + 0.3 * rng.random(L)) for c in range(30)]).astype(np.float32)
+    rcp = ((L - 1) / np.linspace(0.01, 0.05, 30)).astype(np.float32)
+    cg = mpss.host_common_grid(tab, rcp)
+    _check_layout(tab, rcp, cg)
+    assert np.all(cg["u1lim"] - cg["u0lim"] < 64)
+
+
+def test_common_grid_equal_spacing_is_exact(mpss):
+    """Bands sharing one spacing: the group grid is every band's own, the rows are the tables."""
+    L = 30000
+    x = np.arange(L) / L
+    tab = np.stack([np.exp(-x * (4 + 0.2 * c)) for c in range(30)]).astype(np.float32)
+    rcp = np.full(30, (L - 1) / 0.004, np.float32)
+    cg = mpss.host_common_grid(tab, rcp)
+    assert cg["ok"] and cg["rel_err"].max() == 0
+    _check_layout(tab, rcp, cg, tol=0.0)
+    ub, r0 = int(cg["ubase"][0]), int(cg["row0"][0])
+    c = cg["bands"][0][0]
+    assert np.array_equal(cg["rows"][r0:r0 + 100, 0], tab[c, ub:ub + 100])
+
+
+@pytest.mark.parametrize("bad", ["zero_rcp", "short"])
+def test_common_grid_declines_degenerate_tables(mpss, bad):
+    L = 3 if bad == "short" else 100
+    tab = np.ones((30, L), np.float32)
+    rcp = np.full(30, 10.0, np.float32)
+    if bad == "zero_rcp":
+        rcp[3] = 0.0
+    cg = mpss.host_common_grid(tab, rcp)
+    assert not cg["ok"] and len(cg["rows"]) == 0

@@ -5,12 +5,15 @@
       profile and rho tables vs the oracle, irradiance on a 300k-point prefix (the sampler's
       random numbers depend only on the point's index, so a prefix is a valid subset), and two
       windows rendered by both: a 32x32 window on the cheek and a ragged 37x29 window across
-      the silhouette, with the image tolerance of test_render_parity_gpu.py.
-  C3  2048x2048 at 256 spp dealt over 8 ranks by cost (bench.py's multi-GPU deal): every rank's
-      tile set rendered on this GPU and reassembled is bitwise the single-call frame.
+      the silhouette, with the image tolerance of test_render_parity_gpu.py; and the WHOLE benched
+      frame (1024x1024 x 64 spp, every pixel) against the oracle on the host's CPUs.
+  C3  2048x2048 at 256 spp: a cheek window and a silhouette window at the config's own 256 spp vs
+      the oracle; dealt over 8 ranks by cost (bench.py's multi-GPU deal), every rank's tile set
+      rendered on this GPU and reassembled is bitwise the single-call frame.
   C4  scenes/mcprofile.pbrt's layers at 1e7 photons vs the oracle's random walk.
   C5  the 4.06 M-triangle subdivided head with the original tessellation as pointsfile: surface
-      irradiance on a prefix and a 32x32 cheek window at 4 spp against the oracle.
+      irradiance on a prefix and a 32x32 cheek window at the config's own 512 spp against the oracle
+      (at 512 spp a wave's 64 lanes are one pixel's samples: the gather's lane-coherent regime).
 """
 import os
 
@@ -113,6 +116,49 @@ def test_c2_window_parity(c2, where):
     assert (ref[..., 1] > 0).mean() > (0.9 if where == "cheek" else 0.2)
 
 
+def test_c2_full_frame_parity(c2):
+    """Every pixel of the benched C2 frame (skin.pbrt 1024x1024, 64 spp, hash sampler, production
+    sharded gather) vs the oracle's render of the same frame (multipolesubsurface.cpp:253-304 driven
+    by samplerrenderer.cpp:60-167's pixel loop), with tests/parity.py's unfloored 1e-4 relative L-inf."""
+    torch, sc, ctx, o = c2
+    if not getattr(o, "_octree_set", False):
+        o.set_octree(ctx.surface_points(), ctx.irradiance())
+        o._octree_set = True
+    got = _render(torch, ctx, sc.spp, 7, 0, sc.xres, 0, sc.yres)
+    ref = o.render_tile(sc.spp, 7, 0, sc.xres, 0, sc.yres, nthreads=NT)
+    st = parity.check_image(got, ref)
+    assert 0.03 < (ref[..., 1] > 0).mean() < 0.5  # the head covers ~5 % of the frame, lit background none
+    print("C2 full frame: relative L-inf %.3g over %d values" % (st["rel_linf"], st["values"]))
+
+
+@pytest.fixture(scope="module")
+def c3(mpss):
+    import torch
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=2048, yres=2048, spp=256)
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=1)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    o.set_octree(ctx.surface_points(), ctx.irradiance())
+    yield torch, sc, ctx, o
+    ctx.close()
+
+
+@pytest.mark.parametrize("where", ["cheek", "silhouette"])
+def test_c3_window_parity_256spp(c3, where):
+    """C3 at its own 2048x2048 x 256 spp: windows of the frame through the production gather vs the oracle."""
+    torch, sc, ctx, o = c3
+    assert sc.spp == 256
+    if where == "cheek":
+        x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
+    else:
+        x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 37, 29, lambda f: 0.3 < f < 0.7)
+    got = _render(torch, ctx, sc.spp, 11, x0, x1, y0, y1)
+    ref = o.render_tile(sc.spp, 11, x0, x1, y0, y1, nthreads=NT)
+    _check(got, ref)
+    assert (ref[..., 1] > 0).mean() > (0.9 if where == "cheek" else 0.2)
+
+
 def test_c3_rank_tiles_reassemble_bitwise(mpss):
     """C3 (2048x2048, 256 spp, 8 ranks): bench.py's cost-balanced deal of 64x64 tiles; each rank's
     tile set rendered separately and reassembled equals one render of the whole frame."""
@@ -176,11 +222,11 @@ def test_c4_mcprofile_1e7_photons(mpss):
 
 def test_c5_dense_mesh_window(mpss):
     """C5's geometry (head.pbrt subdivided four times: 4.06 M triangles) with the original mesh's
-    2.2 M tessellated points as the pointsfile, at 4096x4096: irradiance on a prefix and a 32x32
-    cheek window at 4 spp against the oracle (its own BVH over the same 4.06 M triangles)."""
+    2.2 M tessellated points as the pointsfile, at 4096x4096 and the config's 512 spp: irradiance on
+    a prefix and a 32x32 cheek window against the oracle (its own BVH over the same 4.06 M triangles)."""
     import torch
     from mpss import pbrtscene
-    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=4096, yres=4096, spp=4)
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=4096, yres=4096, spp=512)
     pts = pbrtscene.mesh_points(sc)
     sc.meshes = [pbrtscene.subdivide_mesh(me, 4) for me in sc.meshes]
     assert sum(len(me["indices"]) for me in sc.meshes) > 4_000_000

@@ -4,11 +4,13 @@ The kernel follows the reference recursion's summation order (diffusionutil.h:17
 rounds every product/sum like the scalar code, so equality is exact, not a tolerance.
 Counters (octree nodes entered, leaf points evaluated) must match the oracle's
 instrumented recursion too (they feed the algorithmic-bytes figure).
-The default spectrally sharded kernel (exact_mo=0) and the packet kernel (exact_mo=2) must
-agree bit for bit with each other; the packet kernel evaluates the same terms with one running sum per
-band; it is held to 2e-5 relative of the reference order (all terms are >= 0, so the
-reassociation error is bounded by n*eps of the result) and must visit exactly the same
-pruned node/point sets as the exact kernel.
+The spectrally sharded kernel (exact_mo=0) with per-band tables (mo_common_grid=0) and the packet
+kernel (exact_mo=2) must agree bit for bit with each other; the packet kernel evaluates the same terms
+with one running sum per band; it is held to 2e-5 relative of the reference order (all terms are
+>= 0, so the reassociation error is bounded by n*eps of the result) and must visit exactly the same
+pruned node/point sets as the exact kernel. The default sharded gather reads each band group's far
+field from its resampled common grid (mo_common_grid=1, accepted per material by a measured error
+bound): same traversal, the same 2e-5 bound against the reference order.
 """
 import numpy as np
 import pytest
@@ -166,7 +168,9 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
         cloud = synth.ellipsoid_cloud(npts, radii=RADII, seed=23, black_frac=0.05)
         q = synth.surface_queries(6001, radii=RADII, seed=29)
         fast, cnt_f, plain_f, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=2)
-        band, cnt_b, plain_b, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=0)
+        band, cnt_b, plain_b, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=0,
+                                          mo_common_grid=0)
+        cg, cnt_g, plain_g, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=0)
         exact, cnt_e, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=True)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, max_error)
         assert np.array_equal(exact, ref)
@@ -177,6 +181,10 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
         assert np.array_equal(band, fast) and np.array_equal(plain_b, fast) and np.array_equal(plain_f, fast)
         # per-group pruning never visits more than the all-band traversal, per group
         assert np.all(cnt_b[:, 2] <= 8 * cnt_f[:, 2]) and np.all(cnt_b[:, 2] > 0)
+        # the common grid: the same traversal, its far lookups resampled
+        assert np.array_equal(cnt_g, cnt_b) and np.array_equal(plain_g, cg)
+        assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
+        assert np.array_equal(cg == 0, ref == 0)
 
 
 def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
@@ -187,10 +195,12 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
             synth.surface_queries(61, radii=(0.002, 0.002, 0.002), seed=5, sort=False),
             cloud[0][:1], np.float32([[10.0, 10.0, 10.0]])]))  # 63 queries: ragged last packet
         fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=2)
-        band, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0)
+        band, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0, mo_common_grid=0)
+        cg, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0)
         ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
         assert _rel_close(fast, ref, 2e-5), npts
         assert np.array_equal(band, fast), npts
+        assert _rel_close(cg, ref, 2e-5), npts
 
 
 @pytest.mark.parametrize("cfg", [dict(mo_band_dealing=1), dict(mo_work_stealing=0), dict(mo_near_field=5088),
@@ -204,9 +214,9 @@ def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profi
     cloud = synth.ellipsoid_cloud(120000, radii=RADII, seed=23, black_frac=0.05)
     q = synth.surface_queries(20000, radii=RADII, seed=29)
     table, rcp = skin_profile
-    _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
+    _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0)
     packet, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=2)
-    _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
+    _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
     assert np.array_equal(base, alt)
     assert np.array_equal(base, packet)  # one running sum per band, the packet kernel's order
     ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
@@ -214,7 +224,31 @@ def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profi
     assert np.any(ref > 0)
 
 
+@pytest.mark.parametrize("cfg", [dict(), dict(mo_work_stealing=0), dict(mo_band_dealing=1)])
+def test_mo_common_grid_vs_oracle(oracle, mpss, torch_dev, skin_profile, cfg):
+    """The default gather with the skin profile's common grid (accepted: mpss_get_gather_info) vs the
+    reference-order oracle, 2e-5 relative as the per-band gather; the choices that do not change a bit
+    with per-band tables do not change one with the common grid either (work stealing), and a
+    different band dealing builds its own grid within the same bound."""
+    cloud = synth.ellipsoid_cloud(120000, radii=RADII, seed=23, black_frac=0.05)
+    q = synth.surface_queries(20000, radii=RADII, seed=29)
+    table, rcp = skin_profile
+    ctx = mpss.Context(max_error=0.1, **cfg)
+    mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
+    info = ctx.gather_info(mid)
+    ctx.close()
+    assert info["common_grid"] and info["l1_err"].max() <= 1e-7 and info["rel_err"].max() <= 1e-5
+    _, _, cg, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
+    _, _, band, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
+    ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
+    assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
+    assert not np.array_equal(cg, band)  # the grid is in use
+    if cfg.get("mo_work_stealing") == 0:
+        _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
+        assert np.array_equal(base, cg)
+
+
 def test_mo_gather_rejects_bad_choices(mpss, torch_dev):
-    for cfg in (dict(mo_near_field=4096), dict(mo_band_dealing=2)):
+    for cfg in (dict(mo_near_field=4096), dict(mo_band_dealing=2), dict(mo_common_grid=2)):
         with pytest.raises(mpss.MpssError):
             mpss.Context(**cfg)
