@@ -90,6 +90,8 @@ def parse(argv=None):
     ap.add_argument("--common-grid", type=int, choices=(0, 1), default=1,
                     help="mpss_config.mo_common_grid: 1 (default) the Mo() gather's far field from the band groups' "
                          "resampled common-grid tables; 0 the per-band tables")
+    ap.add_argument("--near-field", type=int, choices=(10236, 5088), default=None,
+                    help="mpss_config.mo_near_field (default: the library's)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3 strong-scaling figure at N > 1")
@@ -139,6 +141,8 @@ def build_scene(a, label_cfg, local):
     t0 = time.perf_counter()
     kw = {} if a.batch_log2 is None else {"max_batch_samples": 1 << a.batch_log2}
     kw["mo_common_grid"] = a.common_grid
+    if a.near_field:
+        kw["mo_near_field"] = a.near_field
     ctx = pbrtscene.build_context(sc, device=local, **kw)
     t_mat = time.perf_counter() - t0
     if pts is not None:

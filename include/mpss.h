@@ -101,8 +101,11 @@ typedef struct {
                                   reach; 1: snake rounds (every group one of the 8 longest reaches) */
     int mo_work_stealing;      /* 1 (default): a workgroup whose band group runs dry moves on to the
                                   next group with work left; 0: each stays on its own group (XCD) */
-    int mo_near_field;         /* profile entries per band kept in LDS: 10236 (default; one workgroup
-                                  per CU holds the whole 160 KB) or 5088 (two workgroups per CU) */
+    int mo_near_field;         /* profile entries per band kept in LDS: 5088 (default; two 1024-thread
+                                  workgroups per CU, 8 waves per SIMD) or 10236 (one workgroup per CU
+                                  holds the whole 160 KB, 4 waves per SIMD). With the common grid the
+                                  gather waits on memory latency more than on the L2 request rate, and
+                                  8 waves hide more of it (C2: 59.4 vs 68.8 ms per frame) */
     int tessellate_on_host;    /* 1: Preprocess tessellates on the host (threads over triangles,
                                   scene.cpp); 0 (default): one GPU thread per triangle (render.hip
                                   tess_kernel), the same points bit for bit (tessellate.h) */

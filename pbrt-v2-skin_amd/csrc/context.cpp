@@ -168,8 +168,8 @@ void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }
 void Context::gather_info(uint32_t id, int *common_grid, float *rel_err, float *l1_err) const {
     const Material &m = material(id);  // (takes mu_; materials are never replaced)
     const bool band = !m.dipole && !m.rgb;
-    const bool on = band && cfg_.exact_mo == 0 && cfg_.mo_common_grid != 0 && cfg_.mo_near_field == 10236 &&
-                    m.dev_profile.cg.on;
+    const bool on = band && cfg_.exact_mo == 0 && cfg_.mo_common_grid != 0 &&
+                    (cfg_.mo_near_field == 10236 ? m.dev_profile.cg.on : m.dev_profile.cg_half.on);
     *common_grid = on ? 1 : 0;
     for (int c = 0; c < NB; ++c) {
         if (rel_err) rel_err[c] = band ? m.dev_profile.cg_rel_err[c] : 0.f;

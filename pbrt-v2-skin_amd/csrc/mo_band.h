@@ -126,7 +126,8 @@ struct BandTree {
     const float *leaf_r2;                // DeviceOctree::leaf_r2 (nullable: no LDS-only point loops)
     int L, n_nodes, n_points;
     float max_error, prune_f;
-    CommonGrid cg;
+    CommonGrid cg;       // the grid the launch uses (launch_band: cg_half for the 5088 layout)
+    CommonGrid cg_half;
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
@@ -343,15 +344,15 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // issue order (vector memory returns in order), so the second does not wait for the first.
     const int path = u < c.u0lim ? 1 : (u < c.u1lim ? 0 : 2);
     // both global steps' addresses up front, so the allocator cannot place one step's address in
-    // registers the other step's loads are still filling (that would wait for those loads)
-    gf4v *row = (gf4v *)(c.tab + 2u * ((uint32_t)u + c.rowoff));
-    gfloat *tp[4];
+    // registers the other step's loads are still filling (that would wait for those loads); as 32-bit
+    // byte offsets from the (wave-uniform) table bases: one VGPR each, global loads in saddr form
+    uint32_t orow = 32u * ((uint32_t)u + c.rowoff), otp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
-        tp[j] = (gfloat *)(table + c.off[j] + (sj < c.lm2 ? sj : c.lm2));
+        otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
     }
-    asm volatile("" : "+v"(row), "+v"(tp[0]), "+v"(tp[1]), "+v"(tp[2]), "+v"(tp[3]));
+    asm volatile("" : "+v"(orow), "+v"(otp[0]), "+v"(otp[1]), "+v"(otp[2]), "+v"(otp[3]));
     if (path == 1) {  // s_j < klim_j for every band: inside its LDS row
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
         const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
@@ -362,13 +363,16 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // own way and puts the LDS step last)
     asm volatile("" : "+v"(r.p01), "+v"(r.p23)::"memory");
     if (path == 0) {
+        gf4v *row = (gf4v *)((const __attribute__((address_space(1))) char *)c.tab + orow);
         r.p01 = row[0];
         r.p23 = row[1];
 #pragma unroll
         for (int j = 0; j < 4; ++j) r.f[j] = u;
     }
     if (path == 2) {
-        const f2v q0 = *(gf2v *)tp[0], q1 = *(gf2v *)tp[1], q2 = *(gf2v *)tp[2], q3 = *(gf2v *)tp[3];
+        const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
+        const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
+        const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
     }

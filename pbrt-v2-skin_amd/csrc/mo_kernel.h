@@ -58,8 +58,8 @@ struct DeviceProfile {
     // The common grid of each band group (mo_band.h CommonGrid), built by upload() for the 10236-entry
     // LDS layout: ctab holds the groups' pair rows (two float4 per row); cg.on = 1 when some group has
     // an accurate row range.
-    DevBuf<float4> ctab;
-    CommonGrid cg{};
+    DevBuf<float4> ctab, ctab_half;
+    CommonGrid cg{}, cg_half{};  // for the 10236 and 5088 LDS layouts
     float cg_rel_err[NB] = {};  // per band: max |R - T| / |T| over its knots read from the group rows
     float cg_l1_err[NB] = {};   // per band: sum of |R - T| over those knots / sum of |T| over the table
     // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
@@ -75,7 +75,7 @@ constexpr double kCgRelTol = 2e-6;
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group
 // has rows.
 bool build_common_grid(const float *tab, int L, const float *rcp, const BandGroups &groups, CommonGrid &cg,
-                       std::vector<float4> &h, float rel_err[NB], float l1_err[NB]);
+                       std::vector<float4> &h, float rel_err[NB], float l1_err[NB], int near_field = 10236);
 
 // Choices of the sharded gather (mpss_config.mo_near_field / mo_work_stealing; count_noprune =
 // mpss_config.count_traversal == 2, instrumented passes only).

@@ -369,13 +369,15 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
 // Waves per SIMD the register allocation targets: 8 with two workgroups per CU (the 5088-entry near
 // field); the 10236-entry near field fills the LDS with one workgroup (4 waves per SIMD), so up to
 // 128 VGPRs are free to use -- the bands' row bases then stay in VGPRs for the whole traversal.
-template <int KLDS>
+// WGT: threads per workgroup.
+template <int KLDS, int WGT>
 constexpr int wave_kernel_wpe() {
-    return KLDS > 5088 ? 4 : 8;
+    return (WGT / 64) * (KLDS > 5088 ? 1 : 2) / 4;
 }
 
-template <bool COUNT, int KLDS, bool STEAL, bool CG>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS>(), wave_kernel_wpe<KLDS>())))
+template <bool COUNT, int KLDS, bool STEAL, bool CG, int WGT = 1024>
+__global__ __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS, WGT>(),
+                                                                     wave_kernel_wpe<KLDS, WGT>())))
 void mo_band_wave_kernel(BandArgs a) {
     constexpr int ROWF = near_row<KLDS>();
     constexpr bool VROWS = KLDS > 5088;
@@ -413,13 +415,13 @@ void mo_band_wave_kernel(BandArgs a) {
             const int c = a.t.groups.band[grp][j];
             const int o = (int)a.t.cg.lrow[grp][j];
             const int n = a.t.cg.lcnt[grp][j];
-            for (int k = tid; k < n; k += 1024) lt[o + k] = c >= 0 ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
+            for (int k = tid; k < n; k += WGT) lt[o + k] = c >= 0 ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
     } else if (KLDS > 0) {
         // entries 0..kmax of each band, kmax = min(KLDS, L - 2), zeros after (the last two floats of
         // a row are the zero pair of the lanes past the profile end)
         const int kmax = KLDS < a.t.L - 2 ? KLDS : a.t.L - 2;
-        for (int i = tid; i < 4 * ROWF; i += 1024) {
+        for (int i = tid; i < 4 * ROWF; i += WGT) {
             const int j = i / ROWF, k = i % ROWF, c = a.t.groups.band[grp][j];
             lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
@@ -476,12 +478,12 @@ void mo_band_wave_kernel(BandArgs a) {
 // 41.2 ms per launch, profiles/r02j_variants.txt). opts.count_noprune (instrumented pass only):
 // the reach pruning off, so each group walks exactly the records the reference's Mo() recursion
 // reads (bench.py's SURVEY 8d algorithmic bytes).
-template <bool COUNT, int KLDS, bool CG = false>
+template <bool COUNT, int KLDS, bool CG = false, int WGT = 1024>
 void launch_wave(const BandArgs &a, dim3 grid, bool steal, hipStream_t stream) {
     if (steal)
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true, CG>), grid, dim3(1024), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true, CG, WGT>), grid, dim3(WGT), 0, stream, a);
     else
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false, CG>), grid, dim3(1024), 0, stream, a);
+        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false, CG, WGT>), grid, dim3(WGT), 0, stream, a);
 }
 
 void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, const GatherOpts &opts,
@@ -502,11 +504,16 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, cons
     const bool wide = opts.near_field == 10236;
     const int cap = wide ? 32 : 64;  // resident workgroups per group: 1 or 2 per CU of an XCD
     const dim3 grid((unsigned)((chunks < cap ? chunks : cap) * kGroups));
-    const bool cg = wide && opts.common_grid && a.t.cg.on && a.t.cg.tab;
-    if (cg && count)
+    if (!wide) a.t.cg = a.t.cg_half;  // the grid built for the 5088 layout's LDS split
+    const bool cg = opts.common_grid && a.t.cg.on && a.t.cg.tab;
+    if (cg && count && wide)
         launch_wave<true, 10236, true>(a, grid, opts.steal, stream);
-    else if (cg)
+    else if (cg && wide)
         launch_wave<false, 10236, true>(a, grid, opts.steal, stream);
+    else if (cg && count)
+        launch_wave<true, 5088, true>(a, grid, opts.steal, stream);
+    else if (cg)
+        launch_wave<false, 5088, true>(a, grid, opts.steal, stream);
     else if (count && wide)
         launch_wave<true, 10236>(a, grid, opts.steal, stream);
     else if (count)
@@ -547,8 +554,9 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     }
     bt.leaf_r2 = (t.leaf_r2.ptr && t.leaf_r2_error == max_error) ? t.leaf_r2.ptr : nullptr;
     bt.cg = p.cg;
+    bt.cg_half = p.cg_half;
     if (!bt.leaf_r2)
-        for (int g = 0; g < kGroups; ++g) bt.cg.lds_r2[g] = 0.f;
+        for (int g = 0; g < kGroups; ++g) bt.cg.lds_r2[g] = bt.cg_half.lds_r2[g] = 0.f;
     bt.L = p.L;
     bt.n_nodes = t.n_nodes;
     bt.n_points = t.n_points;
@@ -656,11 +664,11 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 constexpr int kCgMaxRows = 65536;
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
-                       std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB]) {
+                       std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field) {
     cg = CommonGrid{};
     h.clear();
     for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
-    constexpr int kLdsFloats = 4 * near_row<10236>();
+    const int kLdsFloats = 4 * (near_field + 3);
     if (L < 4) return false;
     for (int c = 0; c < NB; ++c)
         if (!(host_rcp[c] > 0.f) || !std::isfinite(host_rcp[c])) return false;  // no uniform grid to resample
@@ -803,8 +811,16 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
 
 void DeviceProfile::build_common(const float *tab) {
     ctab.release();
+    ctab_half.release();
     std::vector<float4> h;
-    if (!build_common_grid(tab, L, host_rcp, groups, cg, h, cg_rel_err, cg_l1_err)) {
+    float rel[NB], l1[NB];
+    if (build_common_grid(tab, L, host_rcp, groups, cg_half, h, rel, l1, 5088)) {
+        ctab_half.upload(h.data(), h.size());
+        cg_half.tab = ctab_half.ptr;
+    } else {
+        cg_half.on = 0;
+    }
+    if (!build_common_grid(tab, L, host_rcp, groups, cg, h, cg_rel_err, cg_l1_err, 10236)) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }

@@ -77,7 +77,7 @@ void mpss_config_defaults(mpss_config *c) {
     c->octree_on_host = 0;
     c->mo_band_dealing = 0;
     c->mo_work_stealing = 1;
-    c->mo_near_field = 10236;
+    c->mo_near_field = 5088;
     c->tessellate_on_host = 0;
     c->mo_common_grid = 1;
 }

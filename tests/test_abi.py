@@ -29,7 +29,7 @@ def test_defaults_match_reference_factories(mpss):
     assert (c.max_depth, round(c.max_error, 6), round(c.min_sample_distance, 6), round(c.mix, 6)) == \
         (5, 0.05, 0.25, 0.5)
     # the sharded gather's choices (none changes a result bit; tests/test_mo_gpu.py)
-    assert (c.mo_band_dealing, c.mo_work_stealing, c.mo_near_field) == (0, 1, 10236)
+    assert (c.mo_band_dealing, c.mo_work_stealing, c.mo_near_field) == (0, 1, 5088)
     assert c.mo_common_grid == 1  # the far field from the resampled group tables (within its checked bound)
     assert (c.octree_on_host, c.tessellate_on_host, c.profile_on_host) == (0, 0, 0)  # Preprocess on the GPU
     m = mpss.default_skin()

@@ -203,13 +203,13 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
         assert _rel_close(cg, ref, 2e-5), npts
 
 
-@pytest.mark.parametrize("cfg", [dict(mo_band_dealing=1), dict(mo_work_stealing=0), dict(mo_near_field=5088),
-                                 dict(mo_band_dealing=1, mo_work_stealing=0, mo_near_field=5088)])
+@pytest.mark.parametrize("cfg", [dict(mo_band_dealing=1), dict(mo_work_stealing=0), dict(mo_near_field=10236),
+                                 dict(mo_band_dealing=1, mo_work_stealing=0, mo_near_field=10236)])
 def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profile, cfg):
-    """The default gather deals bands into adjacent-reach groups, lets workgroups steal other
-    groups' units and keeps 10236 profile entries per band in LDS; snake-round groups
-    (mo_band_dealing 1), per-XCD groups (mo_work_stealing 0) and the two-workgroups-per-CU near
-    field (mo_near_field 5088) evaluate the same non-zero terms in the same order, so every sum
+    """The per-band gather (mo_common_grid 0) deals bands into adjacent-reach groups, lets
+    workgroups steal other groups' units and keeps 5088 profile entries per band in LDS; snake-round
+    groups (mo_band_dealing 1), per-XCD groups (mo_work_stealing 0) and the one-workgroup-per-CU near
+    field (mo_near_field 10236) evaluate the same non-zero terms in the same order, so every sum
     must match bit for bit (and the oracle)."""
     cloud = synth.ellipsoid_cloud(120000, radii=RADII, seed=23, black_frac=0.05)
     q = synth.surface_queries(20000, radii=RADII, seed=29)
@@ -224,7 +224,7 @@ def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profi
     assert np.any(ref > 0)
 
 
-@pytest.mark.parametrize("cfg", [dict(), dict(mo_work_stealing=0), dict(mo_band_dealing=1)])
+@pytest.mark.parametrize("cfg", [dict(), dict(mo_work_stealing=0), dict(mo_band_dealing=1), dict(mo_near_field=10236)])
 def test_mo_common_grid_vs_oracle(oracle, mpss, torch_dev, skin_profile, cfg):
     """The default gather with the skin profile's common grid (accepted: mpss_get_gather_info) vs the
     reference-order oracle, 2e-5 relative as the per-band gather; the choices that do not change a bit
@@ -237,12 +237,18 @@ def test_mo_common_grid_vs_oracle(oracle, mpss, torch_dev, skin_profile, cfg):
     mid = ctx.set_material_tables(table, rcp, np.zeros(1025, np.float32))
     info = ctx.gather_info(mid)
     ctx.close()
-    assert info["common_grid"] and info["l1_err"].max() <= 1e-7 and info["rel_err"].max() <= 1e-5
+    # adjacent-reach groups (the default) get rows; snake rounds mix reaches 1:400 within a group, which
+    # leaves their LDS split too short for an accurate row range (then the exact tables serve it all)
+    assert info["common_grid"] == (cfg.get("mo_band_dealing", 0) == 0)
+    assert info["l1_err"].max() <= 1e-7 and info["rel_err"].max() <= 2e-6
     _, _, cg, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
     _, _, band, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
     ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
     assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
-    assert not np.array_equal(cg, band)  # the grid is in use
+    if info["common_grid"]:
+        assert not np.array_equal(cg, band)  # the grid is in use
+    else:
+        assert np.array_equal(cg, band)
     if cfg.get("mo_work_stealing") == 0:
         _, _, base, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0)
         assert np.array_equal(base, cg)
