@@ -80,7 +80,10 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
                     help="weak: one frame per GPU per step; strong: one frame per step split over the GPUs "
                          "(default: the config's)")
-    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"))
+    ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "skin.pbrt"),
+                    help="scene file (scenes/skin_textured.pbrt: C2 with imagemap albedo and bump)")
+    ap.add_argument("--rgb-profile", action="store_true",
+                    help="LayeredSkin \"rgbprofile\" on (ComputeRGBMultipoleProfile: three profiles, FromRGB)")
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None, help="tile size (default 128; 64 for c3 on several GPUs)")
@@ -134,6 +137,9 @@ def build_scene(a, label_cfg, local):
     res = a.res or res
     spp = a.spp or spp
     sc = pbrtscene.load(a.scene, xres=res, yres=res, spp=spp)
+    if a.rgb_profile:
+        for m in sc.materials:
+            m["rgb_profile"] = 1
     pts = None
     if subdiv:
         pts = pbrtscene.mesh_points(sc)
@@ -282,6 +288,7 @@ def main(a):
     sss_per_step, traced_per_step = float(sss[0].item()), float(sss[1].item())
     # dominant kernel + Mo gather roofline (per-launch averages over the timed region, this rank)
     kern = {"primary": (st["ms_camera"], st["n_camera"]), "shade_direct": (st["ms_direct"], st["n_direct"]),
+            "shade_tex": (st["ms_tex"], st["n_tex"]),
             "mo_band": (st["ms_shade"], st["n_shade"]),
             "film": (st["ms_film"], st["n_film"])}
     dom = max(kern, key=lambda k: kern[k][0])
@@ -348,12 +355,14 @@ def main(a):
                 "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f32",
-                "data": "synthetic (reconstructed skin.pbrt, head.pbrt mesh%s)" % (", subdivided" if subdiv else ""),
+                "data": "synthetic (reconstructed %s, head.pbrt mesh%s%s)" % (
+                    os.path.basename(a.scene), ", subdivided" if subdiv else "", ", rgbprofile" if a.rgb_profile else ""),
                 "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles%s%s"
                            % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T,
                               ", independent whole frames, one per GPU" if frames == world and world > 1 else
                               (" dealt by cost" if world > 1 else ""),
                               ", one RCCL film gather per step" if world > 1 else ""),
+                           "scene": os.path.basename(a.scene), "rgb_profile": bool(a.rgb_profile),
                            "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3), "tile_deal_s": round(t_deal, 3),

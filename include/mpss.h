@@ -150,7 +150,10 @@ typedef struct {
                              the layers' 30-band mua / musp reduced to RGB (ToRGBSpectrum), three
                              profiles, Rd(d^2) = FromRGB(reflectance) of the three lookups
                              (multipole.cpp:85-107); the exported table then holds the R, G, B
-                             profiles in rows c % 3. Mo() runs the reference-order gather */
+                             profiles in rows c % 3. Mo(): the sharded gather reads the three
+                             profiles in every band group (its common grid built over them) and
+                             takes FromRGB per record into the group's bands; exact_mo = 1 runs the
+                             reference-order gather */
 } mpss_layeredskin;
 
 void mpss_layeredskin_defaults(mpss_layeredskin *m);
@@ -174,8 +177,9 @@ int mpss_get_material_tables(mpss_ctx *ctx, uint32_t material_id, float *rd_tabl
                              float *rho_hd, uint32_t *n_rho, float *total_reflectance);
 /* How the sharded gather evaluates material `id` (mpss_config.mo_common_grid): *common_grid = 1 when
  * its far field is read from the resampled group tables, 0 for per-band tables (or a material the
- * sharded gather does not run: dipole, rgbprofile). rel_err / l1_err (nullable, 30 floats): the
- * measured resampling error per band (see mo_common_grid), 0 without a common grid. */
+ * sharded gather does not run: dipole). rel_err / l1_err (nullable, 30 floats): the measured
+ * resampling error per band (see mo_common_grid; rgbprofile: entries 0..2, its R, G, B profiles),
+ * 0 without a common grid. */
 int mpss_get_gather_info(mpss_ctx *ctx, uint32_t id, int *common_grid, float *rel_err, float *l1_err);
 
 /* Texture "imagemap" (CreateImageSpectrumTexture / CreateImageFloatTexture, textures/imagemap.cpp:
@@ -306,6 +310,8 @@ typedef struct {
      * the group rows (two 16-byte loads), from the LDS near field, from the bands' own tables (four
      * 8-byte loads) */
     int64_t mo_row_lane_records, mo_lds_lane_records, mo_table_lane_records;
+    double ms_tex;        /* texture lookups at the camera hits (albedo / bump imagemaps; shade_tex) */
+    int64_t n_tex;
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal (0, 1 or 2, as mpss_config) after creation
@@ -363,16 +369,18 @@ int mpss_host_dipole_rd(const float *sigma_a, const float *sigmap_s, float eta, 
 int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, int sqrt_samples, float *hd,
                         float *hh);
 /* The common grid the sharded gather builds for a profile (mpss_config.mo_common_grid), on the host:
- * table [30][L], rcp [30]; snake as mpss_config.mo_band_dealing. Outputs (each nullable): rows
+ * table [30][L], rcp [30]; snake as mpss_config.mo_band_dealing (0, 1), or 2: an rgbprofile table
+ * (rows 0..2 = R, G, B, read in slots 0..2 of every group). Outputs (each nullable): rows
  * [n_rows][8] (the groups' pair rows: group g's row for u is row0[g] + u - ubase[g], holding
  * R_0(u), R_0(u+1), ..., R_3(u), R_3(u+1)); *n_rows (call with rows NULL to size it); bands [8][4]
- * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim [8]
- * (lanes with u < u0lim read the exact LDS near field, u0lim <= u < u1lim the rows, u >= u1lim the
- * bands' own tables); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over
- * the knots each band reads from the rows); *ok = 1 when some group has rows. */
+ * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim /
+ * u1start [8] (lanes with u < u0lim read the exact LDS near field, u1start <= u < u1lim the rows, any
+ * other u the bands' own tables; u1start = u0lim unless the rows begin past the end of bands the grid
+ * cannot follow); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over the
+ * knots each band reads from the rows); *ok = 1 when some group has rows. */
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
-                          int32_t *bands, float *rg, float *u0lim, float *u1lim, uint32_t *row0, uint32_t *ubase,
-                          float *rel_err, float *l1_err, int *ok);
+                          int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
+                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok);
 /* Octree build + pre-order export (sizes first with NULL outputs). */
 int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
                             uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,

@@ -106,7 +106,7 @@ void Context::end_inflight() {
 void Context::ensure_layouts() {
     if (!have_octree_) return;
     for (const auto &m : materials_)
-        if (!m->dipole && !m->rgb) dev_octree_.ensure_layout(m->dev_profile.groups);
+        if (!m->dipole) dev_octree_.ensure_layout(m->dev_profile.groups);
 }
 
 // SubsurfaceOctreeNode::Mo for a batch of points (mpss_mo_batch). The octree, profile and band
@@ -129,8 +129,8 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         mode = cfg_.exact_mo;
         if (m->dipole) {
             mode = -1;  // closed-form functor: the reference-order gather (dipole.h)
-        } else if (m->rgb) {
-            mode = -2;  // FromRGB of three lookups: the reference-order gather
+        } else if (m->rgb && mode != 0) {
+            mode = -2;  // FromRGB of three lookups in the reference order (exact_mo 1; also for the packet mode)
         } else if (mode == 0) {
             layout = &dev_octree_.ensure_layout(m->dev_profile.groups);
             ws = acquire_ws();
@@ -167,7 +167,7 @@ void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }
 
 void Context::gather_info(uint32_t id, int *common_grid, float *rel_err, float *l1_err) const {
     const Material &m = material(id);  // (takes mu_; materials are never replaced)
-    const bool band = !m.dipole && !m.rgb;
+    const bool band = !m.dipole;  // (rgbprofile: the grid of its R, G, B profiles, rel/l1_err[0..2])
     const bool on = band && cfg_.exact_mo == 0 && cfg_.mo_common_grid != 0 &&
                     (cfg_.mo_near_field == 10236 ? m.dev_profile.cg.on : m.dev_profile.cg_half.on);
     *common_grid = on ? 1 : 0;
@@ -239,7 +239,7 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
         mat->dev_rgb.upload(mat->profile.table.data(), 3 * (size_t)mat->profile.length);
         for (int k = 0; k < 3; ++k) mat->rgb_rcp[k] = mat->profile.rcp[k];
         mat->dev_rgb_rcp.upload(mat->rgb_rcp, 3);
-        for (int c = 0; c < NB; ++c) mat->dev_profile.groups.pos[c] = c;  // Mo() rows in band order
+        mat->dev_profile.set_rgb(mat->profile.table.data());  // the sharded gather's three lookups + FromRGB
     }
     mat->dev_rho.upload(mat->rho.hd.data(), mat->rho.hd.size());
     materials_.push_back(std::move(mat));

@@ -94,19 +94,21 @@ inline bool same_groups(const BandGroups &a, const BandGroups &b) {
 // unrelated offsets (the gather is bound by the L2 request rate of these per-lane loads, DESIGN.md
 // §4). Each lane takes one of three paths by u:
 //   u < u0lim          every band's exact pair from its LDS near field (as the per-band gather);
-//   u0lim <= u < u1lim the group rows -- only where the resampling is accurate: build_common measures
-//                      the error at every band's own grid knots and ends the range before the first
-//                      knot off by more than kCgRelTol of the band's local value (the tables' far
-//                      tails carry the MPC resampler's kinks and float noise a coarser grid cannot
-//                      follow);
-//   u >= u1lim         every band's exact pair from its own table in HBM/L2 (as the per-band gather).
+//   u1start <= u < u1lim the group rows -- only where the resampling is accurate: build_common
+//                      measures the error at every band's own grid knots and ends the range before
+//                      the first knot off by more than kCgRelTol of the band's local value (the
+//                      tables' far tails carry the MPC resampler's kinks and float noise a coarser
+//                      grid cannot follow); u1start = u0lim, or (bands of widely different reach,
+//                      the rgbprofile's R, G, B) past the end of the bands the grid cannot follow;
+//   otherwise          every band's exact pair from its own table in HBM/L2 (as the per-band gather).
 struct CommonGrid {
     const float4 *tab;          // pair rows, two float4 each; group g's row for u at 2 * (row0[g] + u - ubase[g])
     uint32_t row0[kGroups];     // group g's first pair row
     uint32_t ubase[kGroups];    // the u of that row
     float rg[kGroups];          // the group's grid: u = d2 * rg (its smallest rcp)
     float u0lim[kGroups];       // u < u0lim => every band's pair (s, s + 1) lies in its LDS near field
-    float u1lim[kGroups];       // u0lim <= u < u1lim: the pair rows (u1lim = u0lim: none)
+    float u1lim[kGroups];       // u1start <= u < u1lim: the pair rows (u1lim = u0lim: none)
+    float u1start[kGroups];     // (u0lim, or past the end of the bands the rows cannot serve)
     float tau[kGroups][4];      // d2 >= tau <=> fl(d2 * rcp) >= L - 1: the band is past its profile end
     uint32_t lrow[kGroups][4];  // float offset of slot j's near-field row in LDS (entries 0..klim_j)
     int lcnt[kGroups][4];       // its length, klim_j + 1 floats (2 zeros for an empty slot)
@@ -128,6 +130,11 @@ struct BandTree {
     float max_error, prune_f;
     CommonGrid cg;       // the grid the launch uses (launch_band: cg_half for the 5088 layout)
     CommonGrid cg_half;
+    // The table row each group slot looks up: groups.band for a spectral profile; for an rgbprofile
+    // material (RGB = 1) rows 0, 1, 2 (its R, G, B profiles) in every group, slot 3 unused -- the
+    // group's four OUTPUT bands stay groups.band (Rd_c = FromRGB of the three lookups, band c).
+    int lband[kGroups][4];
+    const float *rgb_refl;  // RGB: rgbRefl2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue} [7][NB]
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
@@ -269,12 +276,78 @@ __device__ __forceinline__ void band_rd_lerp(const float f[4], const RdPair v[4]
     }
 }
 
-// The combine half: lerp, the Mo() products and the running sums (one point or node).
-template <bool POINT>
+// Band c of SampledSpectrum::FromRGB(rgb, SPECTRUM_REFLECTANCE) (spectrum.cpp:103-186) with the
+// refl tables in memory ([7][NB], c wave-uniform: scalar loads): the float operations of the
+// 30-band host code (spectral.cpp spectrum_from_rgb) and of the reference-order gather's FN_RGB.
+__device__ __forceinline__ float from_rgb_c(const float *__restrict__ refl, float R, float G, float B, int c) {
+    enum { W = 0, CY = 1, MG = 2, YE = 3, RD = 4, GR = 5, BL = 6 };
+    const float *k = refl + c;
+    float r = 0.f;
+    if (R <= G && R <= B) {
+        r += k[W * NB] * R;
+        if (G <= B) { r += k[CY * NB] * (G - R); r += k[BL * NB] * (B - G); }
+        else { r += k[CY * NB] * (B - R); r += k[GR * NB] * (G - B); }
+    } else if (G <= R && G <= B) {
+        r += k[W * NB] * G;
+        if (R <= B) { r += k[MG * NB] * (R - G); r += k[BL * NB] * (B - R); }
+        else { r += k[MG * NB] * (B - G); r += k[RD * NB] * (R - B); }
+    } else {
+        r += k[W * NB] * B;
+        if (R <= G) { r += k[YE * NB] * (R - B); r += k[GR * NB] * (G - R); }
+        else { r += k[YE * NB] * (G - B); r += k[RD * NB] * (R - G); }
+    }
+    const float v = r * (float).94;
+    return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
+}
+
+// from_rgb_c for the group's four output bands (obands, -1 = empty: 0), without the branches: the
+// case split only picks which component is the minimum, middle and maximum and which two of the
+// six secondary/primary tables weigh the differences, so it is done once per term with selects and
+// every band then takes the same three products and two sums as from_rgb_c's taken branch
+// (W * min + X * (mid - min) + Y * (max - mid), * .94, clamp), the identical float operations.
+__device__ __forceinline__ void from_rgb4(const float *__restrict__ refl, float R, float G, float B,
+                                          const int *obands, float o[4]) {
+    enum { W = 0, CY = 1, MG = 2, YE = 3, RD = 4, GR = 5, BL = 6 };
+    const bool rmin = R <= G && R <= B;
+    const bool gmin = !rmin && G <= R && G <= B;
+    const bool c2 = rmin ? G <= B : (gmin ? R <= B : R <= G);
+    const float mn = rmin ? R : (gmin ? G : B);
+    const float md = rmin ? (c2 ? G : B) : (gmin ? (c2 ? R : B) : (c2 ? R : G));
+    const float mx = rmin ? (c2 ? B : G) : (gmin ? (c2 ? B : R) : (c2 ? G : R));
+    const float d1 = md - mn, d2 = mx - md;
+    // Y: the primary of the maximum (blue, green or red)
+    const bool ybl = c2 && !(!rmin && !gmin), yrd = !c2 && !rmin;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (obands[j] < 0) {
+            o[j] = 0.f;
+            continue;
+        }
+        const float *k = refl + obands[j];
+        const float kx = rmin ? k[CY * NB] : (gmin ? k[MG * NB] : k[YE * NB]);
+        const float ky = ybl ? k[BL * NB] : (yrd ? k[RD * NB] : k[GR * NB]);
+        float r = k[W * NB] * mn;
+        r += kx * d1;
+        r += ky * d2;
+        const float v = r * (float).94;
+        o[j] = v < 0.f ? 0.f : v;
+    }
+}
+
+// The combine half: lerp, the Mo() products and the running sums (one point or node). RGB: the
+// slots hold the R, G, B lookups, and the group's output bands (obands, -1 = empty) take FromRGB.
+template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
-                                                f2v acc[2]) {
+                                                f2v acc[2], const float *refl = nullptr,
+                                                const int *obands = nullptr) {
     float rd[4];
     band_rd_lerp(f, v, rd);
+    if (RGB) {
+        float o[4];
+        from_rgb4(refl, rd[0], rd[1], rd[2], obands, o);
+        band_rd_products<POINT>(o, e, w, acc);
+        return;
+    }
     band_rd_products<POINT>(rd, e, w, acc);
 }
 
@@ -283,7 +356,7 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
 struct CgLane {
     const float4 *tab;    // the pair rows, indexed by u0 + rowoff
     uint32_t rowoff;      // row0 - ubase (mod 2^32)
-    float rg, u0lim, u1lim;
+    float rg, u0lim, u1lim, u1start;
     float tau[4];
     float tau_min;        // the group's first profile end
     uint32_t lrow[4];     // LDS float offsets of the slots' exact near-field rows
@@ -342,7 +415,7 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // earlier step's loads target only once those have returned, and LDS returns first (the
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
     // issue order (vector memory returns in order), so the second does not wait for the first.
-    const int path = u < c.u0lim ? 1 : (u < c.u1lim ? 0 : 2);
+    const int path = u < c.u0lim ? 1 : ((u < c.u1lim && u >= c.u1start) ? 0 : 2);
     // both global steps' addresses up front, so the allocator cannot place one step's address in
     // registers the other step's loads are still filling (that would wait for those loads); as 32-bit
     // byte offsets from the (wave-uniform) table bases: one VGPR each, global loads in saddr form
@@ -400,9 +473,9 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 // gather's, the group rows' on the group grid -- then its range test (multipole.cpp:65-66) as
 // d2 >= tau: only lanes off the LDS path can be past a band's end, and only at the group's reach, so
 // the test runs when some lane of the wave is past the group's first end.
-template <bool POINT>
+template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
-                                           f2v acc[2]) {
+                                           f2v acc[2], const float *refl = nullptr, const int *obands = nullptr) {
     float rd[4];
     const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
     band_rd_lerp(r.f, v, rd);
@@ -410,16 +483,23 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
 #pragma unroll
         for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
     }
+    if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
+        float o[4];
+        from_rgb4(refl, rd[0], rd[1], rd[2], obands, o);
+        band_rd_products<POINT>(o, e, w, acc);
+        return;
+    }
     band_rd_products<POINT>(rd, e, w, acc);
 }
 
-template <bool POINT, bool COUNT, int KLDS>
+template <bool POINT, bool COUNT, int KLDS, bool RGB = false>
 __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   int hist[7]) {
+                                                   int hist[7], const float *refl = nullptr,
+                                                   const int *obands = nullptr) {
     float f[4];
     RdPair v[4];
     band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
-    band_rd_combine<POINT>(f, v, e, w, acc);
+    band_rd_combine<POINT, RGB>(f, v, e, w, acc, refl, obands);
 }
 
 // sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d)
@@ -443,17 +523,20 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m) {
 // CG: far lookups from the group's common grid (CommonGrid; the LDS holds the exact near field in
 // CommonGrid::lrow's per-slot rows), else every band from its own table (bit-identical to the packet
 // kernel).
-template <bool COUNT, int KLDS, bool VROWS, bool CG = false>
+template <bool COUNT, int KLDS, bool VROWS, bool CG = false, bool RGB = false>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
                                                  int hist[7], const float *lt) {
     BandLane b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int c = a.groups.band[grp][j];
+        const int c = a.lband[grp][j];
         b.rcp[j] = a.grcp[grp][j];
         b.off[j] = (uint32_t)(c >= 0 ? c : 0) * (uint32_t)a.L;
     }
+    int ob[4];  // RGB: the group's output bands
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ob[j] = a.groups.band[grp][j];
     b.lm1 = (uint32_t)(a.L - 1);
     const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
     b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
@@ -469,6 +552,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         cl.rg = a.cg.rg[grp];
         cl.u0lim = a.cg.u0lim[grp];
         cl.u1lim = a.cg.u1lim[grp];
+        cl.u1start = a.cg.u1start[grp];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             cl.tau[j] = a.cg.tau[grp][j];
@@ -524,9 +608,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<false>(cl, r, d2, e, 1.f, acc);
+                        cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, a.rgb_refl, ob);
                     } else {
-                        band_rd_accumulate<false, COUNT, KLDS>(b, d2, e, 1.f, acc, hist);
+                        band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, a.rgb_refl, ob);
                     }
                 } else {
                     open = true;
@@ -554,16 +638,16 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         if (CG) {
                             const CgRec ra = cg_fetch_near(b, cl, d2a), rb = cg_fetch_near(b, cl, d2b);
-                            cg_combine<true>(cl, ra, d2a, e0, pa.w, lacc);
-                            cg_combine<true>(cl, rb, d2b, e1, pb.w, lacc);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, a.rgb_refl, ob);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, a.rgb_refl, ob);
                             continue;
                         }
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
                         band_rd_fetch_lds<KLDS>(b, d2a, fa, va);
                         band_rd_fetch_lds<KLDS>(b, d2b, fb, vb);
-                        band_rd_combine<true>(fa, va, e0, pa.w, lacc);
-                        band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, a.rgb_refl, ob);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, a.rgb_refl, ob);
                     }
                 }
                 for (; i0 + 1 < live; i0 += 2) {
@@ -587,8 +671,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                             const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
                             const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
                             const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                            cg_combine<true>(cl, ra, d2a, e0, pa.w, lacc);
-                            cg_combine<true>(cl, rb, d2b, e1, pb.w, lacc);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, a.rgb_refl, ob);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, a.rgb_refl, ob);
                             continue;
                         }
                         float fa[4], fb[4];
@@ -602,8 +686,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                                          "v"(vb[1].a), "v"(vb[1].b), "v"(vb[2].a), "v"(vb[2].b), "v"(vb[3].a),
                                          "v"(vb[3].b));
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                        band_rd_combine<true>(fa, va, e0, pa.w, lacc);
-                        band_rd_combine<true>(fb, vb, e1, pb.w, lacc);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, a.rgb_refl, ob);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, a.rgb_refl, ob);
                     }
                 for (int i = i0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
@@ -616,9 +700,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<true>(cl, r, d2, e, ph.w, lacc);
+                        cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, a.rgb_refl, ob);
                     } else {
-                        band_rd_accumulate<true, COUNT, KLDS>(b, d2, e, ph.w, lacc, hist);
+                        band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, a.rgb_refl, ob);
                     }
                 }
                 acc[0] += lacc[0];

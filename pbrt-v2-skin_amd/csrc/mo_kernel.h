@@ -64,7 +64,13 @@ struct DeviceProfile {
     float cg_l1_err[NB] = {};   // per band: sum of |R - T| over those knots / sum of |T| over the table
     // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
     void upload(const float *table, int L, const float *rcp, bool snake = false);
-    void build_common(const float *table);  // (upload calls it; host table [NB][L])
+    // (upload calls it with groups, set_rgb with rows 0..2 in every group; host table [NB][L])
+    void build_common(const float *table, const BandGroups &slots);
+    // rgbprofile material: rows 0..2 of the table are its R, G, B profiles; the sharded gather looks
+    // up those three for every group and converts them with FromRGB (rgb_refl: the device copy of
+    // the rgbRefl2Spect tables, [7][NB]; set_rgb after upload)
+    DevBuf<float> rgb_refl;
+    void set_rgb(const float *table);
 };
 
 // The common grid's bound on the resampling error of a lookup relative to the band's own value there

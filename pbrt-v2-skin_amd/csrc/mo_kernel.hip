@@ -27,6 +27,7 @@
 #include "mo_kernel.h"
 #include "spectral.h"
 #include "mo_packet.h"
+#include "mo_wave.h"
 
 #include <algorithm>
 #include <cmath>
@@ -291,48 +292,6 @@ __global__ __launch_bounds__(256) void mo_packet_kernel(MoArgs a, int nblocks) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Spectrally sharded gather (mo_band.h), in two launches: mo_sort_kernel sorts each 1024-query
-// chunk by a Morton key of its query positions into a permutation, then the persistent
-// mo_band_wave_kernel deals 64 sorted queries at a time to waves. Workgroup b starts on band group
-// b % 8 (one XCD under the round-robin dispatch), so each XCD's L2 holds only its group's tables.
-// Every result goes to its query's own slot, so neither the order nor the stealing changes a bit.
-// ---------------------------------------------------------------------------------------
-
-struct BandArgs {
-    BandTree t;
-    const float *__restrict__ queries3;  // q * 3 (batch API) or null
-    const float4 *__restrict__ queries4; // {p, *} (render path) or null
-    const int *__restrict__ count;       // device query count (nullable: use nq)
-    const uint32_t *__restrict__ hit_s;  // render path with several BSSRDF materials: material filter
-    int mat;
-    int nq;
-    float *__restrict__ out;             // batch: out[q * stride + band]
-    float4 *__restrict__ out4;           // render: out4[q * 8 + group]
-    int out_stride;
-    int32_t *__restrict__ counters;      // batch API COUNT: q * 4 (+= per group)
-    unsigned long long *__restrict__ counts;  // render COUNT: [kStatStride * kGroups]
-    int *__restrict__ work;              // [kGroups] chunk counters (zeroed before the launch)
-    float klo[3], kinv[3];               // Morton key quantization (octree root bounds)
-    int *perm;                           // chunk-sorted query ids (-1: none), mo_sort_kernel
-};
-
-__device__ __forceinline__ bool band_query(const BandArgs &a, int q, float &px, float &py, float &pz) {
-    if (a.queries4) {
-        const float4 v = a.queries4[q];
-        px = v.x;
-        py = v.y;
-        pz = v.z;
-        bool live = v.w >= 0.f;  // render hit list: w < 0 marks hits without a BSSRDF
-        if (live && a.hit_s) live = (int)((a.hit_s[q] >> 16) & 0xffu) == a.mat;
-        return live;
-    }
-    px = a.queries3[3 * (size_t)q];
-    py = a.queries3[3 * (size_t)q + 1];
-    pz = a.queries3[3 * (size_t)q + 2];
-    return true;
-}
-
 // Step 1: each 1024-query chunk sorted by the Morton key of its live queries, written as a
 // permutation: perm[base + i] = the i-th query
 // of the chunk in key order, -1 past the live ones. Chunks at or past the query count write nothing.
@@ -363,129 +322,6 @@ __global__ __launch_bounds__(1024) void mo_sort_kernel(BandArgs a) {
     a.perm[base + tid] = (mine >> 32) != 0xffffffffull ? base + (int)(mine & 0xffffffffull) : -1;
 }
 
-// Step 2: every wave takes 64 consecutive entries of perm at a time from its group's counter and
-// walks them to the end on its own -- no workgroup barrier between chunks, so a wave with a short
-// traversal does not wait for the slowest wave of its workgroup. Same traversal, same sums.
-// Waves per SIMD the register allocation targets: 8 with two workgroups per CU (the 5088-entry near
-// field); the 10236-entry near field fills the LDS with one workgroup (4 waves per SIMD), so up to
-// 128 VGPRs are free to use -- the bands' row bases then stay in VGPRs for the whole traversal.
-// WGT: threads per workgroup.
-template <int KLDS, int WGT>
-constexpr int wave_kernel_wpe() {
-    return (WGT / 64) * (KLDS > 5088 ? 1 : 2) / 4;
-}
-
-template <bool COUNT, int KLDS, bool STEAL, bool CG, int WGT = 1024>
-__global__ __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(wave_kernel_wpe<KLDS, WGT>(),
-                                                                     wave_kernel_wpe<KLDS, WGT>())))
-void mo_band_wave_kernel(BandArgs a) {
-    constexpr int ROWF = near_row<KLDS>();
-    constexpr bool VROWS = KLDS > 5088;
-    __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
-    __shared__ int next_grp;
-    const int tid = (int)threadIdx.x, lane = tid & 63;
-    const int nq = a.count ? *a.count : a.nq;
-    // STEAL: a workgroup whose group queue is dry moves on to the next group with units left
-    // (groups g + 1, g + 2, ... in turn), reloading its near field; the XCDs whose groups finish
-    // first then take over the tail of the slowest group.
-    const int home = (int)(blockIdx.x & (kGroups - 1));
-    for (int ph = 0; ph < (STEAL ? kGroups : 1); ++ph) {
-    int grp = home;
-    if (STEAL) {
-        if (ph > 0) {
-            __syncthreads();  // every wave is done with the previous group's near field
-            if (tid == 0) {
-                int g = -1;
-                for (int k = ph; k < kGroups && g < 0; ++k) {
-                    const int c = (home + k) & (kGroups - 1);
-                    if (__hip_atomic_load(&a.work[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * 64 < nq) g = c;
-                }
-                next_grp = g;
-            }
-            __syncthreads();
-            grp = next_grp;
-            if (grp < 0) break;
-            // (the loop index stays ph; later phases search from ph onwards, so a group is tried at
-            // most once after it was found dry)
-        }
-    }
-    if (CG) {
-        // slot j's exact near field: entries 0..klim_j of its band (CommonGrid::lrow, lcnt = klim_j + 1)
-        for (int j = 0; j < 4; ++j) {
-            const int c = a.t.groups.band[grp][j];
-            const int o = (int)a.t.cg.lrow[grp][j];
-            const int n = a.t.cg.lcnt[grp][j];
-            for (int k = tid; k < n; k += WGT) lt[o + k] = c >= 0 ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
-        }
-    } else if (KLDS > 0) {
-        // entries 0..kmax of each band, kmax = min(KLDS, L - 2), zeros after (the last two floats of
-        // a row are the zero pair of the lanes past the profile end)
-        const int kmax = KLDS < a.t.L - 2 ? KLDS : a.t.L - 2;
-        for (int i = tid; i < 4 * ROWF; i += WGT) {
-            const int j = i / ROWF, k = i % ROWF, c = a.t.groups.band[grp][j];
-            lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
-        }
-    }
-    __syncthreads();  // the near field is read-only from here on
-    for (;;) {
-        int u = 0;
-        if (lane == 0) u = atomicAdd(&a.work[grp], 1);
-        u = __builtin_amdgcn_readfirstlane(__shfl(u, 0));
-        const int base = u * 64;
-        if (base >= nq) break;
-        const int q = a.perm[base + lane];
-        float px = 0.f, py = 0.f, pz = 0.f;
-        const bool live = q >= 0 && band_query(a, q, px, py, pz);
-        float acc[4];
-        int kn = 0, kp = 0, wn = 0, wp = 0, hist[7] = {0, 0, 0, 0, 0, 0, 0};
-        mo_band_traverse<COUNT, KLDS, VROWS && !CG, CG>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist, lt);
-        if (live) {
-            if (a.out4) {
-                a.out4[(size_t)q * kGroups + grp] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int c = a.t.groups.band[grp][j];
-                    if (c >= 0) a.out[(size_t)q * a.out_stride + c] = acc[j];
-                }
-            }
-        }
-        if (COUNT) {
-            if (a.counters && live) {
-                atomicAdd(&a.counters[4 * (size_t)q + 2], kn);
-                atomicAdd(&a.counters[4 * (size_t)q + 3], kp);
-            }
-            if (a.counts) {
-                if (kn) atomicAdd(&a.counts[kStatStride * grp], (unsigned long long)kn);
-                if (kp) atomicAdd(&a.counts[kStatStride * grp + 1], (unsigned long long)kp);
-                if (lane == 0) {
-                    atomicAdd(&a.counts[kStatStride * grp + 2], (unsigned long long)wn);
-                    atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
-                }
-#pragma unroll
-                for (int k = 0; k < 7; ++k)
-                    if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
-            }
-        }
-    }
-    }
-}
-
-// The sharded gather: the sort launch, then the persistent wave-queue launch. opts.near_field picks
-// the LDS near field per band: 10236 entries (one 1024-thread workgroup per CU holding the whole
-// 160 KB; 32 workgroups per group) or 5088 (two workgroups per CU, 64 per group). opts.steal: a
-// workgroup whose group queue runs dry moves on to the next group with work left (C2: 42.5 ->
-// 41.2 ms per launch, profiles/r02j_variants.txt). opts.count_noprune (instrumented pass only):
-// the reach pruning off, so each group walks exactly the records the reference's Mo() recursion
-// reads (bench.py's SURVEY 8d algorithmic bytes).
-template <bool COUNT, int KLDS, bool CG = false, int WGT = 1024>
-void launch_wave(const BandArgs &a, dim3 grid, bool steal, hipStream_t stream) {
-    if (steal)
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, true, CG, WGT>), grid, dim3(WGT), 0, stream, a);
-    else
-        hipLaunchKernelGGL((mo_band_wave_kernel<COUNT, KLDS, false, CG, WGT>), grid, dim3(WGT), 0, stream, a);
-}
-
 void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, const GatherOpts &opts,
                  hipStream_t stream) {
     if (nq_max <= 0) return;
@@ -506,22 +342,14 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, cons
     const dim3 grid((unsigned)((chunks < cap ? chunks : cap) * kGroups));
     if (!wide) a.t.cg = a.t.cg_half;  // the grid built for the 5088 layout's LDS split
     const bool cg = opts.common_grid && a.t.cg.on && a.t.cg.tab;
-    if (cg && count && wide)
-        launch_wave<true, 10236, true>(a, grid, opts.steal, stream);
-    else if (cg && wide)
-        launch_wave<false, 10236, true>(a, grid, opts.steal, stream);
-    else if (cg && count)
-        launch_wave<true, 5088, true>(a, grid, opts.steal, stream);
+    if (a.t.rgb_refl && cg)  // rgbprofile: three lookups per record, FromRGB into the group's bands
+        launch_wave_rgb_cg(a, grid, count, wide, opts.steal, stream);
+    else if (a.t.rgb_refl)
+        launch_wave_rgb(a, grid, count, wide, opts.steal, stream);
     else if (cg)
-        launch_wave<false, 5088, true>(a, grid, opts.steal, stream);
-    else if (count && wide)
-        launch_wave<true, 10236>(a, grid, opts.steal, stream);
-    else if (count)
-        launch_wave<true, 5088>(a, grid, opts.steal, stream);
-    else if (wide)
-        launch_wave<false, 10236>(a, grid, opts.steal, stream);
+        launch_wave_cg(a, grid, count, wide, opts.steal, stream);
     else
-        launch_wave<false, 5088>(a, grid, opts.steal, stream);
+        launch_wave_plain(a, grid, count, wide, opts.steal, stream);
     MPSS_HIP(hipGetLastError());
 }
 
@@ -555,6 +383,25 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     bt.leaf_r2 = (t.leaf_r2.ptr && t.leaf_r2_error == max_error) ? t.leaf_r2.ptr : nullptr;
     bt.cg = p.cg;
     bt.cg_half = p.cg_half;
+    for (int g = 0; g < kGroups; ++g)
+        for (int s2 = 0; s2 < 4; ++s2) bt.lband[g][s2] = p.groups.band[g][s2];
+    bt.rgb_refl = nullptr;
+    if (p.rgb_refl.ptr) {  // rgbprofile: rows 0..2 (R, G, B) in every group, one reach for all
+        float rmin = INFINITY, rmax = 0.f;
+        for (int k = 0; k < 3; ++k) {
+            rmin = std::min(rmin, p.host_rcp[k]);
+            rmax = std::max(rmax, p.host_rcp[k]);
+        }
+        for (int g = 0; g < kGroups; ++g) {
+            for (int s2 = 0; s2 < 4; ++s2) {
+                bt.lband[g][s2] = s2 < 3 ? s2 : -1;
+                bt.grcp[g][s2] = s2 < 3 ? p.host_rcp[s2] : 0.f;
+            }
+            bt.grcp_max[g] = rmax;
+            bt.groups.rcp_min[g] = rmin;
+        }
+        bt.rgb_refl = p.rgb_refl.ptr;  // (p.cg: the grid of the three profiles, set_rgb)
+    }
     if (!bt.leaf_r2)
         for (int g = 0; g < kGroups; ++g) bt.cg.lds_r2[g] = bt.cg_half.lds_r2[g] = 0.f;
     bt.L = p.L;
@@ -644,7 +491,8 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
     for (int c = 1; c < NB; ++c) rcp_min = rcp_[c] < rcp_min ? rcp_[c] : rcp_min;
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
     groups = make_band_groups(rcp_, snake);
-    build_common(tab);
+    rgb_refl.release();
+    build_common(tab, groups);
 }
 
 // The common grid (mo_band.h CommonGrid), on the host from the band tables:
@@ -670,8 +518,12 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
     for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
     const int kLdsFloats = 4 * (near_field + 3);
     if (L < 4) return false;
-    for (int c = 0; c < NB; ++c)
-        if (!(host_rcp[c] > 0.f) || !std::isfinite(host_rcp[c])) return false;  // no uniform grid to resample
+    for (int g = 0; g < kGroups; ++g)
+        for (int j = 0; j < 4; ++j) {
+            const int c = groups.band[g][j];
+            if (c >= 0 && (!(host_rcp[c] > 0.f) || !std::isfinite(host_rcp[c])))
+                return false;  // no uniform grid to resample
+        }
     bool any = false;
     for (int g = 0; g < kGroups; ++g) {
         float rg = INFINITY;
@@ -756,43 +608,74 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             const float *T = tab + (size_t)c * L;
             return (float)((1.0 - t) * (double)T[sidx] + t * (double)T[sidx + 1]);
         };
-        // the accurate range: the rows end a cell before the first band knot off by > kCgRelTol
-        const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor((double)u0f) - 1);
-        double ubad = (double)(L - 1);
+        // The row range: every band knot past the near field (s >= u0lim r_j - 1) whose rows value is
+        // off by more than kCgRelTol of |T[s]| (unfloored: a zero or a sign change counts) is "bad";
+        // the rows serve the longest stretch of u between bad knots, a grid cell of margin either
+        // side (the rows' error inside a cell is bounded by that at the knots in it), capped at
+        // kCgMaxRows rows. Usually the first stretch, from the near field's end; for bands of widely
+        // different reach (the rgbprofile's R, G, B: the shortest reach's knots are much denser than
+        // the grid, so it is off from the start) one past its end -- there tau's range test makes it
+        // exactly 0, as its rows hold.
+        auto knot_err = [&](int j, int k) -> double {  // relative error at band j's knot k, inf = bad
+            const float *T = tab + (size_t)groups.band[g][j] * L;
+            const double u = (double)k / r[j];
+            const int64_t ui = (int64_t)std::floor(u);
+            const double t = u - (double)ui;
+            const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
+            const double err = std::fabs(approx - (double)T[k]);
+            const bool sign_ok = T[k] != 0.f && (T[k] > 0.f) == (T[k + 1] > 0.f) && T[k + 1] != 0.f;
+            return (!sign_ok || err > kCgRelTol * std::fabs((double)T[k])) ? INFINITY : err;
+        };
+        std::vector<double> bad;
         for (int j = 0; j < 4; ++j) {
+            if (groups.band[g][j] < 0) continue;
+            for (int k = std::max(0, (int)std::floor((double)u0f * r[j]) - 1); k < L - 1; ++k)
+                if (knot_err(j, k) == INFINITY) bad.push_back((double)k / r[j]);
+        }
+        bad.push_back((double)(L - 1));
+        std::sort(bad.begin(), bad.end());
+        double start = u0f, ubad = u0f, best = -1.0;
+        {
+            double from = u0f;  // the current stretch's first servable u
+            for (const double ub : bad) {
+                if (ub >= from) {
+                    const double len = std::min(std::floor(ub) - 1.0, from + (double)kCgMaxRows) - from;
+                    if (len > best) {
+                        best = len;
+                        start = from;
+                        ubad = ub;
+                    }
+                }
+                from = std::max(from, std::floor(ub) + 2.0);
+            }
+        }
+        for (int j = 0; j < 4; ++j) {  // the error over the knots the rows serve
             const int c = groups.band[g][j];
             if (c < 0) continue;
             const float *T = tab + (size_t)c * L;
             double l1 = 0.0, emax = 0.0, esum = 0.0;
             for (int k = 0; k < L; ++k) l1 += std::fabs(T[k]);
-            const int s_lo = std::max(0, (int)std::floor((double)u0f * r[j]) - 1);
-            for (int k = s_lo; k < L - 1; ++k) {
+            for (int k = std::max(0, (int)std::floor(start * r[j]) - 1); k < L - 1; ++k) {
                 const double u = (double)k / r[j];
+                if (u < start) continue;
                 if (u >= ubad) break;
-                const int64_t ui = (int64_t)std::floor(u);
-                const double t = u - (double)ui;
-                const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
-                const double err = std::fabs(approx - (double)T[k]);
-                const bool sign_ok = T[k] != 0.f && (T[k] > 0.f) == (T[k + 1] > 0.f) && T[k + 1] != 0.f;
-                if (!sign_ok || err > kCgRelTol * std::fabs((double)T[k])) {
-                    ubad = std::min(ubad, u);
-                    break;
-                }
-                emax = std::max(emax, err / std::fabs((double)T[k]));
-                esum += err;
+                const double e = knot_err(j, k);
+                emax = std::max(emax, e / std::fabs((double)T[k]));
+                esum += e;
             }
             cg_rel_err[c] = (float)emax;
             cg_l1_err[c] = (float)(l1 > 0.0 ? esum / l1 : 0.0);
         }
+        const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
         int64_t u1 = (int64_t)std::floor(ubad) - 1;
         u1 = std::min<int64_t>(u1, ubase + kCgMaxRows);
         u1 = std::min<int64_t>(u1, (int64_t)L - 1);
-        if (u1 <= (int64_t)u0f + 1) {  // no accurate range: the exact tables past the near field
-            cg.ubase[g] = (uint32_t)ubase;
-            cg.u1lim[g] = u0f;
+        cg.ubase[g] = (uint32_t)ubase;
+        if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
+            cg.u1lim[g] = cg.u1start[g] = u0f;
             continue;
         }
-        cg.ubase[g] = (uint32_t)ubase;
+        cg.u1start[g] = (float)start;  // (u0f, or an integer below 2^24)
         cg.u1lim[g] = (float)u1;  // lanes with u < u1 read rows u0 <= u1 - 1 (values R(u0), R(u0 + 1))
         for (int64_t u = ubase; u < u1; ++u) {
             float v[4][2];
@@ -809,18 +692,32 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
     return any;
 }
 
-void DeviceProfile::build_common(const float *tab) {
+void DeviceProfile::set_rgb(const float *tab) {
+    static const float refl[7][NB] = {MPSS_BAND_RGBREFL2SPECTWHITE_INIT, MPSS_BAND_RGBREFL2SPECTCYAN_INIT,
+                                      MPSS_BAND_RGBREFL2SPECTMAGENTA_INIT, MPSS_BAND_RGBREFL2SPECTYELLOW_INIT,
+                                      MPSS_BAND_RGBREFL2SPECTRED_INIT, MPSS_BAND_RGBREFL2SPECTGREEN_INIT,
+                                      MPSS_BAND_RGBREFL2SPECTBLUE_INIT};
+    rgb_refl.upload(&refl[0][0], 7 * NB);
+    // the common grid of the R, G, B profiles (rows 0..2, the same three slots in every group: the
+    // sharded gather reads them in band_tree's lband order)
+    BandGroups g3 = groups;
+    for (int g = 0; g < kGroups; ++g)
+        for (int j = 0; j < 4; ++j) g3.band[g][j] = j < 3 ? j : -1;
+    build_common(tab, g3);
+}
+
+void DeviceProfile::build_common(const float *tab, const BandGroups &slots) {
     ctab.release();
     ctab_half.release();
     std::vector<float4> h;
     float rel[NB], l1[NB];
-    if (build_common_grid(tab, L, host_rcp, groups, cg_half, h, rel, l1, 5088)) {
+    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, rel, l1, 5088)) {
         ctab_half.upload(h.data(), h.size());
         cg_half.tab = ctab_half.ptr;
     } else {
         cg_half.on = 0;
     }
-    if (!build_common_grid(tab, L, host_rcp, groups, cg, h, cg_rel_err, cg_l1_err, 10236)) {
+    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err, cg_l1_err, 10236)) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }

@@ -43,7 +43,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 10; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 11; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
                                           // 6: GPU octree build (octree_on_host), mpss_octree_export;
@@ -54,6 +54,8 @@ int mpss_abi_version(void) { return 10; }  // 2: poisson point finder, infinite 
                                           // 9: GPU tessellation (tessellate_on_host), size bounds
                                           // 10: mo_common_grid, mpss_get_gather_info, common-grid
                                           //     lane-record counts in mpss_render_stats
+                                          // 11: rgbprofile through the sharded gather (its own common
+                                          //     grid), mpss_host_common_grid u1start / rgb mode
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -180,12 +182,16 @@ int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len,
 }
 
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
-                          int32_t *bands, float *rg, float *u0lim, float *u1lim, uint32_t *row0, uint32_t *ubase,
-                          float *rel_err, float *l1_err, int *ok) {
+                          int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
+                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok) {
     return guarded([&] {
         require(table && rcp && ok, "mpss_host_common_grid: null argument");
         require(L >= 2 && L < (1u << 24), "mpss_host_common_grid: L out of range");
-        const BandGroups g = make_band_groups(rcp, snake != 0);
+        require(snake >= 0 && snake <= 2, "mpss_host_common_grid: snake must be 0, 1 or 2");
+        BandGroups g = make_band_groups(rcp, snake == 1);
+        if (snake == 2)  // rgbprofile: rows 0..2 (R, G, B) in every group (DeviceProfile::set_rgb)
+            for (int k = 0; k < kGroups; ++k)
+                for (int j = 0; j < 4; ++j) g.band[k][j] = j < 3 ? j : -1;
         CommonGrid cg;
         std::vector<float4> h;
         float rel[NB], l1[NB];
@@ -201,6 +207,7 @@ int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int 
             if (rg) rg[k] = cg.rg[k];
             if (u0lim) u0lim[k] = cg.u0lim[k];
             if (u1lim) u1lim[k] = cg.u1lim[k];
+            if (u1start) u1start[k] = cg.u1start[k];
             if (row0) row0[k] = cg.row0[k];
             if (ubase) ubase[k] = cg.ubase[k];
         }

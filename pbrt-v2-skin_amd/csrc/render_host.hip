@@ -629,8 +629,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         for (size_t i = 0; i < materials_.size(); ++i)
             if (!materials_[i]->dipole)
                 sss.push_back(SssMat{(int)i, materials_[i].get(),
-                                     materials_[i]->rgb ? nullptr
-                                                        : &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
+                                     &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
     sc.have_octree = sss.empty() ? 0 : 1;
     if (replay) {
@@ -803,10 +802,13 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                     grow(ws->st, ws->st_n, lanes, 1);
                     inf_st = ws->st.ptr;
                 }
-                time_begin(timing, stream, ev);
-                if (sc.any_tex)
+                if (sc.any_tex) {
+                    time_begin(timing, stream, ev);
                     hipLaunchKernelGGL(shade_tex_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, stream, sc,
                                        rec, spp, seed, (int)nh);
+                    time_end(timing, stream, ev, 5, timed);
+                }
+                time_begin(timing, stream, ev);
                 if (nlights > 0) {
                     hipLaunchKernelGGL(shade_direct_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0,
                                        stream, sc, rec, spp, seed, (int)nh, ns_max, terms, inf_st);
@@ -826,17 +828,10 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             }
             if (!sss.empty()) {
                 time_begin(timing, stream, ev);
-                for (const SssMat &s : sss) {
-                    if (s.m->rgb)  // Mo() rows in band order (the material's pos is the identity)
-                        launch_mo_rgb(dev_octree_, s.m->dev_rgb.ptr, s.m->dev_rgb_rcp.ptr, s.m->rgb_rcp,
-                                      s.m->profile.length, max_error, (int)nh, nullptr, ws->q.ptr, ws->count.ptr,
-                                      sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, (float *)ws->mo.ptr, 4 * kGroups,
-                                      nullptr, stream);
-                    else
-                        launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)nh, ws->q.ptr,
-                                       ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
-                                       ws->work.ptr, ws->perm.ptr, gopts, stream);
-                }
+                for (const SssMat &s : sss)  // (an rgbprofile material: FromRGB of its R, G, B lookups)
+                    launch_mo_band(dev_octree_, *s.layout, s.m->dev_profile, max_error, (int)nh, ws->q.ptr,
+                                   ws->count.ptr, ws->mo.ptr, sss.size() > 1 ? ws->hs.ptr : nullptr, s.id, counts,
+                                   ws->work.ptr, ws->perm.ptr, gopts, stream);
                 time_end(timing, stream, ev, 2, timed);
             }
             time_begin(timing, stream, ev);
@@ -918,9 +913,10 @@ mpss_render_stats Context::render_stats() {
         MPSS_HIP(hipEventElapsedTime(&ms, t.a, t.b));
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
-        double *dst[5] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film,
-                          &stats_.ms_direct};
-        int64_t *cnt[5] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film, &stats_.n_direct};
+        double *dst[6] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film,
+                          &stats_.ms_direct, &stats_.ms_tex};
+        int64_t *cnt[6] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film, &stats_.n_direct,
+                           &stats_.n_tex};
         *dst[t.kind] += ms;
         *cnt[t.kind] += 1;
     }

@@ -35,12 +35,12 @@ def _R(T, r, u, L):
     return np.where((f - r > L - 1) | (u >= L), 0.0, v)
 
 
-def _check_layout(tab, rcp, cg, tol=2e-6):
+def _check_layout(tab, rcp, cg, tol=2e-6, groups=None):
     """Groups, the LDS split, the pair rows against numpy, and that every band knot the rows serve
     is within tol of the band's own value (unfloored)."""
     L = tab.shape[1]
     T64 = tab.astype(np.float64)
-    for g, bands in enumerate(_groups(rcp)):
+    for g, bands in enumerate(groups or _groups(rcp)):
         slots = cg["bands"][g]
         assert sorted(b for b in slots if b >= 0) == sorted(int(b) for b in bands)
         rg = np.float32(rcp[bands].min())
@@ -52,7 +52,9 @@ def _check_layout(tab, rcp, cg, tol=2e-6):
         u0, u1, ub, r0 = cg["u0lim"][g], cg["u1lim"][g], int(cg["ubase"][g]), int(cg["row0"][g])
         if u1 <= u0:
             continue
-        assert ub == max(0, int(np.floor(u0)) - 1)
+        us = cg["u1start"][g]  # the rows serve u in [u1start, u1lim)
+        assert us >= u0 and us < u1
+        assert ub == max(0, int(np.floor(us)) - 1)
         n = int(u1) - ub
         rows = cg["rows"][r0:r0 + n].astype(np.float64)
         assert len(rows) == n
@@ -65,10 +67,10 @@ def _check_layout(tab, rcp, cg, tol=2e-6):
             want1 = _R(T64[c], r[j], u + 1, L).astype(np.float32)
             np.testing.assert_array_equal(rows[:, 2 * j].astype(np.float32), want0)
             np.testing.assert_array_equal(rows[:, 2 * j + 1].astype(np.float32), want1)
-            # the knots the rows serve: u in [u0lim, u1lim)
-            k = np.arange(int(np.floor(u0 * r[j])), L - 1)
+            # the knots the rows serve: u in [u1start, u1lim)
+            k = np.arange(int(np.floor(us * r[j])), L - 1)
             uk = k / r[j]
-            sel = (uk >= u0) & (uk < u1)
+            sel = (uk >= us) & (uk < u1)
             k, uk = k[sel], uk[sel]
             ui = np.floor(uk).astype(np.int64) - ub
             t = uk - np.floor(uk)
@@ -104,9 +106,31 @@ def test_common_grid_of_the_benched_skin_profile(mpss):
     _check_layout(tab, rcp, cg)
 
 
+def test_common_grid_of_the_rgb_profile(mpss):
+    """rgbprofile at C2's length (desiredlength 512): the R, G, B profiles in slots 0..2 of every
+    group, grid = G's (the longest reach). B reaches ~15x less far in d^2 and its knots are that much
+    denser than the grid (off from the start), so the rows serve the stretch past B's end (u1start:
+    there B is exactly 0 by tau's range test) and R and G within the bound."""
+    import oracle_lib
+    from test_rgbprofile import rgb_layers
+    mua, musp, th, eta = oracle_lib.skin_layers(0.3, 40e6, 0.5, 0.5, 0.5, 0.5, (0.25e6, 20e6), (1.4, 1.4))
+    ra, rs = rgb_layers(mua, musp)
+    tab, rcp, _, _ = oracle_lib.compute_profile(ra, rs, eta, th, desired_length=512)
+    cg = mpss.host_common_grid(tab, rcp, rgb=True)
+    assert cg["ok"]
+    assert np.all(cg["bands"] == np.array([0, 1, 2, -1]))
+    reach_b = (tab.shape[1] - 1) / np.float64(rcp[2]) * np.float64(rcp[:3].min())
+    assert np.all(cg["u1start"] > reach_b) and np.all(cg["u1start"] > cg["u0lim"])
+    assert np.all(cg["u1lim"] - cg["u1start"] > 5 * cg["u1start"])  # (7926 .. 64585 of G's 119765)
+    rows = cg["rows"].reshape(8, -1, 8)
+    assert np.all(rows[:, 2:, 4:] == 0)  # B past its end (its last segment continued one row) and slot 3
+    assert cg["rel_err"][:3].max() <= 2e-6 and cg["rel_err"][2] == 0
+    _check_layout(tab, rcp, cg, groups=[[0, 1, 2]] * 8)
+
+
 def test_common_grid_of_a_rough_table(mpss):
     """A table that is rough on the groups' grids: whatever rows are built serve only knots within
-    the bound (here none past the near field)."""
+    the bound (here none where a resampled band is live)."""
     rng = np.random.default_rng(5)
     L = 4096
     x = np.arange(L) / L
@@ -114,7 +138,14 @@ def test_common_grid_of_a_rough_table(mpss):
     rcp = ((L - 1) / np.linspace(0.01, 0.05, 30)).astype(np.float32)
     cg = mpss.host_common_grid(tab, rcp)
     _check_layout(tab, rcp, cg)
-    assert np.all(cg["u1lim"] - cg["u0lim"] < 64)
+    # no stretch where a resampled band is live: rows (if any) only past the end of every band but
+    # the grid's own (whose rows are its table)
+    for g in range(8):
+        if cg["u1lim"][g] <= cg["u0lim"][g]:
+            continue
+        for c in cg["bands"][g]:
+            if c >= 0 and rcp[c] != cg["rg"][g]:
+                assert (L - 1) / np.float64(rcp[c]) * np.float64(cg["rg"][g]) <= cg["u1start"][g]
 
 
 def test_common_grid_equal_spacing_is_exact(mpss):

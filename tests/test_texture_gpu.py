@@ -79,3 +79,31 @@ def test_texture_changes_the_image(mpss, oracle):
     assert np.abs(img1[..., 1] - img0[..., 1]).max() > 1e-3 * np.abs(img0[..., 1]).max()
     ctx0.close()
     ctx1.close()
+
+
+def test_textured_c2_window_parity(mpss, oracle):
+    """scenes/skin_textured.pbrt at the benched C2 parameters (1024x1024, 64 spp, desiredlength 512,
+    minsampledistance 0.0015): imagemap albedo (gamma 2.2, scale 2, clamp) and bumpmap on the head,
+    a 32x32 cheek window through the production path vs the oracle; the tessellation with the bumped
+    normals bit-exact."""
+    import torch
+    import oracle_lib
+    from mpss import pbrtscene
+    from test_configs_gpu import _windows
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin_textured.pbrt"))
+    assert (sc.xres, sc.spp) == (1024, 64)
+    m = sc.materials[0]
+    assert m["albedo_tex"]["texels"] is not None and m["bump_tex"]["texels"] is not None
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=1)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    assert pts.tobytes() == o.tessellate().tobytes()
+    o.set_octree(pts, ctx.irradiance())
+    x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
+    got = _render_gpu(torch, ctx, sc, x0, x1, y0, y1, 7)
+    ref = o.render_tile(sc.spp, 7, x0, x1, y0, y1, nthreads=oracle_lib.nthreads())
+    _check(got, ref)
+    assert (ref[..., 1] > 0).all()
+    o.close()
+    ctx.close()

@@ -15,6 +15,7 @@
 #   kt[=CFG]          rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG[_CFG]/kt
 #   pmc[=CFG]         rocprofv3 --pmc passes of the bench (one counter set per run, $PMC_SETS
 #                     overrides the default sets, one per line)   -> gpurun_out/prof_TAG[_CFG]/pmc_i
+# $BENCH_ARGS: extra bench.py arguments for kt and pmc (e.g. "--rgb-profile").
 # Afterwards `python tools/summarize_prof.py TAG` writes profiles/TAG_kernel_stats.csv + TAG_pmc.json.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -73,7 +74,7 @@ for step in "$@"; do
       steps=(--steps 3 --warmup 1)
       [ $cfg = c5 ] && steps=(--steps 1 --warmup 1)
       echo "== kernel trace $cfg"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/kt -o run --output-format csv -- python3 bench.py --config $cfg "${steps[@]}" --no-cpu-baseline > $d/kt.log 2>&1 || fail kt $d/kt.log 30
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/kt -o run --output-format csv -- python3 bench.py --config $cfg "${steps[@]}" --no-cpu-baseline $BENCH_ARGS > $d/kt.log 2>&1 || fail kt $d/kt.log 30
       grep '"metric"' $d/kt.log > $d/kt_bench.jsonl || true ;;
     pmc)
       cfg=${arg:-c2}
@@ -84,7 +85,7 @@ for step in "$@"; do
         [ -z "$line" ] && continue
         i=$((i+1))
         echo "== pmc $cfg $i: $line"
-        timeout -s KILL 300 rocprofv3 --pmc $line -d $d/pmc_$i -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline > $d/pmc_$i.log 2>&1 || fail "pmc pass $i" $d/pmc_$i.log 20
+        timeout -s KILL 300 rocprofv3 --pmc $line -d $d/pmc_$i -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline $BENCH_ARGS > $d/pmc_$i.log 2>&1 || fail "pmc pass $i" $d/pmc_$i.log 20
       done <<< "${PMC_SETS:-$DEFAULT_PMC}" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
