@@ -84,6 +84,11 @@ def parse(argv=None):
                     help="scene file (scenes/skin_textured.pbrt: C2 with imagemap albedo and bump)")
     ap.add_argument("--rgb-profile", action="store_true",
                     help="LayeredSkin \"rgbprofile\" on (ComputeRGBMultipoleProfile: three profiles, FromRGB)")
+    ap.add_argument("--sampler", choices=("hash", "reference"), default="hash",
+                    help="mpss_config.sampler: hash (default, counter-based (0,2) sequences) or reference (pbrt's "
+                         "per-task MT19937 streams replayed, replay_cores emulated cores; the window tables are "
+                         "generated per render batch inside the timed region)")
+    ap.add_argument("--replay-cores", type=int, default=8)
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None, help="tile size (default 128; 64 for c3 on several GPUs)")
@@ -149,6 +154,10 @@ def build_scene(a, label_cfg, local):
     kw["mo_common_grid"] = a.common_grid
     if a.near_field:
         kw["mo_near_field"] = a.near_field
+    if a.sampler == "reference":
+        import mpss
+        kw["sampler"] = mpss.SAMPLER_REFERENCE
+        kw["replay_cores"] = a.replay_cores
     ctx = pbrtscene.build_context(sc, device=local, **kw)
     t_mat = time.perf_counter() - t0
     if pts is not None:
@@ -288,7 +297,7 @@ def main(a):
     sss_per_step, traced_per_step = float(sss[0].item()), float(sss[1].item())
     # dominant kernel + Mo gather roofline (per-launch averages over the timed region, this rank)
     kern = {"primary": (st["ms_camera"], st["n_camera"]), "shade_direct": (st["ms_direct"], st["n_direct"]),
-            "shade_tex": (st["ms_tex"], st["n_tex"]),
+            "shade_tex": (st["ms_tex"], st["n_tex"]), "replay": (st["ms_replay"], st["n_replay"]),
             "mo_band": (st["ms_shade"], st["n_shade"]),
             "film": (st["ms_film"], st["n_film"])}
     dom = max(kern, key=lambda k: kern[k][0])
@@ -356,13 +365,15 @@ def main(a):
                 "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": scaling,
                 "vs_baseline": None, "dtype": "f32",
                 "data": "synthetic (reconstructed %s, head.pbrt mesh%s%s)" % (
-                    os.path.basename(a.scene), ", subdivided" if subdiv else "", ", rgbprofile" if a.rgb_profile else ""),
+                    os.path.basename(a.scene), ", subdivided" if subdiv else "", ", rgbprofile" if a.rgb_profile else "")
+                    + (", pbrt's sampler replayed" if a.sampler == "reference" else ""),
                 "config": {"workload": "%s (%dx%d, %d spp%s), %dx%d tiles%s%s"
                            % (label, sc.xres, sc.yres, sc.spp, " per GPU" if scaling == "weak" else "", T, T,
                               ", independent whole frames, one per GPU" if frames == world and world > 1 else
                               (" dealt by cost" if world > 1 else ""),
                               ", one RCCL film gather per step" if world > 1 else ""),
                            "scene": os.path.basename(a.scene), "rgb_profile": bool(a.rgb_profile),
+                           "sampler": a.sampler if a.sampler == "hash" else "reference (%d cores)" % a.replay_cores,
                            "frames_per_step": frames, "triangles": int(sum(len(me["indices"]) for me in sc.meshes)),
                            "irradiance_points": n_points, "preprocess_s": round(t_pre, 3),
                            "material_build_s": round(t_materials, 3), "tile_deal_s": round(t_deal, 3),

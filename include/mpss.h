@@ -79,7 +79,10 @@ typedef struct {
     int64_t max_batch_samples; /* camera samples per render batch (default 1 << 26: a whole C2 frame
                                   in two batches, one Mo() launch each); the workspace grows to the
                                   largest batch rendered, sized for the worst case (every sample a
-                                  hit): ~280 B/sample, 18.8 GB for a full 2^26 batch of the 288 GB */
+                                  hit): ~280 B/sample, 18.8 GB for a full 2^26 batch of the 288 GB;
+                                  at least 2^10. The reference sampler also closes a batch before
+                                  its window table (the pieces' bounding box x spp x 22 floats for
+                                  skin.pbrt) passes 2^29 floats */
     int use_poisson_point_finder; /* "usepoissonpointfinder" = false: SurfacePoints by random-walk
                                   dart throwing (FindPoissonPointDistribution) instead of tessellation */
     int sampler;               /* MPSS_SAMPLER_HASH (default): counter-hash scrambled (0,2) sequences, a
@@ -312,6 +315,8 @@ typedef struct {
     int64_t mo_row_lane_records, mo_lds_lane_records, mo_table_lane_records;
     double ms_tex;        /* texture lookups at the camera hits (albedo / bump imagemaps; shade_tex) */
     int64_t n_tex;
+    double ms_replay;     /* the reference sampler's values of each batch's window (replay_window) */
+    int64_t n_replay;
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal (0, 1 or 2, as mpss_config) after creation

@@ -78,6 +78,12 @@ struct RenderWorkspace {
     DevBuf<float4> q, mo, ha, hb, xyz, alb, frame, st;
     DevBuf<unsigned char> terms;
     DevBuf<float> ld;
+    // reference-sampler replay: the batch's window table and the render tasks' stream cursors
+    // (render.h ReplayCursors; valid for rp_key = {scene generation, spp, tasks})
+    DevBuf<float> rp_table;
+    DevBuf<uint32_t> rp_mt;
+    DevBuf<int> rp_pix, rp_mti;
+    uint64_t rp_key[3] = {~0ull, 0, 0};
     int64_t n = 0, rec_n = 0, hits = 0, tex_hits = 0, terms_n = 0, st_n = 0, px = 0;
     hipEvent_t done = nullptr;
     int device = 0;
@@ -151,10 +157,14 @@ private:
     void upload_scene();
     RenderScene render_scene() const;
     int first_bssrdf_material() const;
-    // reference-sampler replay (mpss_config.sampler): sample table of the whole sample extent
-    void ensure_replay_table(int spp);
-    DevBuf<float> replay_vals_;
-    int replay_spp_ = 0, replay_k_ = kReplayImage;
+    // reference-sampler replay (mpss_config.sampler): floats per camera sample in the window tables,
+    // and the scene generation the workspaces' task cursors belong to (upload_scene bumps it)
+    int replay_k_ = kReplayImage;
+    uint64_t scene_gen_ = 0;
+    // the window [x0, x1) x [y0, y1) of the sample extent at spp into ws->rp_table (the cursors in ws
+    // reset when the scene, spp or task count changed); on `stream`
+    void replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp, int x0, int x1, int y0, int y1,
+                       hipStream_t stream);
     SceneData scene_;
     bool scene_dirty_ = true, have_points_ = false;
     std::vector<SurfacePoint> points_;

@@ -72,21 +72,39 @@ struct RenderScene {
     int any_tex;      // some material has an albedo texture or a bump map: shade_tex_kernel runs
     float raster_to_camera[16], camera_to_world[16];
     float dx_camera[3], dy_camera[3];  // PerspectiveCamera dxCamera / dyCamera (perspective.cpp:47-48)
-    // reference-sampler replay (replay.h); null: the counter-hash sampler
-    const float *replay;      // [((y * replay_w + x) * replay_spp + s) * replay_k + ...] sample values
-    int replay_k, replay_w, replay_spp;
+    // reference-sampler replay (replay.h); null: the counter-hash sampler. The sample values of one
+    // render batch's window [replay_x0, replay_x0 + replay_w) x [replay_y0, ...) (replay_gen.hip),
+    // column-major: value k of camera sample s of window pixel p at [(k * replay_npix + p) *
+    // replay_spp + s] (a wave's lanes, consecutive samples of one pixel, read consecutive floats)
+    const float *replay;
+    int replay_k, replay_spp, replay_x0, replay_y0, replay_w;
+    int64_t replay_npix;
     const uint32_t *irr_scr;  // [point][light][2] IrradianceTask Sample02 scrambles
 };
 
-// The GPU replay of the reference's render-task streams (replay.h): one lane per task, sample
-// values of the film's whole sample extent ((xres + 1) x (yres + 1) pixels x spp) into vals.
-// mt: 624 x ntasks words of MT state. li_draws: RNG values Li consumes per camera-ray hit.
-struct ReplayGen {
-    int ntasks, spp, K, li_draws;
+// The GPU replay of the reference's render-task streams for one window of the sample extent
+// (replay_gen.hip): one wave per SamplerRendererTask whose sub-window meets the window, resuming
+// the task's MT19937 stream from its cursor (the next pixel of its sub-window, in row order) or
+// from RNG(task) when the window lies behind it. The cursors persist between windows, so a frame
+// rendered in row order replays every stream once. mt: [ntasks][624] states; cur_pix: the next
+// pixel ordinal per task (-1: not seeded); cur_mti: the state's word index.
+struct ReplayCursors {
     uint32_t *mt;
-    float *vals;
+    int *cur_pix, *cur_mti;
 };
-__global__ void replay_render_kernel(RenderScene sc, ReplayGen g);
+struct ReplayWindow {
+    int ntasks, nx;            // the task grid (ComputeSubWindow: nx x (ntasks / nx))
+    int xo0, nxr, yo0, nyr;    // the tasks meeting the window: columns xo0.., rows yo0..
+    int x0, y0, w, h;          // the window (pixels of the sample extent)
+    int spp, K, li_draws, nmax;  // nmax: the largest light-sample count (array length)
+    ReplayCursors cur;
+    float *out;                // the window table (RenderScene::replay layout)
+};
+// Launches the generation on `stream` (the host picks the task ranges: replay_window_tasks).
+void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStream_t stream);
+// The task grid and the task columns / rows meeting [x0, x1) x [y0, y1) of the (xres + 1) x
+// (yres + 1) sample extent.
+void replay_window_tasks(int xres, int yres, int ntasks, int x0, int x1, int y0, int y1, ReplayWindow &w);
 // IrradianceTask streams: scr[(i * nlights + l) * 2 + {0, 1}] for points i < n
 __global__ void replay_irradiance_kernel(int n, int nlights, int ntasks, uint32_t *mt, uint32_t *scr);
 

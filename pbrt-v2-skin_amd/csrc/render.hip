@@ -16,6 +16,7 @@
 #include <climits>
 
 #include "../../data/spectral_bands.h"
+#include "bvh_trace.h"
 #include "geom.h"
 #include "tessellate.h"
 
@@ -38,27 +39,10 @@ __constant__ float kRefl[7][NB] = {MPSS_BAND_RGBREFL2SPECTWHITE_INIT,  MPSS_BAND
 
 namespace {
 
-constexpr int kStack = 48;  // BVH traversal stack depth (host checks the tree depth)
+constexpr int kStack = kTraceStack;
 
 // ------------------------------------------------------------------ BVH traversal (per lane)
-__device__ __forceinline__ bool bbox_hit(const BvhNode &n, V3 o, V3 inv, const int neg[3], float mint, float maxt) {
-    // bvh.cpp:126-148 (IntersectP of a node's bounds)
-    const float *lo = n.bmin, *hi = n.bmax;
-    float tmin = ((neg[0] ? hi[0] : lo[0]) - o.x) * inv.x;
-    float tmax = ((neg[0] ? lo[0] : hi[0]) - o.x) * inv.x;
-    const float tymin = ((neg[1] ? hi[1] : lo[1]) - o.y) * inv.y;
-    const float tymax = ((neg[1] ? lo[1] : hi[1]) - o.y) * inv.y;
-    if ((tmin > tymax) || (tymin > tmax)) return false;
-    if (tymin > tmin) tmin = tymin;
-    if (tymax < tmax) tmax = tymax;
-    const float tzmin = ((neg[2] ? hi[2] : lo[2]) - o.z) * inv.z;
-    const float tzmax = ((neg[2] ? lo[2] : hi[2]) - o.z) * inv.z;
-    if ((tmin > tzmax) || (tzmin > tmax)) return false;
-    if (tzmin > tmin) tmin = tzmin;
-    if (tzmax < tmax) tmax = tzmax;
-    return (tmin < maxt) && (tmax > mint);
-}
-
+// (bbox_hit, trace_any: bvh_trace.h)
 struct Hit {
     float t, b1, b2;
     int tri;    // global triangle id (>= 0) or -1 - light index, or INT_MIN for a miss
@@ -113,43 +97,6 @@ __device__ Hit trace_closest(const RenderScene &sc, V3 o, V3 d, float mint, floa
         }
     }
     return h;
-}
-
-// Scene::IntersectP (bvh.cpp:442-488 + Sphere::IntersectP)
-__device__ bool trace_any(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, int *stk, int sstride) {
-    for (int l = 0; l < sc.nlights; ++l) {
-        float t;
-        if (!sc.lights[l].kind && sphere_intersect(sc.lights[l].s, o, d, mint, maxt, t, nullptr)) return true;
-    }
-    const V3 inv = V3{1.f / d.x, 1.f / d.y, 1.f / d.z};
-    const int neg[3] = {inv.x < 0.f, inv.y < 0.f, inv.z < 0.f};
-    int todo = 0, node = 0;
-    for (;;) {
-        const BvhNode n = sc.bvh[node];
-        if (bbox_hit(n, o, inv, neg, mint, maxt)) {
-            if (n.nprims > 0) {
-                for (int i = 0; i < n.nprims; ++i) {
-                    const TriRec tr = sc.tris[n.offset + i];
-                    float t, b1, b2;
-                    if (tri_intersect(o, d, mint, maxt, V3{tr.p1[0], tr.p1[1], tr.p1[2]},
-                                      V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2))
-                        return true;
-                }
-                if (todo == 0) break;
-                node = stk[--todo * sstride];
-            } else if (neg[n.axis]) {
-                stk[todo++ * sstride] = node + 1;
-                node = n.offset;
-            } else {
-                stk[todo++ * sstride] = n.offset;
-                node = node + 1;
-            }
-        } else {
-            if (todo == 0) break;
-            node = stk[--todo * sstride];
-        }
-    }
-    return false;
 }
 
 // Sphere::Intersect out of line: its double-precision atan2 (the phi test) would otherwise set the
@@ -678,18 +625,18 @@ __global__ __launch_bounds__(256) void poisson_walk_kernel(RenderScene sc, Poiss
     count[i] = n;
 }
 
-// The replay-table row of camera sample s of pixel (px, py) (replay.h layout)
-__device__ __forceinline__ const float *replay_row(const RenderScene &sc, int px, int py, int s) {
-    return sc.replay + (((int64_t)py * sc.replay_w + px) * sc.replay_spp + s) * sc.replay_k;
+// Value k of camera sample s of pixel (px, py) in the batch's replay window (RenderScene::replay)
+__device__ __forceinline__ float replay_val(const RenderScene &sc, int px, int py, int s, int k) {
+    const int64_t p = (int64_t)(py - sc.replay_y0) * sc.replay_w + (px - sc.replay_x0);
+    return sc.replay[((int64_t)k * sc.replay_npix + p) * sc.replay_spp + s];
 }
 
 // The image sample of camera sample s of pixel (px, py): LDPixelSample's imageX = xPos + u
 __device__ __forceinline__ void image_sample(const RenderScene &sc, uint32_t seed, int px, int py, int s, float &X,
                                              float &Y) {
     if (sc.replay) {
-        const float *r = replay_row(sc, px, py, s);
-        X = (float)px + r[0];
-        Y = (float)py + r[1];
+        X = (float)px + replay_val(sc, px, py, s, 0);
+        Y = (float)py + replay_val(sc, px, py, s, 1);
         return;
     }
     const uint32_t pix = (uint32_t)py * (uint32_t)sc.xres + (uint32_t)px;
@@ -947,13 +894,13 @@ __global__ __launch_bounds__(256) void shade_direct_kernel(RenderScene sc, Sampl
     // LightSample(sample, offsets, j) / BSDFSample(sample, offsets, j) (light.cpp, reflection.cpp)
     float lu0, lu1, ubc, ub0, ub1;
     if (sc.replay) {
-        const float *r = replay_row(sc, (int)(pix % (uint32_t)sc.xres), (int)(pix / (uint32_t)sc.xres), s) +
-                         L.replay_off + j * kReplayPerLightSample;
-        lu0 = r[0];
-        lu1 = r[1];
-        ubc = r[2];
-        ub0 = r[3];
-        ub1 = r[4];
+        const int px = (int)(pix % (uint32_t)sc.xres), py = (int)(pix / (uint32_t)sc.xres);
+        const int k = L.replay_off + j * kReplayPerLightSample;
+        lu0 = replay_val(sc, px, py, s, k);
+        lu1 = replay_val(sc, px, py, s, k + 1);
+        ubc = replay_val(sc, px, py, s, k + 2);
+        ub0 = replay_val(sc, px, py, s, k + 3);
+        ub1 = replay_val(sc, px, py, s, k + 4);
     } else {
         const uint32_t xr = (spp & (spp - 1)) == 0 ? (hash3(seed, pix, 16u * l + 9u) & (uint32_t)(spp - 1)) : 0u;
         const uint32_t nidx = (uint32_t)(s ^ (int)xr) * (uint32_t)ns + (uint32_t)j;
@@ -1515,127 +1462,7 @@ __global__ __launch_bounds__(256) void probe_kernel(RenderScene sc, int x0, int 
 }
 
 // ------------------------------------------------------------------ reference-sampler replay
-// One lane per SamplerRendererTask (replay.h): RNG(task) through LDPixelSample for every pixel
-// of the task's sub-window, writing the sample values the render kernels consume into the
-// replay table, and the camera ray of every sample (only whether it hits: Li's 6 draws).
-namespace {
-// Shuffle(samp, count, dims, rng) of `count` blocks of `dims` floats that sit `bstride` floats
-// apart (montecarlo.h:183-189): count draws
-__device__ void replay_shuffle(Mt19937 &rng, float *base, int count, int dims, int64_t bstride) {
-    for (int i = 0; i < count; ++i) {
-        const int other = i + (int)(rng.next() % (uint32_t)(count - i));
-        if (other == i) continue;
-        float *a = base + (int64_t)i * bstride, *b = base + (int64_t)other * bstride;
-        for (int d = 0; d < dims; ++d) {
-            const float t = a[d];
-            a[d] = b[d];
-            b[d] = t;
-        }
-    }
-}
-// Shuffle of a light-sample array inside one camera sample's row: n elements of `dims` floats
-// at stride kReplayPerLightSample
-__device__ void replay_shuffle_elems(Mt19937 &rng, float *e0, int n, int dims) {
-    for (int j = 0; j < n; ++j) {
-        const int other = j + (int)(rng.next() % (uint32_t)(n - j));
-        if (other == j) continue;
-        float *a = e0 + j * kReplayPerLightSample, *b = e0 + other * kReplayPerLightSample;
-        for (int d = 0; d < dims; ++d) {
-            const float t = a[d];
-            a[d] = b[d];
-            b[d] = t;
-        }
-    }
-}
-}  // namespace
-
-__global__ __launch_bounds__(64) void replay_render_kernel(RenderScene sc, ReplayGen g) {
-    __shared__ int stk_all[kStack * 64];
-    int *stk = stk_all + threadIdx.x;
-    const int task = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (task >= g.ntasks) return;
-    const int ew = sc.xres + 1, eh = sc.yres + 1, spp = g.spp, K = g.K;
-    int x0, x1, y0, y1;
-    replay_sub_window(task, g.ntasks, 0, ew, 0, eh, x0, x1, y0, y1);
-    Mt19937 rng{g.mt + task, g.ntasks, 624};
-    rng.seed((uint32_t)task);
-    const V3 o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
-    for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) {
-            float *rows = g.vals + ((int64_t)y * ew + x) * spp * K;  // the pixel's spp rows
-            // image: LDShuffleScrambled2D(1, spp)
-            {
-                const uint32_t s0 = rng.next(), s1 = rng.next();
-                for (int i = 0; i < spp; ++i) {
-                    rows[(int64_t)i * K] = van_der_corput((uint32_t)i, s0);
-                    rows[(int64_t)i * K + 1] = sobol2((uint32_t)i, s1);
-                }
-                rng.skip(spp);  // one-element blocks: Shuffle(.., 1, 2) draws once and keeps the order
-                replay_shuffle(rng, rows, spp, 2, K);
-            }
-            rng.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
-            rng.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
-            // 1D arrays: per light (component: drawn only; BSDF component: column 2)
-            for (int l = 0; l < sc.nlights; ++l) {
-                const RenderLight &L = sc.lights[l];
-                const int n = L.nsamples_round;
-                rng.skip(1 + (int64_t)spp * n + spp);
-                const uint32_t scr = rng.next();
-                float *c0 = rows + L.replay_off + 2;
-                for (int i = 0; i < spp; ++i)
-                    for (int j = 0; j < n; ++j)
-                        c0[(int64_t)i * K + j * kReplayPerLightSample] = van_der_corput((uint32_t)(i * n + j), scr);
-                for (int i = 0; i < spp; ++i) replay_shuffle_elems(rng, c0 + (int64_t)i * K, n, 1);
-                for (int i = 0; i < spp; ++i) {  // Shuffle(samples, spp, n): whole blocks
-                    const int other = i + (int)(rng.next() % (uint32_t)(spp - i));
-                    if (other == i) continue;
-                    float *a = c0 + (int64_t)i * K, *b = c0 + (int64_t)other * K;
-                    for (int j = 0; j < n; ++j) {
-                        const float t = a[j * kReplayPerLightSample];
-                        a[j * kReplayPerLightSample] = b[j * kReplayPerLightSample];
-                        b[j * kReplayPerLightSample] = t;
-                    }
-                }
-            }
-            rng.skip(2 * (1 + 2 * (int64_t)spp));  // the emission integrator's two 1D(1) arrays
-            // 2D arrays: per light, light position (columns 0, 1) then BSDF direction (3, 4)
-            for (int l = 0; l < sc.nlights; ++l) {
-                const RenderLight &L = sc.lights[l];
-                const int n = L.nsamples_round;
-                for (int arr = 0; arr < 2; ++arr) {
-                    const uint32_t s0 = rng.next(), s1 = rng.next();
-                    float *c0 = rows + L.replay_off + (arr == 0 ? 0 : 3);
-                    for (int i = 0; i < spp; ++i)
-                        for (int j = 0; j < n; ++j) {
-                            const uint32_t k = (uint32_t)(i * n + j);
-                            c0[(int64_t)i * K + j * kReplayPerLightSample] = van_der_corput(k, s0);
-                            c0[(int64_t)i * K + j * kReplayPerLightSample + 1] = sobol2(k, s1);
-                        }
-                    for (int i = 0; i < spp; ++i) replay_shuffle_elems(rng, c0 + (int64_t)i * K, n, 2);
-                    for (int i = 0; i < spp; ++i) {
-                        const int other = i + (int)(rng.next() % (uint32_t)(spp - i));
-                        if (other == i) continue;
-                        float *a = c0 + (int64_t)i * K, *b = c0 + (int64_t)other * K;
-                        for (int j = 0; j < n; ++j)
-                            for (int d = 0; d < 2; ++d) {
-                                const float t = a[j * kReplayPerLightSample + d];
-                                a[j * kReplayPerLightSample + d] = b[j * kReplayPerLightSample + d];
-                                b[j * kReplayPerLightSample + d] = t;
-                            }
-                    }
-                }
-            }
-            // the pixel's camera rays: Li (6 draws) for every ray that hits
-            if (g.li_draws > 0)
-                for (int i = 0; i < spp; ++i) {
-                    const float X = (float)x + rows[(int64_t)i * K], Y = (float)y + rows[(int64_t)i * K + 1];
-                    const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
-                    const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
-                    const Hit h = trace_closest(sc, o, d, 0.f, INFINITY, stk, 64);
-                    if (h.tri != INT_MIN) rng.skip(g.li_draws);
-                }
-        }
-}
+// (the render tasks' streams: replay_gen.hip)
 
 // IrradianceTask::Run's RNG(47 k) (multipolesubsurface.cpp:81, 110-112): per point of the task's
 // slice and per light, scramble[0], scramble[1], compScramble

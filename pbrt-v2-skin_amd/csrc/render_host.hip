@@ -227,7 +227,7 @@ void Context::upload_scene() {
     }
     d_lights_.upload(rl.data(), rl.size());
     replay_k_ = replay_off;
-    replay_spp_ = 0;  // the replay table (if any) belongs to the old scene
+    ++scene_gen_;  // the workspaces' replay cursors belong to the old scene
     std::vector<RenderMaterial> rmat;
     if (!d_lut_.ptr) d_lut_.upload(ewa_weight_lut(), kEwaLut);
     for (auto &t : textures_)
@@ -563,38 +563,68 @@ void Context::find_poisson_points(uint32_t seed) {
 // list) -> ONE sharded Mo() gather per BSSRDF material over the batch's hits -> film kernel per
 // piece. Calls on different streams may overlap: each takes its own workspace (RenderWorkspace),
 // and the scene, materials and octree are only read after the context lock is released.
-// The reference sampler's values over the whole sample extent at `spp` (replay_render_kernel),
-// rebuilt when spp or the scene changes. mu_ held; synchronous, so every stream sees the table.
-void Context::ensure_replay_table(int spp) {
-    if (replay_spp_ == spp && replay_vals_.ptr) return;
-    const int W = scene_.camera.xres, H = scene_.camera.yres;
+// The reference sampler's values over [x0, x1) x [y0, y1) of the sample extent at `spp`
+// (replay_gen.hip) into ws->rp_table, continuing the workspace's task streams.
+void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp, int x0, int x1, int y0, int y1,
+                            hipStream_t stream) {
+    const int W = sc.xres, H = sc.yres;
     const int T = replay_render_tasks(W, H, std::max(1, cfg_.replay_cores));
-    quiesce_locked();  // no render may still read the old table
-    replay_vals_.alloc((size_t)(W + 1) * (H + 1) * spp * replay_k_);
-    DevBuf<uint32_t> mt;
-    mt.alloc((size_t)624 * T);
-    RenderScene sc = render_scene();
-    ReplayGen g{T, spp, replay_k_, (cfg_.max_depth > 0 && !cfg_.show_irradiance_points) ? kReplayLiDraws : 0, mt.ptr,
-                replay_vals_.ptr};
-    hipLaunchKernelGGL(replay_render_kernel, dim3((T + 63) / 64), dim3(64), 0, 0, sc, g);
-    MPSS_HIP(hipGetLastError());
-    MPSS_HIP(hipDeviceSynchronize());
-    replay_spp_ = spp;
+    const uint64_t key[3] = {scene_gen_, (uint64_t)spp, (uint64_t)T};
+    if (ws->rp_key[0] != key[0] || ws->rp_key[1] != key[1] || ws->rp_key[2] != key[2]) {
+        if ((int64_t)ws->rp_pix.n < T) {
+            ws->rp_mt.alloc((size_t)624 * T);
+            ws->rp_pix.alloc((size_t)T);
+            ws->rp_mti.alloc((size_t)T);
+        }
+        MPSS_HIP(hipMemsetAsync(ws->rp_pix.ptr, 0xff, sizeof(int) * (size_t)T, stream));  // -1: not seeded
+        for (int k = 0; k < 3; ++k) ws->rp_key[k] = key[k];
+    }
+    const size_t need = (size_t)(x1 - x0) * (y1 - y0) * spp * replay_k_;
+    if (ws->rp_table.n < need) {
+        if (ws->pending) MPSS_HIP(hipEventSynchronize(ws->done));
+        ws->rp_table.alloc(need);
+    }
+    ReplayWindow w{};
+    replay_window_tasks(W, H, T, x0, x1, y0, y1, w);
+    w.spp = spp;
+    w.K = replay_k_;
+    w.li_draws = (cfg_.max_depth > 0 && !cfg_.show_irradiance_points) ? kReplayLiDraws : 0;
+    w.nmax = 1;
+    for (const SceneLight &l : scene_.lights) w.nmax = std::max(w.nmax, round_up_pow2(l.nsamples));
+    w.cur = ReplayCursors{ws->rp_mt.ptr, ws->rp_pix.ptr, ws->rp_mti.ptr};
+    w.out = ws->rp_table.ptr;
+    launch_replay_window(sc, w, stream);
 }
 
 void Context::replay_samples(int spp, float *out, uint64_t *n_floats, int *k) {
     activate();
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
     if (cfg_.sampler != MPSS_SAMPLER_REFERENCE) throw Error(MPSS_ERR_INVALID, "replay_samples: the context uses the hash sampler");
     if (scene_dirty_) upload_scene();
     const int W = scene_.camera.xres, H = scene_.camera.yres;
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "replay_samples: no camera");
     spp = round_up_pow2(spp);
-    *k = replay_k_;
-    *n_floats = (uint64_t)(W + 1) * (H + 1) * spp * replay_k_;
+    if (spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay_samples: spp too large for the replay sampler");
+    const int K = replay_k_;
+    *k = K;
+    const int64_t npix = (int64_t)(W + 1) * (H + 1);
+    *n_floats = (uint64_t)npix * spp * K;
     if (!out) return;
-    ensure_replay_table(spp);
-    MPSS_HIP(hipMemcpy(out, replay_vals_.ptr, sizeof(float) * *n_floats, hipMemcpyDeviceToHost));
+    // the whole sample extent as one window, on a workspace of its own cursors
+    RenderWorkspace *ws = acquire_ws();
+    ++inflight_;
+    RenderScene sc = render_scene();
+    lk.unlock();
+    InflightGuard guard{this, ws, nullptr};
+    replay_window(ws, sc, spp, 0, W + 1, 0, H + 1, nullptr);
+    std::vector<float> col((size_t)npix * spp * K);
+    MPSS_HIP(hipMemcpy(col.data(), ws->rp_table.ptr, sizeof(float) * col.size(), hipMemcpyDeviceToHost));
+    ws->rp_key[0] = ~0ull;  // (its cursors now sit at the end of every stream)
+    guard.release();
+    // column-major window -> the documented layout [((y (W + 1) + x) spp + s) K + k]
+    for (int64_t p = 0; p < npix; ++p)
+        for (int s2 = 0; s2 < spp; ++s2)
+            for (int c = 0; c < K; ++c) out[(p * spp + s2) * K + c] = col[((size_t)c * npix + p) * spp + s2];
 }
 
 void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs,
@@ -608,8 +638,8 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     const bool replay = cfg_.sampler == MPSS_SAMPLER_REFERENCE;
     if (replay) {
         spp = round_up_pow2(spp);  // LDSampler rounds pixelsamples up (lowdiscrepancy.cpp:45-49)
-        if (spp > 32768) throw Error(MPSS_ERR_INVALID, "render_tile: spp must be at most 32768 for the replay sampler");
-        ensure_replay_table(spp);
+        if (spp > kReplayMaxSpp)
+            throw Error(MPSS_ERR_INVALID, "render_tile: spp must be at most 4096 for the replay sampler");
     }
     for (int i = 0; i < n; ++i) {
         const int32_t *r = rects + 4 * i;
@@ -632,10 +662,8 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                                      &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
     sc.have_octree = sss.empty() ? 0 : 1;
-    if (replay) {
-        sc.replay = replay_vals_.ptr;
+    if (replay) {  // (the window and its table: per batch, below)
         sc.replay_k = replay_k_;
-        sc.replay_w = W + 1;
         sc.replay_spp = spp;
     }
     const bool timing = cfg_.kernel_timing != 0, counting = cfg_.count_traversal != 0;
@@ -644,7 +672,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         MPSS_HIP(hipMemset(d_counts_.ptr, 0, kStatStride * kGroups * sizeof(unsigned long long)));
     }
     unsigned long long *const counts = counting ? d_counts_.ptr : nullptr;
-    const int64_t max_batch = std::max<int64_t>(cfg_.max_batch_samples, 1 << 16);
+    const int64_t max_batch = std::max<int64_t>(cfg_.max_batch_samples, 1 << 10);
     const int nlights = (int)scene_.lights.size();
     int ns_max = 1;
     for (const SceneLight &l : scene_.lights) ns_max = std::max(ns_max, round_up_pow2(l.nsamples));
@@ -672,7 +700,16 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             float *out;
         };
         std::vector<Piece> pieces;
-        for (int i = 0; i < n; ++i) {
+        // replay: rectangles in row order, so that consecutive batches continue the task streams
+        // (replay_window) and a batch's window stays compact
+        std::vector<int> order(n);
+        for (int i = 0; i < n; ++i) order[i] = i;
+        if (replay)
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+                return rects[4 * a + 2] != rects[4 * b + 2] ? rects[4 * a + 2] < rects[4 * b + 2]
+                                                            : rects[4 * a] < rects[4 * b];
+            });
+        for (int i : order) {
             const int x0 = rects[4 * i], x1 = rects[4 * i + 1], y0 = rects[4 * i + 2], y1 = rects[4 * i + 3];
             const int tw = x1 - x0;
             const int ex0 = std::max(x0 - 1, 0);
@@ -701,8 +738,24 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             // pack pieces into one batch
             size_t pe = pi;
             int64_t total = 0;
-            while (pe < pieces.size() && (pe == pi || total + pieces[pe].tb.nsamples <= max_batch))
+            // replay: the batch's window (the pieces' bounding box) holds spp x replay_k_ floats per
+            // pixel; kept to <= kReplayWindowFloats
+            int bx0 = INT32_MAX, bx1 = 0, by0 = INT32_MAX, by1 = 0;
+            auto fits = [&](const TileBatch &tb) {
+                if (!replay) return true;
+                const int64_t w = std::max(bx1, tb.ex0 + tb.ew) - std::min(bx0, tb.ex0);
+                const int64_t h = std::max(by1, tb.ey0 + tb.eh) - std::min(by0, tb.ey0);
+                return w * h * spp * replay_k_ <= kReplayWindowFloats;
+            };
+            while (pe < pieces.size() &&
+                   (pe == pi || (total + pieces[pe].tb.nsamples <= max_batch && fits(pieces[pe].tb)))) {
+                const TileBatch &tb = pieces[pe].tb;
+                bx0 = std::min(bx0, tb.ex0);
+                bx1 = std::max(bx1, tb.ex0 + tb.ew);
+                by0 = std::min(by0, tb.ey0);
+                by1 = std::max(by1, tb.ey0 + tb.eh);
                 total += pieces[pe++].tb.nsamples;
+            }
             // per-sample buffers: the batch's camera samples (primary_kernel may give each a hit slot)
             if (ws->n < total) {
                 int64_t have = ws->n;
@@ -761,6 +814,16 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 }
             };
             hipEvent_t ev{};
+            if (replay) {  // the reference sampler's values over the batch's window
+                time_begin(timing, stream, ev);
+                replay_window(ws, sc, spp, bx0, bx1, by0, by1, stream);
+                time_end(timing, stream, ev, 6, timed);
+                sc.replay = ws->rp_table.ptr;
+                sc.replay_x0 = bx0;
+                sc.replay_y0 = by0;
+                sc.replay_w = bx1 - bx0;
+                sc.replay_npix = (int64_t)(bx1 - bx0) * (by1 - by0);
+            }
             time_begin(timing, stream, ev);
             launch_pieces(false);
             time_end(timing, stream, ev, 1, timed);
@@ -913,10 +976,10 @@ mpss_render_stats Context::render_stats() {
         MPSS_HIP(hipEventElapsedTime(&ms, t.a, t.b));
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
-        double *dst[6] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film,
-                          &stats_.ms_direct, &stats_.ms_tex};
-        int64_t *cnt[6] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film, &stats_.n_direct,
-                           &stats_.n_tex};
+        double *dst[7] = {&stats_.ms_irradiance, &stats_.ms_camera, &stats_.ms_shade, &stats_.ms_film,
+                          &stats_.ms_direct, &stats_.ms_tex, &stats_.ms_replay};
+        int64_t *cnt[7] = {&stats_.n_irradiance, &stats_.n_camera, &stats_.n_shade, &stats_.n_film, &stats_.n_direct,
+                           &stats_.n_tex, &stats_.n_replay};
         *dst[t.kind] += ms;
         *cnt[t.kind] += 1;
     }

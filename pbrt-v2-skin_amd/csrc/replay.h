@@ -26,9 +26,9 @@
 // NumSystemCores(), N / 4096)) tasks over point slices [k N / T, (k + 1) N / T), RNG(47 k), three
 // draws per (point, light): the Sample02 scrambles and the component scramble.
 //
-// The product replays these streams on the GPU (render.hip replay_render_kernel /
-// replay_irradiance_kernel: one lane per task) into a table of the sample values its kernels
-// consume; oracle/render.c restates the same loop on the CPU.
+// The product replays these streams on the GPU (replay_gen.hip: one wave per render task, per
+// render batch into a table of the batch's window; render.hip replay_irradiance_kernel: one lane
+// per irradiance task); oracle/render.c restates the same loop on the CPU.
 #pragma once
 #include "pbrt_math.h"
 
@@ -39,6 +39,10 @@ namespace mpss {
 // the volume integrator's arrays are drawn (the stream must advance) but not consumed here.
 constexpr int kReplayImage = 2, kReplayPerLightSample = 5;
 constexpr int kReplayLiDraws = 6;
+// the largest (power-of-two) spp the replay generator takes: one pixel's index arrays live in LDS
+constexpr int kReplayMaxSpp = 4096;
+// the largest window table of one render batch (floats: 2 GiB); render_tiles closes a batch before it
+constexpr int64_t kReplayWindowFloats = (int64_t)1 << 29;
 
 MPSS_HD int replay_round_up_pow2(int v) {
     int r = 1;

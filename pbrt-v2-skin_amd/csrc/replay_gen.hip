@@ -1,0 +1,335 @@
+// replay_gen.hip -- the reference sampler's values for one window of the sample extent, on the
+// GPU (replay.h; render.h ReplayWindow). pbrt draws a task's samples from one sequential MT19937
+// stream, so a task cannot be split across lanes; it is split across the stream instead: one wave
+// per task, its 624-word state in LDS, the lanes twisting, tempering and consuming the stream's
+// draws together and computing the camera samples of a pixel side by side.
+//
+// Per pixel, LDPixelSample (lowdiscrepancy.cpp:69-82, montecarlo.cpp:200-250) draws in this
+// order: image (2D, 1 per sample), lens (2D), time (1D), then every 1D array (per light: the light
+// component, the BSDF component), the emission integrator's two 1D(1) arrays, every 2D array (per
+// light: light position, BSDF direction); then Li draws 6 values for every sample whose camera ray
+// hits the scene (integrator.cpp:177-185). An array of n values per sample is LDShuffleScrambled
+// (montecarlo.h:314-333): its scrambles, the (0,2) values, n draws per sample for the shuffle of
+// the sample's own n values, spp draws for the shuffle of the samples (Shuffle, montecarlo.h:183-189).
+//
+// A wave never moves values around: each shuffle is replayed on an index array (the samples'
+// block shuffle, sequential over the spp swaps, on one lane; each sample's own shuffle on its
+// lane), and every value is then computed at its final place from the index it ends up holding --
+// the (0,2) point of that index. The arrays the kernels read (image, light position, BSDF
+// component, BSDF direction) are written to the window table; the others only advance the stream.
+#include "../../include/mpss.h"
+#include "bvh_trace.h"
+#include "render.h"
+
+#include <algorithm>
+
+namespace mpss {
+
+namespace {
+
+constexpr int kMaxWaves = 4;  // waves per workgroup (fewer when a wave's LDS needs more room)
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+// orders one wave's LDS accesses (a wave's LDS operations complete in issue order)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t temper(uint32_t y) {  // RNG::RandomUInt's output transform
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+// One wave's MT19937 (core/rng.cpp): the state in LDS, i = the next word.
+struct WaveMt {
+    uint32_t *st;
+    int i;
+
+    __device__ void seed(uint32_t v) {  // RNG::Seed: a 624-step recurrence, on lane 0
+        if (lane_id() == 0) {
+            st[0] = v;
+            for (int k = 1; k < 624; ++k) {
+                v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)k;
+                st[k] = v;
+            }
+        }
+        wave_sync();
+        i = 624;
+    }
+    // the generator step over all 624 words, 64 at a time in word order: word k reads words k + 1
+    // and k + 397 not yet rewritten (k < 227) or word k - 227 already rewritten, as the sequential
+    // loop does; a block's reads precede its writes
+    __device__ void twist() {
+        const int lane = lane_id();
+        for (int base = 0; base < 624; base += 64) {
+            const int k = base + lane;
+            uint32_t v = 0;
+            if (k < 624) {
+                const uint32_t y = (st[k] & 0x80000000u) | (st[k + 1 < 624 ? k + 1 : 0] & 0x7fffffffu);
+                v = st[k + 397 < 624 ? k + 397 : k - 227] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            wave_sync();
+            if (k < 624) st[k] = v;
+            wave_sync();
+        }
+        i = 0;
+    }
+    // the next `count` draws into db[0, count), in stream order
+    __device__ void fetch(uint32_t *db, int count) {
+        const int lane = lane_id();
+        int done = 0;
+        while (done < count) {
+            if (i >= 624) twist();
+            const int take = min(count - done, 624 - i);
+            for (int k = lane; k < take; k += 64) db[done + k] = temper(st[i + k]);
+            i += take;
+            done += take;
+        }
+        wave_sync();
+    }
+    __device__ void skip(int64_t count) {  // draws whose values are not needed
+        while (count > 0) {
+            if (i >= 624) twist();
+            const int take = (int)min<int64_t>(count, 624 - i);
+            i += take;
+            count -= take;
+        }
+    }
+    __device__ uint2 two() {  // two draws, wave-uniform
+        uint32_t *db = st + 624;  // (the draw buffer follows the state)
+        fetch(db, 2);
+        return make_uint2(db[0], db[1]);
+    }
+    __device__ uint32_t one() {
+        uint32_t *db = st + 624;
+        fetch(db, 1);
+        return db[0];
+    }
+};
+
+// Shuffle(samples, count, dims) of whole samples (its count draws), replayed on idx: idx[i] = the
+// original sample at position i afterwards
+__device__ void block_shuffle(WaveMt &mt, uint32_t *db, uint32_t *idx, int count) {
+    const int lane = lane_id();
+    mt.fetch(db, count);
+    for (int i = lane; i < count; i += 64) {
+        idx[i] = (uint32_t)i;
+        db[i] = (uint32_t)i + db[i] % (uint32_t)(count - i);
+    }
+    wave_sync();
+    if (lane == 0)
+        for (int i = 0; i < count; ++i) {
+            const uint32_t o = db[i];
+            if (o != (uint32_t)i) {
+                const uint32_t t = idx[i];
+                idx[i] = idx[o];
+                idx[o] = t;
+            }
+        }
+    wave_sync();
+}
+
+// Each sample's Shuffle of its own n values (n draws per sample, samples in order), replayed on
+// sig: sig[i * n + j] = the original value at position j of sample i afterwards
+__device__ void own_shuffles(WaveMt &mt, uint32_t *db, uint8_t *sig, int spp, int n) {
+    const int lane = lane_id();
+    for (int c = 0; c < spp; c += 64) {
+        const int cnt = min(64, spp - c);
+        mt.fetch(db, cnt * n);
+        if (lane < cnt) {
+            uint8_t *s = sig + (size_t)(c + lane) * n;
+            for (int j = 0; j < n; ++j) s[j] = (uint8_t)j;
+            for (int j = 0; j < n; ++j) {
+                const int o = j + (int)(db[lane * n + j] % (uint32_t)(n - j));
+                const uint8_t t = s[j];
+                s[j] = s[o];
+                s[o] = t;
+            }
+        }
+        wave_sync();
+    }
+}
+
+__global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderScene sc, ReplayWindow g, int words) {
+    extern __shared__ uint32_t smem[];
+    const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+    const int nwv = (int)(blockDim.x >> 6);
+    const int wid = (int)blockIdx.x * nwv + wv;
+    if (wid >= g.nxr * g.nyr) return;  // (wave-uniform; no workgroup barrier below)
+    const int task = (g.yo0 + wid / g.nxr) * g.nx + g.xo0 + wid % g.nxr;
+    int x0, x1, y0, y1;
+    replay_sub_window(task, g.ntasks, 0, sc.xres + 1, 0, sc.yres + 1, x0, x1, y0, y1);
+    const int ix0 = max(x0, g.x0), ix1 = min(x1, g.x0 + g.w), iy0 = max(y0, g.y0), iy1 = min(y1, g.y0 + g.h);
+    if (ix0 >= ix1 || iy0 >= iy1) return;
+    const int tw = x1 - x0, spp = g.spp;
+    const int first = (iy0 - y0) * tw + (ix0 - x0), last = (iy1 - 1 - y0) * tw + (ix1 - 1 - x0);
+    // this wave's LDS: state [624], draw buffer [max(spp, 64 nmax, 2)], idx [spp], sig [spp nmax bytes];
+    // then the workgroup's traversal stacks
+    uint32_t *base = smem + (size_t)wv * words;
+    WaveMt mt{base, 624};
+    uint32_t *db = base + 624;
+    uint32_t *idx = db + max(max(spp, 64 * g.nmax), 2);
+    uint8_t *sig = (uint8_t *)(idx + spp);
+    int *stk = (int *)(smem + (size_t)nwv * words) + threadIdx.x;
+    const int sstride = (int)blockDim.x;
+
+    uint32_t *gst = g.cur.mt + (size_t)task * 624;
+    int ord = g.cur.cur_pix[task];
+    if (ord < 0 || ord > first) {  // not seeded, or the window lies behind the cursor: RNG(task)
+        mt.seed((uint32_t)task);
+        ord = 0;
+    } else {
+        for (int k = lane; k < 624; k += 64) mt.st[k] = gst[k];
+        wave_sync();
+        mt.i = g.cur.cur_mti[task];
+    }
+    const V3 cam_o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
+    const int64_t npix = (int64_t)g.w * g.h;
+    for (; ord <= last; ++ord) {
+        const int x = x0 + ord % tw, y = y0 + ord / tw;
+        const bool keep = x >= g.x0 && x < g.x0 + g.w && y >= g.y0 && y < g.y0 + g.h;
+        // value k of sample i of this pixel: out[k * npix * spp + i]
+        float *out = keep ? g.out + ((int64_t)(y - g.y0) * g.w + (x - g.x0)) * spp : nullptr;
+        auto put = [&](int k, int i, float v) { out[(int64_t)k * npix * spp + i] = v; };
+        // image: LDShuffleScrambled2D(1, spp); its own-value shuffles (1 draw each) keep the order
+        const uint2 si = mt.two();
+        mt.skip(spp);
+        block_shuffle(mt, db, idx, spp);
+        int hits = 0;
+        for (int c = 0; c < spp; c += 64) {
+            const int i = c + lane;
+            bool hit = false;
+            if (i < spp) {
+                const uint32_t b = idx[i];
+                const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
+                if (keep) {
+                    put(0, i, u);
+                    put(1, i, v);
+                }
+                if (g.li_draws > 0) {  // the camera ray (samplerrenderer.cpp:97-103): only whether it hits
+                    const float X = (float)x + u, Y = (float)y + v;
+                    const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
+                    const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
+                    hit = trace_any(sc, cam_o, d, 0.f, INFINITY, stk, sstride);
+                }
+            }
+            hits += __popcll(__ballot(hit));
+        }
+        mt.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
+        mt.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
+        // 1D arrays, per light: the light component (not read here), the BSDF component (column 2)
+        for (int l = 0; l < sc.nlights; ++l) {
+            const RenderLight &L = sc.lights[l];
+            const int n = L.nsamples_round;
+            mt.skip(1 + (int64_t)spp * n + spp);
+            const uint32_t scr = mt.one();
+            own_shuffles(mt, db, sig, spp, n);
+            block_shuffle(mt, db, idx, spp);
+            if (keep)
+                for (int i = lane; i < spp; i += 64) {
+                    const uint32_t b = idx[i];
+                    const uint8_t *s = sig + (size_t)b * n;
+                    for (int j = 0; j < n; ++j)
+                        put(L.replay_off + j * kReplayPerLightSample + 2, i, van_der_corput(b * n + s[j], scr));
+                }
+            wave_sync();
+        }
+        mt.skip(2 * (1 + 2 * (int64_t)spp));  // the emission integrator's two 1D(1) arrays
+        // 2D arrays, per light: light position (columns 0, 1), BSDF direction (3, 4)
+        for (int l = 0; l < sc.nlights; ++l) {
+            const RenderLight &L = sc.lights[l];
+            const int n = L.nsamples_round;
+            for (int arr = 0; arr < 2; ++arr) {
+                const uint2 s2 = mt.two();
+                own_shuffles(mt, db, sig, spp, n);
+                block_shuffle(mt, db, idx, spp);
+                if (keep) {
+                    const int col = L.replay_off + (arr == 0 ? 0 : 3);
+                    for (int i = lane; i < spp; i += 64) {
+                        const uint32_t b = idx[i];
+                        const uint8_t *s = sig + (size_t)b * n;
+                        for (int j = 0; j < n; ++j) {
+                            const uint32_t k = b * n + s[j];
+                            put(col + j * kReplayPerLightSample, i, van_der_corput(k, s2.x));
+                            put(col + j * kReplayPerLightSample + 1, i, sobol2(k, s2.y));
+                        }
+                    }
+                }
+                wave_sync();
+            }
+        }
+        mt.skip((int64_t)g.li_draws * hits);  // Li, per camera ray that hits
+    }
+    for (int k = lane; k < 624; k += 64) gst[k] = mt.st[k];
+    if (lane == 0) {
+        g.cur.cur_pix[task] = last + 1;
+        g.cur.cur_mti[task] = mt.i;
+    }
+}
+
+}  // namespace
+
+void replay_window_tasks(int xres, int yres, int ntasks, int x0, int x1, int y0, int y1, ReplayWindow &w) {
+    const int ew = xres + 1, eh = yres + 1;
+    int nx = ntasks, ny = 1;  // ComputeSubWindow's split (replay_sub_window)
+    while ((nx & 0x1) == 0 && 2 * ew * ny < eh * nx) {
+        nx >>= 1;
+        ny <<= 1;
+    }
+    w.ntasks = ntasks;
+    w.nx = nx;
+    int lo = -1, hi = -1;
+    for (int xo = 0; xo < nx; ++xo) {
+        int a0, a1, b0, b1;
+        replay_sub_window(xo, ntasks, 0, ew, 0, eh, a0, a1, b0, b1);
+        if (a0 < x1 && a1 > x0) {
+            if (lo < 0) lo = xo;
+            hi = xo;
+        }
+    }
+    w.xo0 = lo < 0 ? 0 : lo;
+    w.nxr = lo < 0 ? 0 : hi - lo + 1;
+    lo = hi = -1;
+    for (int yo = 0; yo < ny; ++yo) {
+        int a0, a1, b0, b1;
+        replay_sub_window(yo * nx, ntasks, 0, ew, 0, eh, a0, a1, b0, b1);
+        if (b0 < y1 && b1 > y0) {
+            if (lo < 0) lo = yo;
+            hi = yo;
+        }
+    }
+    w.yo0 = lo < 0 ? 0 : lo;
+    w.nyr = lo < 0 ? 0 : hi - lo + 1;
+    w.x0 = x0;
+    w.y0 = y0;
+    w.w = x1 - x0;
+    w.h = y1 - y0;
+}
+
+void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStream_t stream) {
+    const int nw = w.nxr * w.nyr;
+    if (nw <= 0) return;
+    if (w.nmax < 1 || w.nmax > 256) throw Error(MPSS_ERR_INVALID, "replay: light sample counts must be in [1, 256]");
+    if (w.spp < 1 || w.spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay: spp out of range");
+    const int words = 624 + std::max(std::max(w.spp, 64 * w.nmax), 2) + w.spp + (w.spp * w.nmax + 3) / 4;
+    auto lds_of = [&](int nwv) {
+        return sizeof(uint32_t) * ((size_t)nwv * words + (size_t)kTraceStack * 64 * nwv);
+    };
+    int nwv = kMaxWaves;
+    while (nwv > 1 && lds_of(nwv) > 64 * 1024) --nwv;  // two workgroups per CU where it fits
+    const size_t lds = lds_of(nwv);
+    if (lds > 160 * 1024)
+        throw Error(MPSS_ERR_INVALID, "replay: spp x light samples too large for the replay generator's LDS");
+    if (lds > 64 * 1024)
+        MPSS_HIP(hipFuncSetAttribute((const void *)replay_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds));
+    hipLaunchKernelGGL(replay_window_kernel, dim3((unsigned)((nw + nwv - 1) / nwv)), dim3(64 * nwv), lds, stream, sc,
+                       w, words);
+    MPSS_HIP(hipGetLastError());
+}
+
+}  // namespace mpss

@@ -59,7 +59,7 @@ class RenderStats(C.Structure):
                 ("n_direct", C.c_int64), ("mo_wave_node_iters", C.c_int64), ("mo_wave_point_iters", C.c_int64),
                 ("mo_lookups", C.c_int64), ("mo_lookups_near", C.c_int64 * 3), ("mo_row_lane_records", C.c_int64),
                 ("mo_lds_lane_records", C.c_int64), ("mo_table_lane_records", C.c_int64), ("ms_tex", C.c_double),
-                ("n_tex", C.c_int64)]
+                ("n_tex", C.c_int64), ("ms_replay", C.c_double), ("n_replay", C.c_int64)]
 
 
 class LayeredSkin(C.Structure):

@@ -242,3 +242,31 @@ def test_c5_dense_mesh_window(mpss):
     x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
     _check(_render(torch, ctx, sc.spp, 5, x0, x1, y0, y1), o.render_tile(sc.spp, 5, x0, x1, y0, y1, nthreads=NT))
     ctx.close()
+
+
+def test_c5_replay_window(mpss):
+    """C5 (4096x4096, 512 spp, 4.06 M triangles) with pbrt's own sampler replayed
+    (MPSS_SAMPLER_REFERENCE, 8 emulated cores: 65,536 render tasks of 16x16 pixels): a 32x32 cheek
+    window against the oracle fed the same tasks' MT19937 streams. The GPU generates only the
+    window's tasks (replay_gen.hip; a whole-frame table would be (4097^2) x 512 x 22 floats)."""
+    import torch
+    from mpss import pbrtscene
+    sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=4096, yres=4096, spp=512)
+    pts = pbrtscene.mesh_points(sc)
+    sc.meshes = [pbrtscene.subdivide_mesh(me, 4) for me in sc.meshes]
+    ctx = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=8)
+    ctx.set_surface_points(pts)
+    ctx.preprocess(seed=0)
+    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    o.set_octree(pts, ctx.irradiance())
+    x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
+    ctx.set_instrumentation(kernel_timing=True)
+    got = _render(torch, ctx, sc.spp, 0, x0, x1, y0, y1)
+    win = o.replay_window(x0, x1, y0, y1)
+    vals = o.replay_table_window(sc.spp, win, cores=8, li_draws=6, nthreads=NT)
+    ref = o.render_tile_replay(sc.spp, vals, x0, x1, y0, y1, nthreads=NT, window=win)
+    parity.check_image(got, ref, "c5_replay_window_512spp")
+    assert (ref[..., 1] > 0).all()
+    assert ctx.render_stats()["n_replay"] >= 1
+    ctx.close()
+

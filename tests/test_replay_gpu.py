@@ -43,6 +43,17 @@ def _pair(mpss, sc, cores=8):
     return torch, ctx, o
 
 
+def _render_many(torch, ctx, sc, rects):
+    """All rectangles in ONE render_tiles call (mpss_render_tiles: batches, one replay window each)."""
+    outs = [torch.zeros(((y1 - y0) * (x1 - x0) * 4,), dtype=torch.float32, device="cuda") for x0, x1, y0, y1 in rects]
+    ctx.render_tiles(sc.spp, 0, rects, [o.data_ptr() for o in outs])
+    torch.cuda.synchronize()
+    img = np.zeros((sc.yres, sc.xres, 4), np.float32)
+    for (x0, x1, y0, y1), o in zip(rects, outs):
+        img[y0:y1, x0:x1] = o.cpu().numpy().reshape(y1 - y0, x1 - x0, 4)
+    return img
+
+
 def _render(torch, ctx, sc, rects):
     img = np.zeros((sc.yres, sc.xres, 4), np.float32)
     for (x0, x1, y0, y1) in rects:
@@ -84,7 +95,19 @@ def test_replay_irradiance_and_image(mpss, oracle, name, lights):
     tiles = [(x, min(x + 13, sc.xres), y, min(y + 11, sc.yres)) for y in range(0, sc.yres, 11)
              for x in range(0, sc.xres, 13)]
     assert np.array_equal(_render(torch, ctx, sc, tiles), full)
+    # tiles behind the task cursors (reverse and shuffled order: each such task restarts from
+    # RNG(task)), and all tiles in one call split into many batches (one window per batch)
+    assert np.array_equal(_render(torch, ctx, sc, tiles[::-1]), full)
+    rng = np.random.default_rng(3)
+    assert np.array_equal(_render(torch, ctx, sc, [tiles[i] for i in rng.permutation(len(tiles))]), full)
     ctx.close()
+    from mpss import pbrtscene
+    ctx2 = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=8, max_batch_samples=1 << 16)
+    ctx2.set_irradiance_points(pts["p"], pts["n"], got_E, pts["area"])
+    ctx2.set_instrumentation(kernel_timing=True)
+    assert np.array_equal(_render_many(torch, ctx2, sc, tiles), full)
+    assert ctx2.render_stats()["n_replay"] > 1
+    ctx2.close()
 
 
 def test_replay_depends_on_core_count_and_not_on_seed(mpss):
