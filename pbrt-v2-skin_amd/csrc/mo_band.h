@@ -116,6 +116,15 @@ struct CommonGrid {
     int on;                     // 1: some group has a non-empty row range (the three-path gather runs)
 };
 
+// A band group's FromRGB weights (SampledSpectrum::FromRGB, spectrum.cpp:103-186) for its four
+// output bands (0 for an empty slot): out = .94 (W min + X (mid - min) + Y (max - mid)) with X the
+// secondary spectrum of the smallest component and Y the primary of the largest.
+struct RgbK {
+    float w[4];     // rgbRefl2SpectWhite
+    float x[3][4];  // Cyan (R smallest), Magenta (G), Yellow (B)
+    float y[3][4];  // Red (R largest), Green (G), Blue (B)
+};
+
 struct BandTree {
     const NodeHdr *__restrict__ nodes;
     const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
@@ -135,6 +144,7 @@ struct BandTree {
     // group's four OUTPUT bands stay groups.band (Rd_c = FromRGB of the three lookups, band c).
     int lband[kGroups][4];
     const float *rgb_refl;  // RGB: rgbRefl2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue} [7][NB]
+    RgbK rgb_k[kGroups];    // RGB: each group's weights (band_tree, from the same tables)
 };
 
 #ifdef __HIP__  // device traversal: HIP translation units only (host .cpp files see the layout types)
@@ -276,75 +286,73 @@ __device__ __forceinline__ void band_rd_lerp(const float f[4], const RdPair v[4]
     }
 }
 
-// Band c of SampledSpectrum::FromRGB(rgb, SPECTRUM_REFLECTANCE) (spectrum.cpp:103-186) with the
-// refl tables in memory ([7][NB], c wave-uniform: scalar loads): the float operations of the
-// 30-band host code (spectral.cpp spectrum_from_rgb) and of the reference-order gather's FN_RGB.
-__device__ __forceinline__ float from_rgb_c(const float *__restrict__ refl, float R, float G, float B, int c) {
-    enum { W = 0, CY = 1, MG = 2, YE = 3, RD = 4, GR = 5, BL = 6 };
-    const float *k = refl + c;
-    float r = 0.f;
-    if (R <= G && R <= B) {
-        r += k[W * NB] * R;
-        if (G <= B) { r += k[CY * NB] * (G - R); r += k[BL * NB] * (B - G); }
-        else { r += k[CY * NB] * (B - R); r += k[GR * NB] * (G - B); }
-    } else if (G <= R && G <= B) {
-        r += k[W * NB] * G;
-        if (R <= B) { r += k[MG * NB] * (R - G); r += k[BL * NB] * (B - R); }
-        else { r += k[MG * NB] * (B - G); r += k[RD * NB] * (R - B); }
-    } else {
-        r += k[W * NB] * B;
-        if (R <= G) { r += k[YE * NB] * (R - B); r += k[GR * NB] * (G - R); }
-        else { r += k[YE * NB] * (G - B); r += k[RD * NB] * (R - G); }
+// SampledSpectrum::FromRGB(rgb, SPECTRUM_REFLECTANCE) (spectrum.cpp:103-186; mo_kernel.hip
+// from_rgb_band restates its branches) for the group's four output bands (k: their weights),
+// without the branches: the case
+// split only picks which component is the minimum, middle and maximum and which secondary (X) and
+// primary (Y) spectra weigh the differences. When every lane of the wave is in the same one of the
+// six cases (the usual one: the lanes' distances to a record are close, and the order of the three
+// profiles changes at a few distances only) the weights are wave-uniform scalars and the bands go
+// two by two through packed products; otherwise each lane selects its own. Both take the reference's
+// float operations (W * min + X * (mid - min) + Y * (max - mid), * .94), and the clamp as max(v, 0)
+// (Clamp's v < 0 ? 0 : v but for v = -0 and NaN, neither of which changes a sum of terms).
+__device__ __forceinline__ void rgb_tail(const f2v w[2], const f2v x[2], const f2v y[2], float mn, float d1, float d2,
+                                         float o[4]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f2v r = w[h] * f2v{mn, mn};
+        r = r + x[h] * f2v{d1, d1};
+        r = r + y[h] * f2v{d2, d2};
+        r = r * f2v{(float).94, (float).94};
+        o[2 * h] = fmaxf(r.x, 0.f);
+        o[2 * h + 1] = fmaxf(r.y, 0.f);
     }
-    const float v = r * (float).94;
-    return v < 0.f ? 0.f : v;  // Clamp(0, INFINITY)
 }
-
-// from_rgb_c for the group's four output bands (obands, -1 = empty: 0), without the branches: the
-// case split only picks which component is the minimum, middle and maximum and which two of the
-// six secondary/primary tables weigh the differences, so it is done once per term with selects and
-// every band then takes the same three products and two sums as from_rgb_c's taken branch
-// (W * min + X * (mid - min) + Y * (max - mid), * .94, clamp), the identical float operations.
-__device__ __forceinline__ void from_rgb4(const float *__restrict__ refl, float R, float G, float B,
-                                          const int *obands, float o[4]) {
-    enum { W = 0, CY = 1, MG = 2, YE = 3, RD = 4, GR = 5, BL = 6 };
+__device__ __forceinline__ void from_rgb4(const RgbK &k, float R, float G, float B, float o[4]) {
     const bool rmin = R <= G && R <= B;
     const bool gmin = !rmin && G <= R && G <= B;
     const bool c2 = rmin ? G <= B : (gmin ? R <= B : R <= G);
+    // case: 0 R<=G<=B, 1 R<=B<G, 2 G<R<=B, 3 G<=B<R, 4 B<R<=G, 5 B<G<R (from_rgb_c's branches)
+    const int cs = (rmin ? 0 : (gmin ? 2 : 4)) + (c2 ? 0 : 1);
+    const int c0 = __builtin_amdgcn_readfirstlane(cs);
+    const f2v w[2] = {f2v{k.w[0], k.w[1]}, f2v{k.w[2], k.w[3]}};
+    if (__builtin_amdgcn_ballot_w64(cs != c0) == 0) {
+        const int xs = c0 >> 1;                                        // CY, MG, YE
+        const int ys = (c0 == 0 || c0 == 2) ? 2 : ((c0 == 3 || c0 == 5) ? 0 : 1);  // BL, RD, GR
+        const float mn = c0 < 2 ? R : (c0 < 4 ? G : B);
+        const float md = (c0 == 0 || c0 == 5) ? G : ((c0 == 1 || c0 == 3) ? B : R);
+        const float mx = (c0 == 0 || c0 == 2) ? B : ((c0 == 1 || c0 == 4) ? G : R);
+        const f2v x[2] = {f2v{k.x[xs][0], k.x[xs][1]}, f2v{k.x[xs][2], k.x[xs][3]}};
+        const f2v y[2] = {f2v{k.y[ys][0], k.y[ys][1]}, f2v{k.y[ys][2], k.y[ys][3]}};
+        rgb_tail(w, x, y, mn, md - mn, mx - md, o);
+        return;
+    }
     const float mn = rmin ? R : (gmin ? G : B);
     const float md = rmin ? (c2 ? G : B) : (gmin ? (c2 ? R : B) : (c2 ? R : G));
     const float mx = rmin ? (c2 ? B : G) : (gmin ? (c2 ? B : R) : (c2 ? G : R));
-    const float d1 = md - mn, d2 = mx - md;
-    // Y: the primary of the maximum (blue, green or red)
-    const bool ybl = c2 && !(!rmin && !gmin), yrd = !c2 && !rmin;
+    const int xs = rmin ? 0 : (gmin ? 1 : 2);
+    const int ys = (c2 && (rmin || gmin)) ? 2 : ((!c2 && !rmin) ? 0 : 1);
+    f2v x[2], y[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (obands[j] < 0) {
-            o[j] = 0.f;
-            continue;
-        }
-        const float *k = refl + obands[j];
-        const float kx = rmin ? k[CY * NB] : (gmin ? k[MG * NB] : k[YE * NB]);
-        const float ky = ybl ? k[BL * NB] : (yrd ? k[RD * NB] : k[GR * NB]);
-        float r = k[W * NB] * mn;
-        r += kx * d1;
-        r += ky * d2;
-        const float v = r * (float).94;
-        o[j] = v < 0.f ? 0.f : v;
+    for (int h = 0; h < 2; ++h) {
+        x[h] = xs == 0 ? f2v{k.x[0][2 * h], k.x[0][2 * h + 1]}
+                       : (xs == 1 ? f2v{k.x[1][2 * h], k.x[1][2 * h + 1]} : f2v{k.x[2][2 * h], k.x[2][2 * h + 1]});
+        y[h] = ys == 0 ? f2v{k.y[0][2 * h], k.y[0][2 * h + 1]}
+                       : (ys == 1 ? f2v{k.y[1][2 * h], k.y[1][2 * h + 1]} : f2v{k.y[2][2 * h], k.y[2][2 * h + 1]});
     }
+    rgb_tail(w, x, y, mn, md - mn, mx - md, o);
 }
 
 // The combine half: lerp, the Mo() products and the running sums (one point or node). RGB: the
-// slots hold the R, G, B lookups, and the group's output bands (obands, -1 = empty) take FromRGB.
+// slots hold the R, G, B lookups, and the group's output bands take FromRGB (rk: their weights).
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
-                                                f2v acc[2], const float *refl = nullptr,
-                                                const int *obands = nullptr) {
+                                                f2v acc[2], const RgbK *rk = nullptr) {
     float rd[4];
     band_rd_lerp(f, v, rd);
     if (RGB) {
         float o[4];
-        from_rgb4(refl, rd[0], rd[1], rd[2], obands, o);
+        from_rgb4(*rk, rd[0], rd[1], rd[2], o);
         band_rd_products<POINT>(o, e, w, acc);
         return;
     }
@@ -475,7 +483,7 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 // the test runs when some lane of the wave is past the group's first end.
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
-                                           f2v acc[2], const float *refl = nullptr, const int *obands = nullptr) {
+                                           f2v acc[2], const RgbK *rk = nullptr) {
     float rd[4];
     const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
     band_rd_lerp(r.f, v, rd);
@@ -485,7 +493,7 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
     }
     if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
         float o[4];
-        from_rgb4(refl, rd[0], rd[1], rd[2], obands, o);
+        from_rgb4(*rk, rd[0], rd[1], rd[2], o);
         band_rd_products<POINT>(o, e, w, acc);
         return;
     }
@@ -494,12 +502,11 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
 
 template <bool POINT, bool COUNT, int KLDS, bool RGB = false>
 __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   int hist[7], const float *refl = nullptr,
-                                                   const int *obands = nullptr) {
+                                                   int hist[7], const RgbK *rk = nullptr) {
     float f[4];
     RdPair v[4];
     band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
-    band_rd_combine<POINT, RGB>(f, v, e, w, acc, refl, obands);
+    band_rd_combine<POINT, RGB>(f, v, e, w, acc, rk);
 }
 
 // sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d)
@@ -534,9 +541,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         b.rcp[j] = a.grcp[grp][j];
         b.off[j] = (uint32_t)(c >= 0 ? c : 0) * (uint32_t)a.L;
     }
-    int ob[4];  // RGB: the group's output bands
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ob[j] = a.groups.band[grp][j];
+    const RgbK rk = a.rgb_k[grp];  // RGB: the group's FromRGB weights (wave-uniform)
     b.lm1 = (uint32_t)(a.L - 1);
     const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
     b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
@@ -608,9 +613,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, a.rgb_refl, ob);
+                        cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, &rk);
                     } else {
-                        band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, a.rgb_refl, ob);
+                        band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, &rk);
                     }
                 } else {
                     open = true;
@@ -638,16 +643,16 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         if (CG) {
                             const CgRec ra = cg_fetch_near(b, cl, d2a), rb = cg_fetch_near(b, cl, d2b);
-                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, a.rgb_refl, ob);
-                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, a.rgb_refl, ob);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, &rk);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, &rk);
                             continue;
                         }
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
                         band_rd_fetch_lds<KLDS>(b, d2a, fa, va);
                         band_rd_fetch_lds<KLDS>(b, d2b, fb, vb);
-                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, a.rgb_refl, ob);
-                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, a.rgb_refl, ob);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, &rk);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, &rk);
                     }
                 }
                 for (; i0 + 1 < live; i0 += 2) {
@@ -671,8 +676,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                             const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
                             const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
                             const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, a.rgb_refl, ob);
-                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, a.rgb_refl, ob);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, &rk);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, &rk);
                             continue;
                         }
                         float fa[4], fb[4];
@@ -686,8 +691,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                                          "v"(vb[1].a), "v"(vb[1].b), "v"(vb[2].a), "v"(vb[2].b), "v"(vb[3].a),
                                          "v"(vb[3].b));
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, a.rgb_refl, ob);
-                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, a.rgb_refl, ob);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, &rk);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, &rk);
                     }
                 for (int i = i0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
@@ -700,9 +705,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, a.rgb_refl, ob);
+                        cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, &rk);
                     } else {
-                        band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, a.rgb_refl, ob);
+                        band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, &rk);
                     }
                 }
                 acc[0] += lacc[0];

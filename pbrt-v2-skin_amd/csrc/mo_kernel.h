@@ -73,9 +73,13 @@ struct DeviceProfile {
     void set_rgb(const float *table);
 };
 
-// The common grid's bound on the resampling error of a lookup relative to the band's own value there
-// (DeviceProfile::build_common; the group rows cover only the range where every band is within it).
+// The common grid's bound on the resampling error of a lookup: kCgRelTol of the band's own value
+// there, or kCgAbsTol of the band's peak where that is larger (the far tails, whose values are
+// 1e-5 .. 1e-11 of the peak and carry under 1 % of a band's mass on C2's profile: there the bound
+// is absolute). DeviceProfile::build_common; the group rows cover only the range where every band is
+// within it.
 constexpr double kCgRelTol = 2e-6;
+constexpr double kCgAbsTol = 1e-10;
 
 // The host half of DeviceProfile::build_common: the layout (cg, without tab), the pair rows h (two
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -401,6 +402,21 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
             bt.groups.rcp_min[g] = rmin;
         }
         bt.rgb_refl = p.rgb_refl.ptr;  // (p.cg: the grid of the three profiles, set_rgb)
+        // the groups' FromRGB weights: rgbRefl2Spect{White, Cyan, Magenta, Yellow, Red, Green, Blue}
+        static const float refl[7][NB] = {MPSS_BAND_RGBREFL2SPECTWHITE_INIT, MPSS_BAND_RGBREFL2SPECTCYAN_INIT,
+                                          MPSS_BAND_RGBREFL2SPECTMAGENTA_INIT, MPSS_BAND_RGBREFL2SPECTYELLOW_INIT,
+                                          MPSS_BAND_RGBREFL2SPECTRED_INIT, MPSS_BAND_RGBREFL2SPECTGREEN_INIT,
+                                          MPSS_BAND_RGBREFL2SPECTBLUE_INIT};
+        for (int g = 0; g < kGroups; ++g)
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int c = p.groups.band[g][s2];
+                auto at = [&](int t) { return c >= 0 ? refl[t][c] : 0.f; };
+                bt.rgb_k[g].w[s2] = at(0);
+                for (int t = 0; t < 3; ++t) {
+                    bt.rgb_k[g].x[t][s2] = at(1 + t);  // Cyan, Magenta, Yellow
+                    bt.rgb_k[g].y[t][s2] = at(4 + t);  // Red, Green, Blue
+                }
+            }
     }
     if (!bt.leaf_r2)
         for (int g = 0; g < kGroups; ++g) bt.cg.lds_r2[g] = bt.cg_half.lds_r2[g] = 0.f;
@@ -510,6 +526,13 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
+static int cg_max_rows() {  // (experiment: MPSS_CG_MAX_ROWS)
+    static const int v = [] {
+        const char *e = getenv("MPSS_CG_MAX_ROWS");
+        return e ? atoi(e) : kCgMaxRows;
+    }();
+    return v;
+}
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field) {
@@ -609,22 +632,27 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             return (float)((1.0 - t) * (double)T[sidx] + t * (double)T[sidx + 1]);
         };
         // The row range: every band knot past the near field (s >= u0lim r_j - 1) whose rows value is
-        // off by more than kCgRelTol of |T[s]| (unfloored: a zero or a sign change counts) is "bad";
+        // off by more than kCgRelTol of |T[s]| and more than kCgAbsTol of the band's peak is "bad";
         // the rows serve the longest stretch of u between bad knots, a grid cell of margin either
         // side (the rows' error inside a cell is bounded by that at the knots in it), capped at
         // kCgMaxRows rows. Usually the first stretch, from the near field's end; for bands of widely
         // different reach (the rgbprofile's R, G, B: the shortest reach's knots are much denser than
         // the grid, so it is off from the start) one past its end -- there tau's range test makes it
         // exactly 0, as its rows hold.
-        auto knot_err = [&](int j, int k) -> double {  // relative error at band j's knot k, inf = bad
+        double peak[4] = {0.0, 0.0, 0.0, 0.0};  // each band's largest |T|
+        for (int j = 0; j < 4; ++j)
+            if (groups.band[g][j] >= 0) {
+                const float *T = tab + (size_t)groups.band[g][j] * L;
+                for (int k = 0; k < L; ++k) peak[j] = std::max(peak[j], std::fabs((double)T[k]));
+            }
+        auto knot_err = [&](int j, int k) -> double {  // |rows - T| at band j's knot k, inf = bad
             const float *T = tab + (size_t)groups.band[g][j] * L;
             const double u = (double)k / r[j];
             const int64_t ui = (int64_t)std::floor(u);
             const double t = u - (double)ui;
             const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
             const double err = std::fabs(approx - (double)T[k]);
-            const bool sign_ok = T[k] != 0.f && (T[k] > 0.f) == (T[k + 1] > 0.f) && T[k + 1] != 0.f;
-            return (!sign_ok || err > kCgRelTol * std::fabs((double)T[k])) ? INFINITY : err;
+            return err > std::max(kCgRelTol * std::fabs((double)T[k]), kCgAbsTol * peak[j]) ? INFINITY : err;
         };
         std::vector<double> bad;
         for (int j = 0; j < 4; ++j) {
@@ -639,7 +667,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             double from = u0f;  // the current stretch's first servable u
             for (const double ub : bad) {
                 if (ub >= from) {
-                    const double len = std::min(std::floor(ub) - 1.0, from + (double)kCgMaxRows) - from;
+                    const double len = std::min(std::floor(ub) - 1.0, from + (double)cg_max_rows()) - from;
                     if (len > best) {
                         best = len;
                         start = from;
@@ -660,7 +688,9 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 if (u < start) continue;
                 if (u >= ubad) break;
                 const double e = knot_err(j, k);
-                emax = std::max(emax, e / std::fabs((double)T[k]));
+                // (relative error where the relative bound governs: |T| >= kCgAbsTol / kCgRelTol of the peak)
+                if (kCgRelTol * std::fabs((double)T[k]) >= kCgAbsTol * peak[j])
+                    emax = std::max(emax, e / std::fabs((double)T[k]));
                 esum += e;
             }
             cg_rel_err[c] = (float)emax;
@@ -668,7 +698,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         }
         const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
         int64_t u1 = (int64_t)std::floor(ubad) - 1;
-        u1 = std::min<int64_t>(u1, ubase + kCgMaxRows);
+        u1 = std::min<int64_t>(u1, ubase + cg_max_rows());
         u1 = std::min<int64_t>(u1, (int64_t)L - 1);
         cg.ubase[g] = (uint32_t)ubase;
         if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
