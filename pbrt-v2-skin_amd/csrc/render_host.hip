@@ -570,8 +570,10 @@ void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp,
     const int W = sc.xres, H = sc.yres;
     const int T = replay_render_tasks(W, H, std::max(1, cfg_.replay_cores));
     const uint64_t key[3] = {scene_gen_, (uint64_t)spp, (uint64_t)T};
+    if (ws->pending) MPSS_HIP(hipStreamWaitEvent(stream, ws->done, 0));  // the workspace's previous user
     if (ws->rp_key[0] != key[0] || ws->rp_key[1] != key[1] || ws->rp_key[2] != key[2]) {
         if ((int64_t)ws->rp_pix.n < T) {
+            if (ws->pending) MPSS_HIP(hipEventSynchronize(ws->done));
             ws->rp_mt.alloc((size_t)624 * T);
             ws->rp_pix.alloc((size_t)T);
             ws->rp_mti.alloc((size_t)T);
