@@ -154,6 +154,7 @@ struct __attribute__((aligned(4))) RdPair {
     float a, b;
 };
 typedef float f2v __attribute__((ext_vector_type(2)));  // v_pk_{add,mul}_f32 operands
+typedef float f4v __attribute__((ext_vector_type(4)));
 // The octree is read-only while a gather runs. Reading it through the constant address space
 // says so to the compiler: with stores of results earlier in the same (persistent) kernel it
 // otherwise cannot prove the node records unclobbered and turns the wave-uniform header loads
@@ -287,72 +288,49 @@ __device__ __forceinline__ void band_rd_lerp(const float f[4], const RdPair v[4]
 }
 
 // SampledSpectrum::FromRGB(rgb, SPECTRUM_REFLECTANCE) (spectrum.cpp:103-186; mo_kernel.hip
-// from_rgb_band restates its branches) for the group's four output bands (k: their weights),
-// without the branches: the case
-// split only picks which component is the minimum, middle and maximum and which secondary (X) and
-// primary (Y) spectra weigh the differences. When every lane of the wave is in the same one of the
-// six cases (the usual one: the lanes' distances to a record are close, and the order of the three
-// profiles changes at a few distances only) the weights are wave-uniform scalars and the bands go
-// two by two through packed products; otherwise each lane selects its own. Both take the reference's
-// float operations (W * min + X * (mid - min) + Y * (max - mid), * .94), and the clamp as max(v, 0)
-// (Clamp's v < 0 ? 0 : v but for v = -0 and NaN, neither of which changes a sum of terms).
-__device__ __forceinline__ void rgb_tail(const f2v w[2], const f2v x[2], const f2v y[2], float mn, float d1, float d2,
-                                         float o[4]) {
+// from_rgb_band restates its branches) for the group's four output bands. Its six cases only pick
+// which component is the minimum, middle and maximum, and two weight spectra by which component is
+// the minimum (X: Cyan, Magenta, Yellow) and the maximum (Y: Red, Green, Blue):
+//   out = .94 (W min + X (mid - min) + Y (max - mid)), clamped at 0.
+// Here min / mid / max are v_min3 / v_med3 / v_max3 (the same values), and X, Y rows are read from
+// the group's weights in LDS (rk: W[4], X[3][4], Y[3][4], RgbK's layout) by the lanes' own minimum and
+// maximum components: no per-band selects and no weights held in registers. Where two components
+// tie the reference's case order and this choice may name different X (or Y) rows, but the
+// difference they weigh is then exactly 0, so the result is the same. The float operations are the
+// reference's, the clamp is max(v, 0) (Clamp's v < 0 ? 0 : v but for v = -0 and NaN).
+__device__ __forceinline__ void from_rgb4(lds_float *rk, float R, float G, float B, float o[4]) {
+    const float mn = __builtin_fminf(R, __builtin_fminf(G, B));
+    const float mx = __builtin_fmaxf(R, __builtin_fmaxf(G, B));
+    const float md = __builtin_amdgcn_fmed3f(R, G, B);
+    const uint32_t xs = R == mn ? 0u : (G == mn ? 1u : 2u);
+    const uint32_t ys = R == mx ? 0u : (G == mx ? 1u : 2u);
+    typedef __attribute__((address_space(3))) const f4v lds_f4v;
+    const f4v w = *(lds_f4v *)rk, x = *(lds_f4v *)(rk + 4 + 4 * xs), y = *(lds_f4v *)(rk + 16 + 4 * ys);
+    const float d1 = md - mn, d2 = mx - md;
+    const f2v wv[2] = {f2v{w.x, w.y}, f2v{w.z, w.w}};
+    const f2v xv[2] = {f2v{x.x, x.y}, f2v{x.z, x.w}};
+    const f2v yv[2] = {f2v{y.x, y.y}, f2v{y.z, y.w}};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        f2v r = w[h] * f2v{mn, mn};
-        r = r + x[h] * f2v{d1, d1};
-        r = r + y[h] * f2v{d2, d2};
+        f2v r = wv[h] * f2v{mn, mn};
+        r = r + xv[h] * f2v{d1, d1};
+        r = r + yv[h] * f2v{d2, d2};
         r = r * f2v{(float).94, (float).94};
-        o[2 * h] = fmaxf(r.x, 0.f);
-        o[2 * h + 1] = fmaxf(r.y, 0.f);
+        o[2 * h] = __builtin_fmaxf(r.x, 0.f);
+        o[2 * h + 1] = __builtin_fmaxf(r.y, 0.f);
     }
-}
-__device__ __forceinline__ void from_rgb4(const RgbK &k, float R, float G, float B, float o[4]) {
-    const bool rmin = R <= G && R <= B;
-    const bool gmin = !rmin && G <= R && G <= B;
-    const bool c2 = rmin ? G <= B : (gmin ? R <= B : R <= G);
-    // case: 0 R<=G<=B, 1 R<=B<G, 2 G<R<=B, 3 G<=B<R, 4 B<R<=G, 5 B<G<R (from_rgb_c's branches)
-    const int cs = (rmin ? 0 : (gmin ? 2 : 4)) + (c2 ? 0 : 1);
-    const int c0 = __builtin_amdgcn_readfirstlane(cs);
-    const f2v w[2] = {f2v{k.w[0], k.w[1]}, f2v{k.w[2], k.w[3]}};
-    if (__builtin_amdgcn_ballot_w64(cs != c0) == 0) {
-        const int xs = c0 >> 1;                                        // CY, MG, YE
-        const int ys = (c0 == 0 || c0 == 2) ? 2 : ((c0 == 3 || c0 == 5) ? 0 : 1);  // BL, RD, GR
-        const float mn = c0 < 2 ? R : (c0 < 4 ? G : B);
-        const float md = (c0 == 0 || c0 == 5) ? G : ((c0 == 1 || c0 == 3) ? B : R);
-        const float mx = (c0 == 0 || c0 == 2) ? B : ((c0 == 1 || c0 == 4) ? G : R);
-        const f2v x[2] = {f2v{k.x[xs][0], k.x[xs][1]}, f2v{k.x[xs][2], k.x[xs][3]}};
-        const f2v y[2] = {f2v{k.y[ys][0], k.y[ys][1]}, f2v{k.y[ys][2], k.y[ys][3]}};
-        rgb_tail(w, x, y, mn, md - mn, mx - md, o);
-        return;
-    }
-    const float mn = rmin ? R : (gmin ? G : B);
-    const float md = rmin ? (c2 ? G : B) : (gmin ? (c2 ? R : B) : (c2 ? R : G));
-    const float mx = rmin ? (c2 ? B : G) : (gmin ? (c2 ? B : R) : (c2 ? G : R));
-    const int xs = rmin ? 0 : (gmin ? 1 : 2);
-    const int ys = (c2 && (rmin || gmin)) ? 2 : ((!c2 && !rmin) ? 0 : 1);
-    f2v x[2], y[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        x[h] = xs == 0 ? f2v{k.x[0][2 * h], k.x[0][2 * h + 1]}
-                       : (xs == 1 ? f2v{k.x[1][2 * h], k.x[1][2 * h + 1]} : f2v{k.x[2][2 * h], k.x[2][2 * h + 1]});
-        y[h] = ys == 0 ? f2v{k.y[0][2 * h], k.y[0][2 * h + 1]}
-                       : (ys == 1 ? f2v{k.y[1][2 * h], k.y[1][2 * h + 1]} : f2v{k.y[2][2 * h], k.y[2][2 * h + 1]});
-    }
-    rgb_tail(w, x, y, mn, md - mn, mx - md, o);
 }
 
 // The combine half: lerp, the Mo() products and the running sums (one point or node). RGB: the
 // slots hold the R, G, B lookups, and the group's output bands take FromRGB (rk: their weights).
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v[4], const float e[4], float w,
-                                                f2v acc[2], const RgbK *rk = nullptr) {
+                                                f2v acc[2], lds_float *rk = nullptr) {
     float rd[4];
     band_rd_lerp(f, v, rd);
     if (RGB) {
         float o[4];
-        from_rgb4(*rk, rd[0], rd[1], rd[2], o);
+        from_rgb4(rk, rd[0], rd[1], rd[2], o);
         band_rd_products<POINT>(o, e, w, acc);
         return;
     }
@@ -379,7 +357,6 @@ struct CgLane {
 // without moves -- a move after a load would wait for it to return.
 // (Returned as a value: stores through a reference in the arms of the branch get sunk into one store
 // to a phi of their addresses, which keeps the record in scratch memory.)
-typedef float f4v __attribute__((ext_vector_type(4)));
 struct CgRec {
     float f[4];
     f4v p01, p23;
@@ -483,7 +460,7 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 // the test runs when some lane of the wave is past the group's first end.
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
-                                           f2v acc[2], const RgbK *rk = nullptr) {
+                                           f2v acc[2], lds_float *rk = nullptr) {
     float rd[4];
     const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
     band_rd_lerp(r.f, v, rd);
@@ -493,7 +470,7 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
     }
     if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
         float o[4];
-        from_rgb4(*rk, rd[0], rd[1], rd[2], o);
+        from_rgb4(rk, rd[0], rd[1], rd[2], o);
         band_rd_products<POINT>(o, e, w, acc);
         return;
     }
@@ -502,7 +479,7 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
 
 template <bool POINT, bool COUNT, int KLDS, bool RGB = false>
 __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   int hist[7], const RgbK *rk = nullptr) {
+                                                   int hist[7], lds_float *rk = nullptr) {
     float f[4];
     RdPair v[4];
     band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
@@ -541,7 +518,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         b.rcp[j] = a.grcp[grp][j];
         b.off[j] = (uint32_t)(c >= 0 ? c : 0) * (uint32_t)a.L;
     }
-    const RgbK rk = a.rgb_k[grp];  // RGB: the group's FromRGB weights (wave-uniform)
+    lds_float *rk = (lds_float *)lt + 4 * near_row<KLDS>() - 28;  // RGB: the group's FromRGB weights (LDS)
     b.lm1 = (uint32_t)(a.L - 1);
     const uint32_t lm2 = b.lm1 - 1u;  // L >= 2
     b.klim = (uint32_t)KLDS < lm2 ? (uint32_t)KLDS : lm2;
@@ -613,9 +590,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, &rk);
+                        cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, rk);
                     } else {
-                        band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, &rk);
+                        band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, rk);
                     }
                 } else {
                     open = true;
@@ -643,16 +620,16 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         if (CG) {
                             const CgRec ra = cg_fetch_near(b, cl, d2a), rb = cg_fetch_near(b, cl, d2b);
-                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, &rk);
-                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, &rk);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, rk);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, rk);
                             continue;
                         }
                         float fa[4], fb[4];
                         RdPair va[4], vb[4];
                         band_rd_fetch_lds<KLDS>(b, d2a, fa, va);
                         band_rd_fetch_lds<KLDS>(b, d2b, fb, vb);
-                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, &rk);
-                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, &rk);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, rk);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, rk);
                     }
                 }
                 for (; i0 + 1 < live; i0 += 2) {
@@ -676,8 +653,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                             const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
                             const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
                             const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, &rk);
-                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, &rk);
+                            cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, rk);
+                            cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, rk);
                             continue;
                         }
                         float fa[4], fb[4];
@@ -691,8 +668,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                                          "v"(vb[1].a), "v"(vb[1].b), "v"(vb[2].a), "v"(vb[2].b), "v"(vb[3].a),
                                          "v"(vb[3].b));
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
-                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, &rk);
-                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, &rk);
+                        band_rd_combine<true, RGB>(fa, va, e0, pa.w, lacc, rk);
+                        band_rd_combine<true, RGB>(fb, vb, e1, pb.w, lacc, rk);
                     }
                 for (int i = i0; i < live; ++i) {
                     const int kp = h.leaf_first + i;
@@ -705,9 +682,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
                         const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
-                        cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, &rk);
+                        cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, rk);
                     } else {
-                        band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, &rk);
+                        band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, rk);
                     }
                 }
                 acc[0] += lacc[0];

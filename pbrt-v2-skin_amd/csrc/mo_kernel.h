@@ -65,7 +65,8 @@ struct DeviceProfile {
     // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
     void upload(const float *table, int L, const float *rcp, bool snake = false);
     // (upload calls it with groups, set_rgb with rows 0..2 in every group; host table [NB][L])
-    void build_common(const float *table, const BandGroups &slots);
+    // lds_reserve: floats at the end of the LDS near field the grid's split leaves free
+    void build_common(const float *table, const BandGroups &slots, int lds_reserve);
     // rgbprofile material: rows 0..2 of the table are its R, G, B profiles; the sharded gather looks
     // up those three for every group and converts them with FromRGB (rgb_refl: the device copy of
     // the rgbRefl2Spect tables, [7][NB]; set_rgb after upload)
@@ -85,7 +86,8 @@ constexpr double kCgAbsTol = 1e-10;
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group
 // has rows.
 bool build_common_grid(const float *tab, int L, const float *rcp, const BandGroups &groups, CommonGrid &cg,
-                       std::vector<float4> &h, float rel_err[NB], float l1_err[NB], int near_field = 10236);
+                       std::vector<float4> &h, float rel_err[NB], float l1_err[NB], int near_field = 10236,
+                       int lds_reserve = 0);
 
 // Choices of the sharded gather (mpss_config.mo_near_field / mo_work_stealing; count_noprune =
 // mpss_config.count_traversal == 2, instrumented passes only).

@@ -508,7 +508,7 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
     groups = make_band_groups(rcp_, snake);
     rgb_refl.release();
-    build_common(tab, groups);
+    build_common(tab, groups, 0);
 }
 
 // The common grid (mo_band.h CommonGrid), on the host from the band tables:
@@ -535,11 +535,12 @@ static int cg_max_rows() {  // (experiment: MPSS_CG_MAX_ROWS)
 }
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
-                       std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field) {
+                       std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field,
+                       int lds_reserve) {
     cg = CommonGrid{};
     h.clear();
     for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
-    const int kLdsFloats = 4 * (near_field + 3);
+    const int kLdsFloats = 4 * (near_field + 3) - lds_reserve;
     if (L < 4) return false;
     for (int g = 0; g < kGroups; ++g)
         for (int j = 0; j < 4; ++j) {
@@ -733,21 +734,21 @@ void DeviceProfile::set_rgb(const float *tab) {
     BandGroups g3 = groups;
     for (int g = 0; g < kGroups; ++g)
         for (int j = 0; j < 4; ++j) g3.band[g][j] = j < 3 ? j : -1;
-    build_common(tab, g3);
+    build_common(tab, g3, 28);  // (the LDS's last 28 floats: the groups' FromRGB weights)
 }
 
-void DeviceProfile::build_common(const float *tab, const BandGroups &slots) {
+void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int lds_reserve) {
     ctab.release();
     ctab_half.release();
     std::vector<float4> h;
     float rel[NB], l1[NB];
-    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, rel, l1, 5088)) {
+    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, rel, l1, 5088, lds_reserve)) {
         ctab_half.upload(h.data(), h.size());
         cg_half.tab = ctab_half.ptr;
     } else {
         cg_half.on = 0;
     }
-    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err, cg_l1_err, 10236)) {
+    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err, cg_l1_err, 10236, lds_reserve)) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }

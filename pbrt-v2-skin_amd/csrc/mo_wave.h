@@ -70,6 +70,8 @@ __global__ __launch_bounds__(WGT) __attribute__((amdgpu_waves_per_eu(wave_kernel
 void mo_band_wave_kernel(BandArgs a) {
     constexpr int ROWF = near_row<KLDS>();
     constexpr bool VROWS = KLDS > 5088;
+    // the near field; RGB: its last 28 floats hold the group's FromRGB weights (RgbK; slot 3 is
+    // unused for an rgbprofile, and its common grid's LDS split leaves them free)
     __shared__ float lt[KLDS > 0 ? 4 * ROWF : 1];
     __shared__ int next_grp;
     const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -111,11 +113,12 @@ void mo_band_wave_kernel(BandArgs a) {
         // entries 0..kmax of each band, kmax = min(KLDS, L - 2), zeros after (the last two floats of
         // a row are the zero pair of the lanes past the profile end)
         const int kmax = KLDS < a.t.L - 2 ? KLDS : a.t.L - 2;
-        for (int i = tid; i < 4 * ROWF; i += WGT) {
+        for (int i = tid; i < 4 * ROWF - (RGB ? 28 : 0); i += WGT) {
             const int j = i / ROWF, k = i % ROWF, c = a.t.lband[grp][j];
             lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
     }
+    if (RGB && tid < 28) lt[4 * ROWF - 28 + tid] = (&a.t.rgb_k[grp].w[0])[tid];
     __syncthreads();  // the near field is read-only from here on
     for (;;) {
         int u = 0;

@@ -102,7 +102,7 @@ def test_replay_irradiance_and_image(mpss, oracle, name, lights):
     assert np.array_equal(_render(torch, ctx, sc, [tiles[i] for i in rng.permutation(len(tiles))]), full)
     ctx.close()
     from mpss import pbrtscene
-    ctx2 = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=8, max_batch_samples=1 << 16)
+    ctx2 = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=8, max_batch_samples=1 << 10)
     ctx2.set_irradiance_points(pts["p"], pts["n"], got_E, pts["area"])
     ctx2.set_instrumentation(kernel_timing=True)
     assert np.array_equal(_render_many(torch, ctx2, sc, tiles), full)
