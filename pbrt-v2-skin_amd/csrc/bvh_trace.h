@@ -2,7 +2,10 @@
 // reference-sampler replay generator (replay_gen.hip): the node-bounds test and Scene::IntersectP.
 #pragma once
 #include "geom.h"
+#include "mo_band.h"
 #include "render.h"
+
+#include <climits>
 
 namespace mpss {
 
@@ -62,5 +65,70 @@ __device__ inline bool trace_any(const RenderScene &sc, V3 o, V3 d, float mint, 
     }
     return false;
 }
+
+namespace {
+// Sphere::Intersect out of line: its double-precision atan2 (the phi test) would otherwise set the
+// register budget of every kernel that inlines a light loop.
+__device__ __noinline__ bool sphere_hit_ool(const SphereView &s, V3 o, V3 d, float mint, float maxt, float &thit,
+                                            V3 *nn) {
+    return sphere_intersect(s, o, d, mint, maxt, thit, nn);
+}
+
+// Scene::IntersectP (bvh.cpp:442-488 + Sphere::IntersectP) for every active lane, as trace_any,
+// by a stackless walk of the threaded BVH: pre-order, so after an interior node the walk goes on at
+// node + 1 when some lane hit its box and at its subtree's end (the threaded offset) otherwise. A
+// lane evaluates a node when node >= its resume index; missing a box sets resume to the subtree's
+// end, a hit ends the lane. Each lane tests exactly the nodes and triangles its own traversal
+// reaches with the fixed maxt (any-hit prunes only by the box test, so the order does not change
+// the answer). strict: a triangle counts only when t < maxt (the BSDF ray toward an area light,
+// whose own surface is at maxt). spheres: test the area-light spheres first, as trace_any does.
+__device__ bool trace_any_wave(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, bool active, bool strict,
+                               bool spheres) {
+    bool hit = false;
+    if (active && spheres)
+        for (int l = 0; l < sc.nlights; ++l) {
+            float t;
+            if (!sc.lights[l].kind && sphere_hit_ool(sc.lights[l].s, o, d, mint, maxt, t, nullptr)) {
+                hit = true;
+                break;
+            }
+        }
+    const V3 inv = V3{1.f / d.x, 1.f / d.y, 1.f / d.z};
+    const int neg[3] = {inv.x < 0.f, inv.y < 0.f, inv.z < 0.f};
+    int resume = (active && !hit) ? 0 : INT_MAX;
+    const cptr<BvhNode> nodes = as_const(sc.bvh_thread);
+    const cptr<TriRec> tris = as_const(sc.tris);
+    int node = 0;
+    while (node < sc.nbvh) {
+        node = __builtin_amdgcn_readfirstlane(node);
+        const BvhNode n = nodes[node];
+        const bool act = node >= resume;
+        const bool in = act && bbox_hit(n, o, inv, neg, mint, maxt);
+        if (act && !in) resume = n.nprims > 0 ? node + 1 : n.offset;
+        if (n.nprims > 0) {
+            if (__builtin_amdgcn_ballot_w64(in) != 0) {
+                bool found = false;
+                for (int i = 0; i < (int)n.nprims; ++i) {
+                    const TriRec tr = tris[n.offset + i];
+                    float t, b1, b2;
+                    if (in && !found &&
+                        tri_intersect(o, d, mint, maxt, V3{tr.p1[0], tr.p1[1], tr.p1[2]},
+                                      V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2))
+                        found = !strict || t < maxt;
+                }
+                if (found) {
+                    hit = true;
+                    resume = INT_MAX;
+                }
+                if (__builtin_amdgcn_ballot_w64(resume != INT_MAX) == 0) break;  // every lane is done
+            }
+            node = node + 1;
+        } else {
+            node = __builtin_amdgcn_ballot_w64(in) != 0 ? node + 1 : n.offset;
+        }
+    }
+    return hit;
+}
+}  // namespace
 
 }  // namespace mpss

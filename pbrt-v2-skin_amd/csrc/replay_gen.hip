@@ -167,15 +167,12 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
     if (ix0 >= ix1 || iy0 >= iy1) return;
     const int tw = x1 - x0, spp = g.spp;
     const int first = (iy0 - y0) * tw + (ix0 - x0), last = (iy1 - 1 - y0) * tw + (ix1 - 1 - x0);
-    // this wave's LDS: state [624], draw buffer [max(spp, 64 nmax, 2)], idx [spp], sig [spp nmax bytes];
-    // then the workgroup's traversal stacks
+    // this wave's LDS: state [624], draw buffer [max(spp, 64 nmax, 2)], idx [spp], sig [spp nmax bytes]
     uint32_t *base = smem + (size_t)wv * words;
     WaveMt mt{base, 624};
     uint32_t *db = base + 624;
     uint32_t *idx = db + max(max(spp, 64 * g.nmax), 2);
     uint8_t *sig = (uint8_t *)(idx + spp);
-    int *stk = (int *)(smem + (size_t)nwv * words) + threadIdx.x;
-    const int sstride = (int)blockDim.x;
 
     uint32_t *gst = g.cur.mt + (size_t)task * 624;
     int ord = g.cur.cur_pix[task];
@@ -202,22 +199,19 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         int hits = 0;
         for (int c = 0; c < spp; c += 64) {
             const int i = c + lane;
-            bool hit = false;
-            if (i < spp) {
-                const uint32_t b = idx[i];
-                const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
-                if (keep) {
-                    put(0, i, u);
-                    put(1, i, v);
-                }
-                if (g.li_draws > 0) {  // the camera ray (samplerrenderer.cpp:97-103): only whether it hits
-                    const float X = (float)x + u, Y = (float)y + v;
-                    const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
-                    const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
-                    hit = trace_any(sc, cam_o, d, 0.f, INFINITY, stk, sstride);
-                }
+            const uint32_t b = idx[i < spp ? i : 0];
+            const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
+            if (keep && i < spp) {
+                put(0, i, u);
+                put(1, i, v);
             }
-            hits += __popcll(__ballot(hit));
+            if (g.li_draws > 0) {  // the camera rays (samplerrenderer.cpp:97-103): only whether they hit
+                const float X = (float)x + u, Y = (float)y + v;
+                const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
+                const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
+                const bool hit = trace_any_wave(sc, cam_o, d, 0.f, INFINITY, i < spp, false, true);
+                hits += __popcll(__ballot(hit && i < spp));
+            }
         }
         mt.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
         mt.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
@@ -316,9 +310,7 @@ void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStrea
     if (w.nmax < 1 || w.nmax > 256) throw Error(MPSS_ERR_INVALID, "replay: light sample counts must be in [1, 256]");
     if (w.spp < 1 || w.spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay: spp out of range");
     const int words = 624 + std::max(std::max(w.spp, 64 * w.nmax), 2) + w.spp + (w.spp * w.nmax + 3) / 4;
-    auto lds_of = [&](int nwv) {
-        return sizeof(uint32_t) * ((size_t)nwv * words + (size_t)kTraceStack * 64 * nwv);
-    };
+    auto lds_of = [&](int nwv) { return sizeof(uint32_t) * (size_t)nwv * words; };
     int nwv = kMaxWaves;
     while (nwv > 1 && lds_of(nwv) > 64 * 1024) --nwv;  // two workgroups per CU where it fits
     const size_t lds = lds_of(nwv);
