@@ -97,6 +97,8 @@ struct ReplayWindow {
     int xo0, nxr, yo0, nyr;    // the tasks meeting the window: columns xo0.., rows yo0..
     int x0, y0, w, h;          // the window (pixels of the sample extent)
     int spp, K, li_draws, nmax;  // nmax: the largest light-sample count (array length)
+    int nlights, arr_draws;      // arr_draws: the draws of a pixel's read light arrays, sum over
+                                 // lights of 3 (spp n + spp) + 5
     ReplayCursors cur;
     float *out;                // the window table (RenderScene::replay layout)
 };

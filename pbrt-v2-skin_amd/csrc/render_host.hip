@@ -592,7 +592,13 @@ void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp,
     w.K = replay_k_;
     w.li_draws = (cfg_.max_depth > 0 && !cfg_.show_irradiance_points) ? kReplayLiDraws : 0;
     w.nmax = 1;
-    for (const SceneLight &l : scene_.lights) w.nmax = std::max(w.nmax, round_up_pow2(l.nsamples));
+    w.nlights = (int)scene_.lights.size();
+    w.arr_draws = 0;
+    for (const SceneLight &l : scene_.lights) {
+        const int n = round_up_pow2(l.nsamples);
+        w.nmax = std::max(w.nmax, n);
+        w.arr_draws += 3 * (spp * n + spp) + 5;
+    }
     w.cur = ReplayCursors{ws->rp_mt.ptr, ws->rp_pix.ptr, ws->rp_mti.ptr};
     w.out = ws->rp_table.ptr;
     launch_replay_window(sc, w, stream);

@@ -41,8 +41,9 @@ constexpr int kReplayImage = 2, kReplayPerLightSample = 5;
 constexpr int kReplayLiDraws = 6;
 // the largest (power-of-two) spp the replay generator takes: one pixel's index arrays live in LDS
 constexpr int kReplayMaxSpp = 4096;
-// the largest window table of one render batch (floats: 2 GiB); render_tiles closes a batch before it
-constexpr int64_t kReplayWindowFloats = (int64_t)1 << 29;
+// the largest window table of one render batch (floats: 8 GiB of the 288 GB); render_tiles closes a
+// batch before it. (Larger windows replay more tasks at once: one wave per task is the unit.)
+constexpr int64_t kReplayWindowFloats = (int64_t)1 << 31;
 
 MPSS_HD int replay_round_up_pow2(int v) {
     int r = 1;

@@ -111,47 +111,54 @@ struct WaveMt {
     }
 };
 
-// Shuffle(samples, count, dims) of whole samples (its count draws), replayed on idx: idx[i] = the
-// original sample at position i afterwards
-__device__ void block_shuffle(WaveMt &mt, uint32_t *db, uint32_t *idx, int count) {
-    const int lane = lane_id();
-    mt.fetch(db, count);
-    for (int i = lane; i < count; i += 64) {
+// Shuffle(samples, count, dims) of whole samples replayed on idx (idx[i] = the original sample at
+// position i afterwards), from its count draws already in d: first each draw becomes its swap
+// partner i + d[i] % (count - i) (all lanes), then the swaps run in order on lane `who`
+__device__ void shuffle_partners(uint32_t *d, uint32_t *idx, int count) {
+    for (int i = lane_id(); i < count; i += 64) {
         idx[i] = (uint32_t)i;
-        db[i] = (uint32_t)i + db[i] % (uint32_t)(count - i);
+        d[i] = (uint32_t)i + d[i] % (uint32_t)(count - i);
     }
-    wave_sync();
-    if (lane == 0)
-        for (int i = 0; i < count; ++i) {
-            const uint32_t o = db[i];
-            if (o != (uint32_t)i) {
-                const uint32_t t = idx[i];
-                idx[i] = idx[o];
-                idx[o] = t;
-            }
-        }
-    wave_sync();
+}
+__device__ void shuffle_swaps(const uint32_t *o, uint32_t *idx, int count) {
+    for (int i = 0; i < count; ++i) {
+        const uint32_t p = o[i];
+        const uint32_t t = idx[i];
+        idx[i] = idx[p];
+        idx[p] = t;
+    }
 }
 
-// Each sample's Shuffle of its own n values (n draws per sample, samples in order), replayed on
-// sig: sig[i * n + j] = the original value at position j of sample i afterwards
-__device__ void own_shuffles(WaveMt &mt, uint32_t *db, uint8_t *sig, int spp, int n) {
-    const int lane = lane_id();
-    for (int c = 0; c < spp; c += 64) {
-        const int cnt = min(64, spp - c);
-        mt.fetch(db, cnt * n);
-        if (lane < cnt) {
-            uint8_t *s = sig + (size_t)(c + lane) * n;
-            for (int j = 0; j < n; ++j) s[j] = (uint8_t)j;
-            for (int j = 0; j < n; ++j) {
-                const int o = j + (int)(db[lane * n + j] % (uint32_t)(n - j));
-                const uint8_t t = s[j];
-                s[j] = s[o];
-                s[o] = t;
-            }
-        }
-        wave_sync();
+// One of a pixel's light-sample arrays (LDShuffleScrambled1D/2D(n, spp)): its draws in stream order
+// at d -- hdr scrambles, spp x n own-shuffle draws, spp block-shuffle draws.
+struct ReplayArray {
+    uint32_t *d;
+    uint32_t *idx;  // [spp]
+    uint8_t *sig;   // [spp][n]
+    int n, hdr, col;  // col: the first window-table column (-1: not read, only drawn)
+};
+
+// The arrays of a pixel after its image array that the kernels read, in LDPixelSample's order:
+// per light the BSDF component (1D, column 2), then per light the light position (2D, columns 0-1)
+// and the BSDF direction (2D, columns 3-4). (The light components and the emission integrator's
+// two 1D(1) arrays are drawn between them and not read.) Array a of 3 x nlights, its draws at
+// adraw + the draws of the arrays before it.
+__device__ ReplayArray replay_array(const RenderScene &sc, int spp, int nmax, uint32_t *adraw, uint32_t *aidx,
+                                    uint8_t *asig, int a) {
+    const int nl = sc.nlights;
+    auto shape = [&](int b, int &n, int &hdr, int &col) {
+        const int l = b < nl ? b : (b - nl) >> 1;
+        n = sc.lights[l].nsamples_round;
+        hdr = b < nl ? 1 : 2;
+        col = sc.lights[l].replay_off + (b < nl ? 2 : (((b - nl) & 1) ? 3 : 0));
+    };
+    int off = 0, n, hdr, col;
+    for (int b = 0; b < a; ++b) {
+        shape(b, n, hdr, col);
+        off += hdr + spp * n + spp;
     }
+    shape(a, n, hdr, col);
+    return ReplayArray{adraw + off, aidx + (size_t)a * spp, asig + (size_t)a * spp * nmax, n, hdr, col};
 }
 
 __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderScene sc, ReplayWindow g, int words) {
@@ -167,12 +174,17 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
     if (ix0 >= ix1 || iy0 >= iy1) return;
     const int tw = x1 - x0, spp = g.spp;
     const int first = (iy0 - y0) * tw + (ix0 - x0), last = (iy1 - 1 - y0) * tw + (ix1 - 1 - x0);
-    // this wave's LDS: state [624], draw buffer [max(spp, 64 nmax, 2)], idx [spp], sig [spp nmax bytes]
+    // this wave's LDS (replay_lds_words): state [624], image draws [max(spp, 2)], image idx [spp], the
+    // arrays' draws, idx [arrays][spp], sig [arrays][spp][nmax] bytes
     uint32_t *base = smem + (size_t)wv * words;
     WaveMt mt{base, 624};
-    uint32_t *db = base + 624;
-    uint32_t *idx = db + max(max(spp, 64 * g.nmax), 2);
-    uint8_t *sig = (uint8_t *)(idx + spp);
+    uint32_t *dimg = base + 624;
+    uint32_t *idx0 = dimg + max(spp, 2);
+    uint32_t *adraw = idx0 + spp;
+    uint32_t *aidx = adraw + g.arr_draws;
+    const int na = 3 * sc.nlights;
+    uint8_t *asig = (uint8_t *)(aidx + (size_t)na * spp);
+    auto array = [&](int a) { return replay_array(sc, spp, g.nmax, adraw, aidx, asig, a); };
 
     uint32_t *gst = g.cur.mt + (size_t)task * 624;
     int ord = g.cur.cur_pix[task];
@@ -195,11 +207,15 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         // image: LDShuffleScrambled2D(1, spp); its own-value shuffles (1 draw each) keep the order
         const uint2 si = mt.two();
         mt.skip(spp);
-        block_shuffle(mt, db, idx, spp);
+        mt.fetch(dimg, spp);
+        shuffle_partners(dimg, idx0, spp);
+        wave_sync();
+        if (lane == 0) shuffle_swaps(dimg, idx0, spp);
+        wave_sync();
         int hits = 0;
         for (int c = 0; c < spp; c += 64) {
             const int i = c + lane;
-            const uint32_t b = idx[i < spp ? i : 0];
+            const uint32_t b = idx0[i < spp ? i : 0];
             const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
             if (keep && i < spp) {
                 put(0, i, u);
@@ -215,47 +231,56 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         }
         mt.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
         mt.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
-        // 1D arrays, per light: the light component (not read here), the BSDF component (column 2)
+        // every light array's draws, in stream order (the light components and the emission
+        // arrays only advance the stream)
         for (int l = 0; l < sc.nlights; ++l) {
-            const RenderLight &L = sc.lights[l];
-            const int n = L.nsamples_round;
-            mt.skip(1 + (int64_t)spp * n + spp);
-            const uint32_t scr = mt.one();
-            own_shuffles(mt, db, sig, spp, n);
-            block_shuffle(mt, db, idx, spp);
-            if (keep)
-                for (int i = lane; i < spp; i += 64) {
-                    const uint32_t b = idx[i];
-                    const uint8_t *s = sig + (size_t)b * n;
-                    for (int j = 0; j < n; ++j)
-                        put(L.replay_off + j * kReplayPerLightSample + 2, i, van_der_corput(b * n + s[j], scr));
-                }
-            wave_sync();
+            mt.skip(1 + (int64_t)spp * sc.lights[l].nsamples_round + spp);
+            const ReplayArray A = array(l);
+            mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
-        mt.skip(2 * (1 + 2 * (int64_t)spp));  // the emission integrator's two 1D(1) arrays
-        // 2D arrays, per light: light position (columns 0, 1), BSDF direction (3, 4)
-        for (int l = 0; l < sc.nlights; ++l) {
-            const RenderLight &L = sc.lights[l];
-            const int n = L.nsamples_round;
-            for (int arr = 0; arr < 2; ++arr) {
-                const uint2 s2 = mt.two();
-                own_shuffles(mt, db, sig, spp, n);
-                block_shuffle(mt, db, idx, spp);
-                if (keep) {
-                    const int col = L.replay_off + (arr == 0 ? 0 : 3);
-                    for (int i = lane; i < spp; i += 64) {
-                        const uint32_t b = idx[i];
-                        const uint8_t *s = sig + (size_t)b * n;
-                        for (int j = 0; j < n; ++j) {
-                            const uint32_t k = b * n + s[j];
-                            put(col + j * kReplayPerLightSample, i, van_der_corput(k, s2.x));
-                            put(col + j * kReplayPerLightSample + 1, i, sobol2(k, s2.y));
-                        }
+        mt.skip(2 * (1 + 2 * (int64_t)spp));
+        for (int a = sc.nlights; a < na; ++a) {
+            const ReplayArray A = array(a);
+            mt.fetch(A.d, A.hdr + spp * A.n + spp);
+        }
+        // each sample's own shuffle (lane per sample) and each array's block-shuffle partners
+        for (int a = 0; a < na; ++a) {
+            const ReplayArray A = array(a);
+            for (int i = lane; i < spp; i += 64) {
+                uint8_t *sg = A.sig + (size_t)i * A.n;
+                const uint32_t *dd = A.d + A.hdr + i * A.n;
+                for (int j = 0; j < A.n; ++j) sg[j] = (uint8_t)j;
+                for (int j = 0; j < A.n; ++j) {
+                    const int o = j + (int)(dd[j] % (uint32_t)(A.n - j));
+                    const uint8_t t = sg[j];
+                    sg[j] = sg[o];
+                    sg[o] = t;
+                }
+            }
+            shuffle_partners(A.d + A.hdr + spp * A.n, A.idx, spp);
+        }
+        wave_sync();
+        // the block shuffles: array a's swaps on lane a, all arrays at once
+        if (lane < na) {
+            const ReplayArray A = array(lane);
+            shuffle_swaps(A.d + A.hdr + spp * A.n, A.idx, spp);
+        }
+        wave_sync();
+        if (keep)
+            for (int a = 0; a < na; ++a) {
+                const ReplayArray A = array(a);
+                const uint32_t s0 = A.d[0], s1 = A.d[A.hdr - 1];
+                for (int i = lane; i < spp; i += 64) {
+                    const uint32_t b = A.idx[i];
+                    const uint8_t *sg = A.sig + (size_t)b * A.n;
+                    for (int j = 0; j < A.n; ++j) {
+                        const uint32_t k = b * A.n + sg[j];
+                        put(A.col + j * kReplayPerLightSample, i, van_der_corput(k, s0));
+                        if (A.hdr == 2) put(A.col + j * kReplayPerLightSample + 1, i, sobol2(k, s1));
                     }
                 }
-                wave_sync();
             }
-        }
+        wave_sync();
         mt.skip((int64_t)g.li_draws * hits);  // Li, per camera ray that hits
     }
     for (int k = lane; k < 624; k += 64) gst[k] = mt.st[k];
@@ -309,7 +334,9 @@ void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStrea
     if (nw <= 0) return;
     if (w.nmax < 1 || w.nmax > 256) throw Error(MPSS_ERR_INVALID, "replay: light sample counts must be in [1, 256]");
     if (w.spp < 1 || w.spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay: spp out of range");
-    const int words = 624 + std::max(std::max(w.spp, 64 * w.nmax), 2) + w.spp + (w.spp * w.nmax + 3) / 4;
+    // state, image draws and idx, the arrays' draws, idx and sig (replay_window_kernel)
+    const int na = 3 * w.nlights;
+    const int words = 624 + std::max(w.spp, 2) + w.spp + w.arr_draws + na * w.spp + (na * w.spp * w.nmax + 3) / 4;
     auto lds_of = [&](int nwv) { return sizeof(uint32_t) * (size_t)nwv * words; };
     int nwv = kMaxWaves;
     while (nwv > 1 && lds_of(nwv) > 64 * 1024) --nwv;  // two workgroups per CU where it fits
