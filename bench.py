@@ -47,7 +47,7 @@ REF_RECORD_BYTES = 12 + 4 + 4 * 30  # position, area / sumArea, 30-ba
 L2_GATHER_CEILING_REQ_S = 2.69e11
 # sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
 KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
-                  "pbrt-v2-skin_amd/csrc/octree.h")
+                  "pbrt-v2-skin_amd/csrc/mo_wave.h", "pbrt-v2-skin_amd/csrc/octree.h")
 
 
 # BASELINE.json configs this bench runs: (label, resolution, spp, default scaling, mesh subdivision
