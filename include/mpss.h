@@ -381,14 +381,11 @@ int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, 
  * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim /
  * u1start [8] (lanes with u < u0lim read the exact LDS near field, u1start <= u < u1lim the rows, any
  * other u the bands' own tables; u1start = u0lim unless the rows begin past the end of bands the grid
- * cannot follow); row0 / ubase [8]; the coarse tail u2lim / row2 / vbase [8] (lanes with u1lim <= u <
- * u2lim read row row2 + floor(u / 16) - vbase, holding R_j(16 m), R_j(16 m + 16); u2lim = u1lim: none);
- * rel_err / l1_err [30] (the measured resampling error over the knots each band reads from the
- * rows); *ok = 1 when some group has rows. */
+ * cannot follow); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over the
+ * knots each band reads from the rows); *ok = 1 when some group has rows. */
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
                           int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
-                          uint32_t *ubase, float *u2lim, uint32_t *row2, uint32_t *vbase, float *rel_err,
-                          float *l1_err, int *ok);
+                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok);
 /* Octree build + pre-order export (sizes first with NULL outputs). */
 int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
                             uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,

@@ -34,8 +34,6 @@
 namespace mpss {
 
 constexpr int kGroups = 8;
-// the common grid's coarse tail: rows every kCgCoarse grid steps (CommonGrid::u2lim)
-constexpr int kCgCoarse = 16;
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -111,10 +109,6 @@ struct CommonGrid {
     float u0lim[kGroups];       // u < u0lim => every band's pair (s, s + 1) lies in its LDS near field
     float u1lim[kGroups];       // u1start <= u < u1lim: the pair rows (u1lim = u0lim: none)
     float u1start[kGroups];     // (u0lim, or past the end of the bands the rows cannot serve)
-    // the coarse tail: u1lim <= u < u2lim reads rows on a grid kCgCoarse times coarser (v = u /
-    // kCgCoarse, exact): group g's row for v at row2[g] + floor(v) - vbase[g] (u2lim = u1lim: none)
-    float u2lim[kGroups];
-    uint32_t row2[kGroups], vbase[kGroups];
     float tau[kGroups][4];      // d2 >= tau <=> fl(d2 * rcp) >= L - 1: the band is past its profile end
     uint32_t lrow[kGroups][4];  // float offset of slot j's near-field row in LDS (entries 0..klim_j)
     int lcnt[kGroups][4];       // its length, klim_j + 1 floats (2 zeros for an empty slot)
@@ -348,8 +342,7 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
 struct CgLane {
     const float4 *tab;    // the pair rows, indexed by u0 + rowoff
     uint32_t rowoff;      // row0 - ubase (mod 2^32)
-    uint32_t rowoff2;     // row2 - vbase (mod 2^32): the coarse tail's rows
-    float rg, u0lim, u1lim, u1start, u2lim;
+    float rg, u0lim, u1lim, u1start;
     float tau[4];
     float tau_min;        // the group's first profile end
     uint32_t lrow[4];     // LDS float offsets of the slots' exact near-field rows
@@ -407,14 +400,11 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // earlier step's loads target only once those have returned, and LDS returns first (the
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
     // issue order (vector memory returns in order), so the second does not wait for the first.
-    const int path = u < c.u0lim ? 1 : ((u < c.u2lim && u >= c.u1start) ? 0 : 2);
-    // the coarse tail: its grid is u / kCgCoarse (a power of two: the scaling is exact)
-    const bool coarse = u >= c.u1lim;
-    const float uu = coarse ? u * (1.f / (float)kCgCoarse) : u;
+    const int path = u < c.u0lim ? 1 : ((u < c.u1lim && u >= c.u1start) ? 0 : 2);
     // both global steps' addresses up front, so the allocator cannot place one step's address in
     // registers the other step's loads are still filling (that would wait for those loads); as 32-bit
     // byte offsets from the (wave-uniform) table bases: one VGPR each, global loads in saddr form
-    uint32_t orow = 32u * ((uint32_t)uu + (coarse ? c.rowoff2 : c.rowoff)), otp[4];
+    uint32_t orow = 32u * ((uint32_t)u + c.rowoff), otp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
@@ -435,7 +425,7 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
         r.p01 = row[0];
         r.p23 = row[1];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r.f[j] = uu;
+        for (int j = 0; j < 4; ++j) r.f[j] = u;
     }
     if (path == 2) {
         const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
@@ -545,8 +535,6 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         cl.u0lim = a.cg.u0lim[grp];
         cl.u1lim = a.cg.u1lim[grp];
         cl.u1start = a.cg.u1start[grp];
-        cl.u2lim = a.cg.u2lim[grp];
-        cl.rowoff2 = a.cg.row2[grp] - a.cg.vbase[grp];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             cl.tau[j] = a.cg.tau[grp][j];

@@ -526,7 +526,6 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
-constexpr int kCgMaxCoarseRows = 16384;  // (the coarse tail's rows per group: at most 512 KB)
 static int cg_max_rows() {  // (experiment: MPSS_CG_MAX_ROWS)
     static const int v = [] {
         const char *e = getenv("MPSS_CG_MAX_ROWS");
@@ -704,7 +703,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         u1 = std::min<int64_t>(u1, (int64_t)L - 1);
         cg.ubase[g] = (uint32_t)ubase;
         if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
-            cg.u1lim[g] = cg.u1start[g] = cg.u2lim[g] = u0f;
+            cg.u1lim[g] = cg.u1start[g] = u0f;
             continue;
         }
         cg.u1start[g] = (float)start;  // (u0f, or an integer below 2^24)
@@ -719,75 +718,6 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             h.push_back(make_float4(v[2][0], v[2][1], v[3][0], v[3][1]));
         }
         any = true;
-        // The coarse tail (CommonGrid::u2lim): past u1 the rows go on every kCgCoarse grid steps, the
-        // same per-knot bound deciding how far (the tails are smooth at the bound's absolute floor:
-        // on C2's profile most groups' coarse rows reach the table's end). Row m holds R_j(K m) and
-        // R_j(K m + K); a lane reads row floor(u / K) with t = fract(u / K).
-        cg.u2lim[g] = cg.u1lim[g];
-        cg.row2[g] = (uint32_t)(h.size() / 2);
-        cg.vbase[g] = 0;
-        {
-            const double U1 = (double)cg.u1lim[g], K = (double)kCgCoarse;
-            double cbad = (double)L;  // the first coarse bad knot
-            for (int j = 0; j < 4; ++j) {
-                const int c = groups.band[g][j];
-                if (c < 0) continue;
-                const float *T = tab + (size_t)c * L;
-                for (int k = std::max(0, (int)std::floor(U1 * r[j]) - 1); k < L - 1; ++k) {
-                    const double u = (double)k / r[j];
-                    if (u < U1) continue;
-                    if (u >= cbad) break;
-                    const double v = u / K;
-                    const int64_t m = (int64_t)std::floor(v);
-                    const double t = v - (double)m;
-                    const double approx = (1.0 - t) * R(j, m * kCgCoarse) + t * R(j, (m + 1) * kCgCoarse);
-                    const double err = std::fabs(approx - (double)T[k]);
-                    if (err > std::max(kCgRelTol * std::fabs((double)T[k]), kCgAbsTol * peak[j])) {
-                        cbad = u;
-                        break;
-                    }
-                }
-            }
-            const int64_t m0 = (int64_t)std::floor(U1 / K);
-            int64_t m1 = (int64_t)std::floor(cbad / K) - 1;  // cells m0 .. m1 - 1 (a cell of margin)
-            m1 = std::min<int64_t>(m1, m0 + kCgMaxCoarseRows);
-            if (m1 > m0 + 1) {
-                cg.vbase[g] = (uint32_t)m0;
-                cg.u2lim[g] = (float)(K * (double)m1);  // lanes with u < K m1 read rows m <= m1 - 1
-                for (int64_t m = m0; m < m1; ++m) {
-                    float v[4][2];
-                    for (int j = 0; j < 4; ++j) {
-                        v[j][0] = R(j, m * kCgCoarse);
-                        v[j][1] = R(j, (m + 1) * kCgCoarse);
-                    }
-                    h.push_back(make_float4(v[0][0], v[0][1], v[1][0], v[1][1]));
-                    h.push_back(make_float4(v[2][0], v[2][1], v[3][0], v[3][1]));
-                }
-                // the coarse knots' errors join the served range's statistics
-                for (int j = 0; j < 4; ++j) {
-                    const int c = groups.band[g][j];
-                    if (c < 0) continue;
-                    const float *T = tab + (size_t)c * L;
-                    double l1 = 0.0, esum = 0.0, emax = (double)cg_rel_err[c];
-                    for (int k = 0; k < L; ++k) l1 += std::fabs(T[k]);
-                    for (int k = std::max(0, (int)std::floor(U1 * r[j]) - 1); k < L - 1; ++k) {
-                        const double u = (double)k / r[j];
-                        if (u < U1) continue;
-                        if (u >= (double)cg.u2lim[g]) break;
-                        const double v = u / K;
-                        const int64_t m = (int64_t)std::floor(v);
-                        const double t = v - (double)m;
-                        const double approx = (1.0 - t) * R(j, m * kCgCoarse) + t * R(j, (m + 1) * kCgCoarse);
-                        const double e = std::fabs(approx - (double)T[k]);
-                        if (kCgRelTol * std::fabs((double)T[k]) >= kCgAbsTol * peak[j])
-                            emax = std::max(emax, e / std::fabs((double)T[k]));
-                        esum += e;
-                    }
-                    cg_rel_err[c] = (float)emax;
-                    cg_l1_err[c] += (float)(l1 > 0.0 ? esum / l1 : 0.0);
-                }
-            }
-        }
     }
     cg.on = any ? 1 : 0;
     return any;

@@ -183,8 +183,7 @@ int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len,
 
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
                           int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
-                          uint32_t *ubase, float *u2lim, uint32_t *row2, uint32_t *vbase, float *rel_err,
-                          float *l1_err, int *ok) {
+                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok) {
     return guarded([&] {
         require(table && rcp && ok, "mpss_host_common_grid: null argument");
         require(L >= 2 && L < (1u << 24), "mpss_host_common_grid: L out of range");
@@ -209,9 +208,6 @@ int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int 
             if (u0lim) u0lim[k] = cg.u0lim[k];
             if (u1lim) u1lim[k] = cg.u1lim[k];
             if (u1start) u1start[k] = cg.u1start[k];
-            if (u2lim) u2lim[k] = cg.u2lim[k];
-            if (row2) row2[k] = cg.row2[k];
-            if (vbase) vbase[k] = cg.vbase[k];
             if (row0) row0[k] = cg.row0[k];
             if (ubase) ubase[k] = cg.ubase[k];
         }
