@@ -526,6 +526,13 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
+static double cg_abs_tol() {  // (experiment: MPSS_CG_ABS_TOL)
+    static const double v = [] {
+        const char *e = getenv("MPSS_CG_ABS_TOL");
+        return e ? atof(e) : kCgAbsTol;
+    }();
+    return v;
+}
 static int cg_max_rows() {  // (experiment: MPSS_CG_MAX_ROWS)
     static const int v = [] {
         const char *e = getenv("MPSS_CG_MAX_ROWS");
@@ -653,7 +660,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             const double t = u - (double)ui;
             const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
             const double err = std::fabs(approx - (double)T[k]);
-            return err > std::max(kCgRelTol * std::fabs((double)T[k]), kCgAbsTol * peak[j]) ? INFINITY : err;
+            return err > std::max(kCgRelTol * std::fabs((double)T[k]), cg_abs_tol() * peak[j]) ? INFINITY : err;
         };
         std::vector<double> bad;
         for (int j = 0; j < 4; ++j) {
@@ -690,7 +697,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 if (u >= ubad) break;
                 const double e = knot_err(j, k);
                 // (relative error where the relative bound governs: |T| >= kCgAbsTol / kCgRelTol of the peak)
-                if (kCgRelTol * std::fabs((double)T[k]) >= kCgAbsTol * peak[j])
+                if (kCgRelTol * std::fabs((double)T[k]) >= cg_abs_tol() * peak[j])
                     emax = std::max(emax, e / std::fabs((double)T[k]));
                 esum += e;
             }

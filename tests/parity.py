@@ -23,7 +23,12 @@ def image_errors(got, ref):
     nz = r != 0
     rel = err[nz] / np.abs(r[nz])
     floored = err / (TOL * np.maximum(np.abs(r), 1e-3 * peak)) if peak > 0 else err
-    return {"peak": peak, "rel_linf": float(rel.max()) if rel.size else 0.0,
+    # the relative error over the values above a fraction of the peak (where the worst one sits)
+    above = {}
+    for fr in (1e-3, 1e-5, 1e-7, 1e-9):
+        sel = np.abs(r[nz]) >= fr * peak
+        above["%g" % fr] = float(rel[sel].max()) if sel.any() else 0.0
+    return {"peak": peak, "rel_linf": float(rel.max()) if rel.size else 0.0, "rel_linf_above": above,
             "rel_linf_at_value": float(np.abs(r[nz])[rel.argmax()] / peak) if rel.size and peak > 0 else None,
             "rel_p999": float(np.quantile(rel, 0.999)) if rel.size else 0.0,
             "zero_mismatch": int(((r == 0) != (g == 0)).sum()),
