@@ -75,12 +75,14 @@ struct DeviceProfile {
 };
 
 // The common grid's bound on the resampling error of a lookup: kCgRelTol of the band's own value
-// there, or kCgAbsTol of the band's peak where that is larger (the far tails, whose values are
-// 1e-5 .. 1e-11 of the peak and carry under 1 % of a band's mass on C2's profile: there the bound
-// is absolute). DeviceProfile::build_common; the group rows cover only the range where every band is
-// within it.
+// there, or kCgAbsTol of the band's peak where that is larger (the far tails, whose values fall to
+// 1e-11 of the peak and carry under 1 % of a band's mass on C2's profile: there the bound is
+// absolute). DeviceProfile::build_common; the group rows cover only the range where every band is
+// within it. The floor is chosen on the full C2 frame against the oracle (profiles/r04p_abstol.txt):
+// 0: gather 60.4 ms, unfloored image error 1.1e-6; 1e-13: 48.6 ms, 4.3e-6; 1e-10: 47.1 ms, 9.0e-5
+// (all three at values far below the film's resolution, 1e-16 of the frame's peak).
 constexpr double kCgRelTol = 2e-6;
-constexpr double kCgAbsTol = 1e-10;
+constexpr double kCgAbsTol = 1e-13;
 
 // The host half of DeviceProfile::build_common: the layout (cg, without tab), the pair rows h (two
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group

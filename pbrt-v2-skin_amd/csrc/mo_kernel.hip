@@ -526,20 +526,6 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
-static double cg_abs_tol() {  // (experiment: MPSS_CG_ABS_TOL)
-    static const double v = [] {
-        const char *e = getenv("MPSS_CG_ABS_TOL");
-        return e ? atof(e) : kCgAbsTol;
-    }();
-    return v;
-}
-static int cg_max_rows() {  // (experiment: MPSS_CG_MAX_ROWS)
-    static const int v = [] {
-        const char *e = getenv("MPSS_CG_MAX_ROWS");
-        return e ? atoi(e) : kCgMaxRows;
-    }();
-    return v;
-}
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field,
@@ -660,7 +646,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             const double t = u - (double)ui;
             const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
             const double err = std::fabs(approx - (double)T[k]);
-            return err > std::max(kCgRelTol * std::fabs((double)T[k]), cg_abs_tol() * peak[j]) ? INFINITY : err;
+            return err > std::max(kCgRelTol * std::fabs((double)T[k]), kCgAbsTol * peak[j]) ? INFINITY : err;
         };
         std::vector<double> bad;
         for (int j = 0; j < 4; ++j) {
@@ -675,7 +661,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             double from = u0f;  // the current stretch's first servable u
             for (const double ub : bad) {
                 if (ub >= from) {
-                    const double len = std::min(std::floor(ub) - 1.0, from + (double)cg_max_rows()) - from;
+                    const double len = std::min(std::floor(ub) - 1.0, from + (double)kCgMaxRows) - from;
                     if (len > best) {
                         best = len;
                         start = from;
@@ -697,7 +683,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 if (u >= ubad) break;
                 const double e = knot_err(j, k);
                 // (relative error where the relative bound governs: |T| >= kCgAbsTol / kCgRelTol of the peak)
-                if (kCgRelTol * std::fabs((double)T[k]) >= cg_abs_tol() * peak[j])
+                if (kCgRelTol * std::fabs((double)T[k]) >= kCgAbsTol * peak[j])
                     emax = std::max(emax, e / std::fabs((double)T[k]));
                 esum += e;
             }
@@ -706,7 +692,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         }
         const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
         int64_t u1 = (int64_t)std::floor(ubad) - 1;
-        u1 = std::min<int64_t>(u1, ubase + cg_max_rows());
+        u1 = std::min<int64_t>(u1, ubase + kCgMaxRows);
         u1 = std::min<int64_t>(u1, (int64_t)L - 1);
         cg.ubase[g] = (uint32_t)ubase;
         if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field

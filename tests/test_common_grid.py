@@ -1,7 +1,7 @@
 """The common grid of the sharded Mo() gather (mpss_config.mo_common_grid; mo_band.h CommonGrid),
 host half, on the CPU: the LDS split, the resampled pair rows and the range they serve, against a
 numpy restatement of multipole.cpp:60-73's sampleProfile (every served knot within 2e-6 of the
-band's own value, or 1e-10 of the band's peak in the far tails).
+band's own value, or 1e-13 of the band's peak in the far tails).
 
 The gather itself (LDS and own-table lanes bit-identical to the per-band gather, row lanes within
 the bound) is checked on the GPU by tests/test_mo_gpu.py and the image tests."""
@@ -13,7 +13,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.npz")
 LDS_FLOATS = 4 * (10236 + 3)
-ABS_TOL = 1e-10  # mo_kernel.h kCgAbsTol
+ABS_TOL = 1e-13  # mo_kernel.h kCgAbsTol
 
 
 def _groups(rcp):
@@ -77,7 +77,7 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None):
             t = uk - np.floor(uk)
             approx = (1 - t) * rows[ui, 2 * j] + t * rows[ui, 2 * j + 1]
             err = np.abs(approx - T64[c, k])
-            # kCgRelTol of the band's value, or kCgAbsTol = 1e-10 of its peak where that is larger
+            # kCgRelTol of the band's value, or kCgAbsTol = 1e-13 of its peak where that is larger
             bound = np.maximum(tol * np.abs(T64[c, k]), ABS_TOL * np.abs(T64[c]).max())
             assert np.all(err <= bound * (1 + 1e-9)), (g, c, (err / bound).max())
 
@@ -123,7 +123,10 @@ def test_common_grid_of_the_rgb_profile(mpss):
     assert cg["ok"]
     assert np.all(cg["bands"] == np.array([0, 1, 2, -1]))
     assert np.all(cg["rg"] == np.float32(rcp[:3].min()))
-    assert np.all(cg["u1start"] == cg["u0lim"]) and np.all(cg["u1lim"] - cg["u1start"] > 60000)
+    # B is off near the field's end (its values there still above the floor): the rows start a little
+    # past it (u1start 4185 vs u0lim 2364) and serve all three to ~70 k of G's 120 k steps
+    assert np.all(cg["u1start"] >= cg["u0lim"]) and np.all(cg["u1start"] < 2 * cg["u0lim"])
+    assert np.all(cg["u1lim"] - cg["u1start"] > 60000)
     rows = cg["rows"].reshape(8, -1, 8)
     assert np.all(rows[:, :, 6:] == 0)  # the empty slot
     assert cg["rel_err"][:3].max() <= 2e-6 and cg["l1_err"][:3].max() <= 1e-8
