@@ -345,6 +345,8 @@ def main(a):
             roofline["l2_requests_per_sss_sample"] = round(l2["requests_per_launch"] * launches_per_step /
                                                            max(1, cnt["sss_samples"]), 1)
             roofline["l2_hit_rate"] = l2["hit_rate"]
+        if "valu" in pt:  # the other resource the gather can run out of
+            roofline["valu_issue_frac"] = round(pt["valu"]["issue_frac"], 4)
             if roofline["traffic"] is not None:
                 roofline["hbm_gbs"] = round(roofline["traffic"] / (shade_launch_ms * 1e-3) / 1e9, 1)
                 roofline["hbm_frac"] = round(roofline["hbm_gbs"] / HBM_PEAK_GBS, 4)
@@ -461,6 +463,11 @@ def pmc_traffic(path, launch_ms, config):
     _, f, e = best
     out = {"traffic": e["fetch_bytes_corrected_mean"],
            "source": os.path.relpath(f, ROOT) + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"}
+    if "SQ_INSTS_VALU" in e and launch_ms > 0:
+        # VALU issue: wave64 instructions per launch over what 256 CUs x 4 SIMDs issue in the launch
+        # (one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz)
+        v = e["SQ_INSTS_VALU"]["mean"]
+        out["valu"] = {"insts_per_launch": v, "issue_frac": v / (launch_ms * 1e-3 * 2.4e9 * 1024 / 4)}
     if "TCP_TCC_READ_REQ_sum" in e and launch_ms > 0:
         req = e["TCP_TCC_READ_REQ_sum"]["mean"]
         out["l2"] = {"requests_per_launch": req, "achieved_req_per_s": req / (launch_ms * 1e-3),
