@@ -401,16 +401,11 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
     // issue order (vector memory returns in order), so the second does not wait for the first.
     const int path = u < c.u0lim ? 1 : ((u < c.u1lim && u >= c.u1start) ? 0 : 2);
-    // both global steps' addresses up front, so the allocator cannot place one step's address in
-    // registers the other step's loads are still filling (that would wait for those loads); as 32-bit
-    // byte offsets from the (wave-uniform) table bases: one VGPR each, global loads in saddr form
-    uint32_t orow = 32u * ((uint32_t)u + c.rowoff), otp[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
-        otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
-    }
-    asm volatile("" : "+v"(orow), "+v"(otp[0]), "+v"(otp[1]), "+v"(otp[2]), "+v"(otp[3]));
+    // the row step's address up front, as a 32-bit byte offset from the (wave-uniform) grid base: one
+    // VGPR, a global load in saddr form. (The own-table step's four addresses are formed in its branch:
+    // with the gather VALU-bound, a wave whose lanes all take the rows or the LDS does not pay them.)
+    uint32_t orow = 32u * ((uint32_t)u + c.rowoff);
+    asm volatile("" : "+v"(orow));
     if (path == 1) {  // s_j < klim_j for every band: inside its LDS row
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
         const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
@@ -428,6 +423,12 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
         for (int j = 0; j < 4; ++j) r.f[j] = u;
     }
     if (path == 2) {
+        uint32_t otp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
+            otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
+        }
         const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
         const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
         const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
