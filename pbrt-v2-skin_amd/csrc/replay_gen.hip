@@ -204,35 +204,15 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         // value k of sample i of this pixel: out[k * npix * spp + i]
         float *out = keep ? g.out + ((int64_t)(y - g.y0) * g.w + (x - g.x0)) * spp : nullptr;
         auto put = [&](int k, int i, float v) { out[(int64_t)k * npix * spp + i] = v; };
-        // image: LDShuffleScrambled2D(1, spp); its own-value shuffles (1 draw each) keep the order
+        // every draw of the pixel's arrays first, in stream order: image (LDShuffleScrambled2D(1,
+        // spp): its own-value shuffles, 1 draw each, keep the order), lens and time (only advance the
+        // stream), then per light the light component (advances) and the BSDF component, the emission
+        // integrator's two 1D(1) arrays (advance), per light the light position and BSDF direction
         const uint2 si = mt.two();
         mt.skip(spp);
         mt.fetch(dimg, spp);
-        shuffle_partners(dimg, idx0, spp);
-        wave_sync();
-        if (lane == 0) shuffle_swaps(dimg, idx0, spp);
-        wave_sync();
-        int hits = 0;
-        for (int c = 0; c < spp; c += 64) {
-            const int i = c + lane;
-            const uint32_t b = idx0[i < spp ? i : 0];
-            const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
-            if (keep && i < spp) {
-                put(0, i, u);
-                put(1, i, v);
-            }
-            if (g.li_draws > 0) {  // the camera rays (samplerrenderer.cpp:97-103): only whether they hit
-                const float X = (float)x + u, Y = (float)y + v;
-                const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
-                const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
-                const bool hit = trace_any_wave(sc, cam_o, d, 0.f, INFINITY, i < spp, false, true);
-                hits += __popcll(__ballot(hit && i < spp));
-            }
-        }
         mt.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
         mt.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
-        // every light array's draws, in stream order (the light components and the emission
-        // arrays only advance the stream)
         for (int l = 0; l < sc.nlights; ++l) {
             mt.skip(1 + (int64_t)spp * sc.lights[l].nsamples_round + spp);
             const ReplayArray A = array(l);
@@ -243,7 +223,8 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             const ReplayArray A = array(a);
             mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
-        // each sample's own shuffle (lane per sample) and each array's block-shuffle partners
+        // each sample's own shuffle (lane per sample) and every block shuffle's partners
+        shuffle_partners(dimg, idx0, spp);
         for (int a = 0; a < na; ++a) {
             const ReplayArray A = array(a);
             for (int i = lane; i < spp; i += 64) {
@@ -260,12 +241,32 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             shuffle_partners(A.d + A.hdr + spp * A.n, A.idx, spp);
         }
         wave_sync();
-        // the block shuffles: array a's swaps on lane a, all arrays at once
-        if (lane < na) {
-            const ReplayArray A = array(lane);
+        // the block shuffles, all at once: the image's swaps on lane 0, array a's on lane a + 1
+        if (lane == 0) {
+            shuffle_swaps(dimg, idx0, spp);
+        } else if (lane <= na) {
+            const ReplayArray A = array(lane - 1);
             shuffle_swaps(A.d + A.hdr + spp * A.n, A.idx, spp);
         }
         wave_sync();
+        // the image samples and the camera rays (samplerrenderer.cpp:97-103): only whether they hit
+        int hits = 0;
+        for (int c = 0; c < spp; c += 64) {
+            const int i = c + lane;
+            const uint32_t b = idx0[i < spp ? i : 0];
+            const float u = van_der_corput(b, si.x), v = sobol2(b, si.y);
+            if (keep && i < spp) {
+                put(0, i, u);
+                put(1, i, v);
+            }
+            if (g.li_draws > 0) {
+                const float X = (float)x + u, Y = (float)y + v;
+                const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
+                const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
+                const bool hit = trace_any_wave(sc, cam_o, d, 0.f, INFINITY, i < spp, false, true);
+                hits += __popcll(__ballot(hit && i < spp));
+            }
+        }
         if (keep)
             for (int a = 0; a < na; ++a) {
                 const ReplayArray A = array(a);
