@@ -742,6 +742,10 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
             }
         }
         size_t pi = 0;
+        // replay: the current generated window (it may span several batches: one generation over
+        // more tasks keeps more waves in flight, replay_gen.hip)
+        bool have_win = false;
+        int wx0 = 0, wx1 = 0, wy0 = 0, wy1 = 0;
         while (pi < pieces.size()) {
             // pack pieces into one batch
             size_t pe = pi;
@@ -822,15 +826,33 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
                 }
             };
             hipEvent_t ev{};
-            if (replay) {  // the reference sampler's values over the batch's window
+            if (replay && (!have_win || bx0 < wx0 || bx1 > wx1 || by0 < wy0 || by1 > wy1)) {
+                // the reference sampler's values over a new window: this batch's pieces and the
+                // following ones, as far as the window table allows (kReplayWindowFloats)
+                int gx0 = bx0, gx1 = bx1, gy0 = by0, gy1 = by1;
+                for (size_t k = pe; k < pieces.size(); ++k) {
+                    const TileBatch &tb = pieces[k].tb;
+                    const int nx0 = std::min(gx0, tb.ex0), nx1 = std::max(gx1, tb.ex0 + tb.ew);
+                    const int ny0 = std::min(gy0, tb.ey0), ny1 = std::max(gy1, tb.ey0 + tb.eh);
+                    if ((int64_t)(nx1 - nx0) * (ny1 - ny0) * spp * replay_k_ > kReplayWindowFloats) break;
+                    gx0 = nx0;
+                    gx1 = nx1;
+                    gy0 = ny0;
+                    gy1 = ny1;
+                }
                 time_begin(timing, stream, ev);
-                replay_window(ws, sc, spp, bx0, bx1, by0, by1, stream);
+                replay_window(ws, sc, spp, gx0, gx1, gy0, gy1, stream);
                 time_end(timing, stream, ev, 6, timed);
+                have_win = true;
+                wx0 = gx0;
+                wx1 = gx1;
+                wy0 = gy0;
+                wy1 = gy1;
                 sc.replay = ws->rp_table.ptr;
-                sc.replay_x0 = bx0;
-                sc.replay_y0 = by0;
-                sc.replay_w = bx1 - bx0;
-                sc.replay_npix = (int64_t)(bx1 - bx0) * (by1 - by0);
+                sc.replay_x0 = wx0;
+                sc.replay_y0 = wy0;
+                sc.replay_w = wx1 - wx0;
+                sc.replay_npix = (int64_t)(wx1 - wx0) * (wy1 - wy0);
             }
             time_begin(timing, stream, ev);
             launch_pieces(false);

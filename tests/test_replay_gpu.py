@@ -106,7 +106,8 @@ def test_replay_irradiance_and_image(mpss, oracle, name, lights):
     ctx2.set_irradiance_points(pts["p"], pts["n"], got_E, pts["area"])
     ctx2.set_instrumentation(kernel_timing=True)
     assert np.array_equal(_render_many(torch, ctx2, sc, tiles), full)
-    assert ctx2.render_stats()["n_replay"] > 1
+    st = ctx2.render_stats()
+    assert st["n_camera"] > 1 and st["n_replay"] >= 1  # many batches (one window may serve several)
     ctx2.close()
 
 
