@@ -81,8 +81,9 @@ typedef struct {
                                   largest batch rendered, sized for the worst case (every sample a
                                   hit): ~280 B/sample, 18.8 GB for a full 2^26 batch of the 288 GB;
                                   at least 2^10. The reference sampler also closes a batch before
-                                  its window table (the pieces' bounding box x spp x 22 floats for
-                                  skin.pbrt) passes 2^31 floats */
+                                  its pieces' bounding box x spp x 22 floats (skin.pbrt) passes 2^31
+                                  floats, and generates its values for windows of as many
+                                  consecutive batches as that holds */
     int use_poisson_point_finder; /* "usepoissonpointfinder" = false: SurfacePoints by random-walk
                                   dart throwing (FindPoissonPointDistribution) instead of tessellation */
     int sampler;               /* MPSS_SAMPLER_HASH (default): counter-hash scrambled (0,2) sequences, a
