@@ -109,19 +109,22 @@ typedef struct {
                                   workgroups per CU, 8 waves per SIMD) or 10236 (one workgroup per CU
                                   holds the whole 160 KB, 4 waves per SIMD). With the common grid the
                                   gather waits on memory latency more than on the L2 request rate, and
-                                  8 waves hide more of it (C2: 59.4 vs 68.8 ms per frame) */
+                                  8 waves hide more of it (C2, round 4's first grid: 59.4 vs 68.8 ms
+                                  per frame) */
     int tessellate_on_host;    /* 1: Preprocess tessellates on the host (threads over triangles,
                                   scene.cpp); 0 (default): one GPU thread per triangle (render.hip
                                   tess_kernel), the same points bit for bit (tessellate.h) */
-    int mo_common_grid;        /* 1 (default): the sharded gather (mo_near_field 10236) reads a band
-                                  group's lookups past the exact LDS near field, as far as the
-                                  resampling stays within 2e-6 of each band's own value (measured at
-                                  every band knot when the material is added), from ONE table of the
-                                  group's bands resampled onto its coarsest d^2 grid: two 16-byte loads
-                                  per lookup instead of four 8-byte lerp pairs; farther lookups read the
+    int mo_common_grid;        /* 1 (default): the sharded gather reads a band group's lookups past
+                                  the exact LDS near field, as far as the resampling stays within 2e-6
+                                  of each band's own value or 1e-13 of the band's peak (measured at
+                                  every band knot when the material is added; at most 65,536 rows per
+                                  group), from ONE table of the group's bands resampled onto its
+                                  coarsest d^2 grid: two 16-byte loads from one 32-byte sector per
+                                  lookup instead of four 8-byte lerp pairs; farther lookups read the
                                   bands' own tables. Results differ from the per-band gather by at most
-                                  that relative error per term (mpss_get_gather_info). 0: per-band
-                                  tables everywhere (bit-identical to the packet kernel) */
+                                  that error per term (mpss_get_gather_info; C2 full frame vs the
+                                  oracle: 4.3e-6 relative). 0: per-band tables everywhere
+                                  (bit-identical to the packet kernel) */
 } mpss_config;
 
 enum { MPSS_SAMPLER_HASH = 0, MPSS_SAMPLER_REFERENCE = 1 };
