@@ -347,9 +347,10 @@ def main(a):
             roofline["l2_hit_rate"] = l2["hit_rate"]
         if "valu" in pt:  # the other resource the gather can run out of
             roofline["valu_issue_frac"] = round(pt["valu"]["issue_frac"], 4)
-            if roofline["traffic"] is not None:
-                roofline["hbm_gbs"] = round(roofline["traffic"] / (shade_launch_ms * 1e-3) / 1e9, 1)
-                roofline["hbm_frac"] = round(roofline["hbm_gbs"] / HBM_PEAK_GBS, 4)
+        if roofline["traffic"] is not None:
+            roofline["hbm_gbs"] = round(roofline["traffic"] / (shade_launch_ms * 1e-3) / 1e9, 1)
+            roofline["hbm_frac"] = round(roofline["hbm_gbs"] / HBM_PEAK_GBS, 4)
+        headline_bound(roofline, pt, shade_launch_ms)
 
     secondary = None
     if world > 1 and a.config == "c2" and not a.no_secondary:
@@ -427,6 +428,24 @@ def c3_strong_secondary(a, rank, world, local):
     return {"c3_strong": {"value": round(sc.xres * sc.yres * sc.spp * steps / dt / 1e6, 3),
                           "unit": "Msamples/s", "ms_per_step": round(dt / steps * 1e3, 3), "frames_per_step": 1,
                           "tiles": len(tiles), "deal_balance": round(balance, 4), "scaling": "strong"}}
+
+
+def headline_bound(roofline, pt, launch_ms):
+    """The headline names the resource that binds the gather: the L2 request rate of its lookups
+    (rounds 2-3), or VALU issue once the common grid cut the lookups (round 4: 0.92 of issue vs 0.74
+    of the request ceiling). The other figure stays beside it."""
+    v = pt.get("valu") if pt else None
+    if not v or roofline.get("frac") is None or launch_ms <= 0 or v["issue_frac"] <= roofline["frac"]:
+        return
+    roofline["l2_requests"] = {"achieved": roofline["achieved"], "peak": roofline["peak"], "unit": "Greq/s",
+                               "frac": roofline["frac"], "peak_source": roofline.get("peak_source")}
+    roofline["bound"] = "valu_issue"
+    roofline["achieved"] = round(v["insts_per_launch"] / (launch_ms * 1e-3) / 1e9, 1)
+    roofline["peak"] = round(1024 * 2.4 / 4, 1)
+    roofline["unit"] = "G wave64 VALU instructions/s"
+    roofline["frac"] = round(v["issue_frac"], 4)
+    roofline["peak_source"] = ("MI355X: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at "
+                               "2.4 GHz; SQ_INSTS_VALU per launch from the committed PMC summary")
 
 
 def pmc_traffic(path, launch_ms, config):
