@@ -379,7 +379,8 @@ int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, 
                         float *hh);
 /* The common grid the sharded gather builds for a profile (mpss_config.mo_common_grid), on the host:
  * table [30][L], rcp [30]; snake as mpss_config.mo_band_dealing (0, 1), or 2: an rgbprofile table
- * (rows 0..2 = R, G, B, read in slots 0..2 of every group). Outputs (each nullable): rows
+ * (rows 0..2 = R, G, B, read in slots 0..2 of every group); near_field as mpss_config.mo_near_field
+ * (5088 or 10236: the LDS split the grid is built for). Outputs (each nullable): rows
  * [n_rows][8] (the groups' pair rows: group g's row for u is row0[g] + u - ubase[g], holding
  * R_0(u), R_0(u+1), ..., R_3(u), R_3(u+1)); *n_rows (call with rows NULL to size it); bands [8][4]
  * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim /
@@ -387,9 +388,9 @@ int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, 
  * other u the bands' own tables; u1start = u0lim unless the rows begin past the end of bands the grid
  * cannot follow); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over the
  * knots each band reads from the rows); *ok = 1 when some group has rows. */
-int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
-                          int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
-                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok);
+int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, int near_field, float *rows,
+                          uint32_t *n_rows, int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start,
+                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, int *ok);
 /* Octree build + pre-order export (sizes first with NULL outputs). */
 int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
                             uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,

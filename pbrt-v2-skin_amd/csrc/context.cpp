@@ -168,12 +168,13 @@ void Context::activate() const { MPSS_HIP(hipSetDevice(cfg_.device)); }
 void Context::gather_info(uint32_t id, int *common_grid, float *rel_err, float *l1_err) const {
     const Material &m = material(id);  // (takes mu_; materials are never replaced)
     const bool band = !m.dipole;  // (rgbprofile: the grid of its R, G, B profiles, rel/l1_err[0..2])
+    const int lay = cfg_.mo_near_field == 10236 ? 0 : 1;  // the grid of the configured LDS layout
     const bool on = band && cfg_.exact_mo == 0 && cfg_.mo_common_grid != 0 &&
-                    (cfg_.mo_near_field == 10236 ? m.dev_profile.cg.on : m.dev_profile.cg_half.on);
+                    (lay == 0 ? m.dev_profile.cg.on : m.dev_profile.cg_half.on);
     *common_grid = on ? 1 : 0;
     for (int c = 0; c < NB; ++c) {
-        if (rel_err) rel_err[c] = band ? m.dev_profile.cg_rel_err[c] : 0.f;
-        if (l1_err) l1_err[c] = band ? m.dev_profile.cg_l1_err[c] : 0.f;
+        if (rel_err) rel_err[c] = band ? m.dev_profile.cg_rel_err[lay][c] : 0.f;
+        if (l1_err) l1_err[c] = band ? m.dev_profile.cg_l1_err[lay][c] : 0.f;
     }
 }
 

@@ -135,6 +135,7 @@ public:
     void render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, float *const *outs, hipStream_t stream);
     // the replay sampler's table (mpss_replay_samples); out may be null to query sizes
     void replay_samples(int spp, float *out, uint64_t *n_floats, int *k);
+    void check_replay_lds(int spp, const char *who) const;  // replay_check_lds over the scene's lights
     // SubsurfaceOctreeNode::Mo over q device-resident points with material `mid`'s profile
     // (mpss_mo_batch); stream-ordered, safe for concurrent callers on their own streams
     void mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, int32_t *counters_dev, hipStream_t stream);

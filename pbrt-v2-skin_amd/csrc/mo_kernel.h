@@ -55,13 +55,15 @@ struct DeviceProfile {
     int L = 0;
     float host_rcp[NB];
     BandGroups groups{};   // band -> XCD group assignment for this profile
-    // The common grid of each band group (mo_band.h CommonGrid), built by upload() for the 10236-entry
-    // LDS layout: ctab holds the groups' pair rows (two float4 per row); cg.on = 1 when some group has
-    // an accurate row range.
+    // The common grid of each band group (mo_band.h CommonGrid), built by upload() for each LDS layout
+    // (the 10236-entry near field: cg; the 5088-entry one, the default: cg_half): ctab / ctab_half hold
+    // the groups' pair rows (two float4 per row); on = 1 when some group has an accurate row range.
     DevBuf<float4> ctab, ctab_half;
     CommonGrid cg{}, cg_half{};  // for the 10236 and 5088 LDS layouts
-    float cg_rel_err[NB] = {};  // per band: max |R - T| / |T| over its knots read from the group rows
-    float cg_l1_err[NB] = {};   // per band: sum of |R - T| over those knots / sum of |T| over the table
+    // per band and layout: max |R - T| / |T| over its knots read from the group rows, and the sum of
+    // |R - T| over those knots / the sum of |T| over the table ([0]: 10236 layout, [1]: 5088)
+    float cg_rel_err[2][NB] = {};
+    float cg_l1_err[2][NB] = {};
     // snake: deal the bands to groups in snake rounds instead of runs of adjacent reach (mo_band.h)
     void upload(const float *table, int L, const float *rcp, bool snake = false);
     // (upload calls it with groups, set_rgb with rows 0..2 in every group; host table [NB][L])
@@ -97,7 +99,7 @@ struct GatherOpts {
     int near_field = 10236;
     bool steal = true;
     bool count_noprune = false;
-    bool common_grid = true;  // mpss_config.mo_common_grid (needs near_field 10236 and DeviceProfile::cg.on)
+    bool common_grid = true;  // mpss_config.mo_common_grid (the layout's grid: cg for 10236, cg_half for 5088)
 };
 
 // queries/out/counters are device pointers. out[q * out_stride + c], c < 30.

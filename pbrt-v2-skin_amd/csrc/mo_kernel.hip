@@ -734,14 +734,13 @@ void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int 
     ctab.release();
     ctab_half.release();
     std::vector<float4> h;
-    float rel[NB], l1[NB];
-    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, rel, l1, 5088, lds_reserve)) {
+    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, cg_rel_err[1], cg_l1_err[1], 5088, lds_reserve)) {
         ctab_half.upload(h.data(), h.size());
         cg_half.tab = ctab_half.ptr;
     } else {
         cg_half.on = 0;
     }
-    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err, cg_l1_err, 10236, lds_reserve)) {
+    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err[0], cg_l1_err[0], 10236, lds_reserve)) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }

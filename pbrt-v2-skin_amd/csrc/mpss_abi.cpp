@@ -181,13 +181,14 @@ int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len,
     });
 }
 
-int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, float *rows, uint32_t *n_rows,
-                          int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start, uint32_t *row0,
-                          uint32_t *ubase, float *rel_err, float *l1_err, int *ok) {
+int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, int near_field, float *rows,
+                          uint32_t *n_rows, int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start,
+                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, int *ok) {
     return guarded([&] {
         require(table && rcp && ok, "mpss_host_common_grid: null argument");
         require(L >= 2 && L < (1u << 24), "mpss_host_common_grid: L out of range");
         require(snake >= 0 && snake <= 2, "mpss_host_common_grid: snake must be 0, 1 or 2");
+        require(near_field == 10236 || near_field == 5088, "mpss_host_common_grid: near_field must be 10236 or 5088");
         BandGroups g = make_band_groups(rcp, snake == 1);
         if (snake == 2)  // rgbprofile: rows 0..2 (R, G, B) in every group (DeviceProfile::set_rgb)
             for (int k = 0; k < kGroups; ++k)
@@ -195,7 +196,7 @@ int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int 
         CommonGrid cg;
         std::vector<float4> h;
         float rel[NB], l1[NB];
-        *ok = build_common_grid(table, (int)L, rcp, g, cg, h, rel, l1, 10236, snake == 2 ? 28 : 0) ? 1 : 0;
+        *ok = build_common_grid(table, (int)L, rcp, g, cg, h, rel, l1, near_field, snake == 2 ? 28 : 0) ? 1 : 0;
         if (n_rows) {
             if (rows) require(*n_rows >= h.size() / 2, "mpss_host_common_grid: rows too small");
             *n_rows = (uint32_t)(h.size() / 2);

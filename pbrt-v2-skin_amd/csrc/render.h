@@ -104,6 +104,9 @@ struct ReplayWindow {
 };
 // Launches the generation on `stream` (the host picks the task ranges: replay_window_tasks).
 void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStream_t stream);
+// Throws (naming `who` and the LDS a generator wave would need) when spp pixel samples with lights of
+// these sample counts do not fit the generator's LDS (kReplayMaxLds).
+void replay_check_lds(int spp, const int *light_samples, int nlights, const char *who);
 // The task grid and the task columns / rows meeting [x0, x1) x [y0, y1) of the (xres + 1) x
 // (yres + 1) sample extent.
 void replay_window_tasks(int xres, int yres, int ntasks, int x0, int x1, int y0, int y1, ReplayWindow &w);

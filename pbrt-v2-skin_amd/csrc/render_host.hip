@@ -604,6 +604,12 @@ void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp,
     launch_replay_window(sc, w, stream);
 }
 
+void Context::check_replay_lds(int spp, const char *who) const {
+    std::vector<int> ns;
+    for (const SceneLight &l : scene_.lights) ns.push_back(l.nsamples);
+    replay_check_lds(spp, ns.data(), (int)ns.size(), who);
+}
+
 void Context::replay_samples(int spp, float *out, uint64_t *n_floats, int *k) {
     activate();
     std::unique_lock<std::mutex> lk(mu_);
@@ -613,6 +619,7 @@ void Context::replay_samples(int spp, float *out, uint64_t *n_floats, int *k) {
     if (W <= 0) throw Error(MPSS_ERR_INVALID, "replay_samples: no camera");
     spp = round_up_pow2(spp);
     if (spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay_samples: spp too large for the replay sampler");
+    check_replay_lds(spp, "replay_samples");
     const int K = replay_k_;
     *k = K;
     const int64_t npix = (int64_t)(W + 1) * (H + 1);
@@ -648,6 +655,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
         spp = round_up_pow2(spp);  // LDSampler rounds pixelsamples up (lowdiscrepancy.cpp:45-49)
         if (spp > kReplayMaxSpp)
             throw Error(MPSS_ERR_INVALID, "render_tile: spp must be at most 4096 for the replay sampler");
+        check_replay_lds(spp, "render_tile");
     }
     for (int i = 0; i < n; ++i) {
         const int32_t *r = rects + 4 * i;

@@ -39,8 +39,11 @@ namespace mpss {
 // the volume integrator's arrays are drawn (the stream must advance) but not consumed here.
 constexpr int kReplayImage = 2, kReplayPerLightSample = 5;
 constexpr int kReplayLiDraws = 6;
-// the largest (power-of-two) spp the replay generator takes: one pixel's index arrays live in LDS
+// the largest (power-of-two) spp the replay generator takes: one pixel's index arrays live in LDS,
+// so the binding limit is kReplayMaxLds per generator wave (replay_check_lds: 1,024 spp fit with one
+// light of 4 samples -- 94 KB -- and 2,048 do not; more or larger light-sample arrays fit fewer)
 constexpr int kReplayMaxSpp = 4096;
+constexpr size_t kReplayMaxLds = 160 * 1024;
 // the largest window table of one render batch (floats: 8 GiB of the 288 GB); render_tiles closes a
 // batch before it. (Larger windows replay more tasks at once: one wave per task is the unit.)
 constexpr int64_t kReplayWindowFloats = (int64_t)1 << 31;

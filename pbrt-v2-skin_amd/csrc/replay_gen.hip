@@ -241,12 +241,15 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             shuffle_partners(A.d + A.hdr + spp * A.n, A.idx, spp);
         }
         wave_sync();
-        // the block shuffles, all at once: the image's swaps on lane 0, array a's on lane a + 1
+        // the block shuffles side by side: the image's swaps on lane 0, array a's on lane 1 + a % 63
+        // (lanes 1..63 take arrays a, a + 63, ... in turn: any light count)
         if (lane == 0) {
             shuffle_swaps(dimg, idx0, spp);
-        } else if (lane <= na) {
-            const ReplayArray A = array(lane - 1);
-            shuffle_swaps(A.d + A.hdr + spp * A.n, A.idx, spp);
+        } else {
+            for (int a = lane - 1; a < na; a += 63) {
+                const ReplayArray A = array(a);
+                shuffle_swaps(A.d + A.hdr + spp * A.n, A.idx, spp);
+            }
         }
         wave_sync();
         // the image samples and the camera rays (samplerrenderer.cpp:97-103): only whether they hit
@@ -330,19 +333,42 @@ void replay_window_tasks(int xres, int yres, int ntasks, int x0, int x1, int y0,
     w.h = y1 - y0;
 }
 
+// One generator wave's LDS words (replay_window_kernel): MT state, image draws and idx, the arrays'
+// draws, idx and sig.
+static size_t replay_wave_words(int spp, int nlights, int nmax, int arr_draws) {
+    const size_t na = 3 * (size_t)nlights;
+    return 624 + (size_t)std::max(spp, 2) + spp + arr_draws + na * spp + (na * spp * nmax + 3) / 4;
+}
+
+void replay_check_lds(int spp, const int *light_samples, int nlights, const char *who) {
+    int nmax = 1, arr_draws = 0;
+    for (int l = 0; l < nlights; ++l) {
+        const int n = replay_round_up_pow2(light_samples[l]);
+        if (n < 1 || n > 256) throw Error(MPSS_ERR_INVALID, std::string(who) + ": the reference sampler takes light "
+                                                           "sample counts (rounded up to a power of 2) in [1, 256]");
+        nmax = std::max(nmax, n);
+        arr_draws += 3 * (spp * n + spp) + 5;
+    }
+    const size_t bytes = sizeof(uint32_t) * replay_wave_words(spp, nlights, nmax, arr_draws);
+    if (bytes > kReplayMaxLds)
+        throw Error(MPSS_ERR_INVALID,
+                    std::string(who) + ": the reference sampler replays a pbrt task's stream in one wave whose LDS holds "
+                    "a pixel's draws, index arrays and shuffles: " + std::to_string(spp) + " spp with these lights' sample "
+                    "counts needs " + std::to_string(bytes / 1024) + " KB, more than the 160 KB of LDS (fewer pixel "
+                    "samples or light samples fit)");
+}
+
 void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStream_t stream) {
     const int nw = w.nxr * w.nyr;
     if (nw <= 0) return;
     if (w.nmax < 1 || w.nmax > 256) throw Error(MPSS_ERR_INVALID, "replay: light sample counts must be in [1, 256]");
     if (w.spp < 1 || w.spp > kReplayMaxSpp) throw Error(MPSS_ERR_INVALID, "replay: spp out of range");
-    // state, image draws and idx, the arrays' draws, idx and sig (replay_window_kernel)
-    const int na = 3 * w.nlights;
-    const int words = 624 + std::max(w.spp, 2) + w.spp + w.arr_draws + na * w.spp + (na * w.spp * w.nmax + 3) / 4;
+    const int words = (int)replay_wave_words(w.spp, w.nlights, w.nmax, w.arr_draws);
     auto lds_of = [&](int nwv) { return sizeof(uint32_t) * (size_t)nwv * words; };
     int nwv = kMaxWaves;
     while (nwv > 1 && lds_of(nwv) > 64 * 1024) --nwv;  // two workgroups per CU where it fits
     const size_t lds = lds_of(nwv);
-    if (lds > 160 * 1024)
+    if (lds > kReplayMaxLds)
         throw Error(MPSS_ERR_INVALID, "replay: spp x light samples too large for the replay generator's LDS");
     if (lds > 64 * 1024)
         MPSS_HIP(hipFuncSetAttribute((const void *)replay_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

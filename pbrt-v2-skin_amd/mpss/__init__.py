@@ -138,7 +138,7 @@ _sig("mpss_host_imagemap_lookup", C.c_int, [C.POINTER(Imagemap), u32, f32p, f32p
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
-_sig("mpss_host_common_grid", C.c_int, [f32p, u32, f32p, C.c_int, vp, u32p] + [vp] * 9 + [C.POINTER(C.c_int)])
+_sig("mpss_host_common_grid", C.c_int, [f32p, u32, f32p, C.c_int, C.c_int, vp, u32p] + [vp] * 9 + [C.POINTER(C.c_int)])
 _sig("mpss_host_octree_export", C.c_int, [u32, f32p, f32p, f32p, f32p, u32p] + [vp] * 8)
 
 
@@ -308,10 +308,11 @@ def host_rho_table(roughness, eta, n=1025, sqrt_samples=256, double_ref_sslf=Fal
     return hd, hh.value
 
 
-def host_common_grid(table, rcp, snake=False, rgb=False):
+def host_common_grid(table, rcp, snake=False, rgb=False, near_field=5088):
     """The sharded gather's common grid for a profile (mpss_host_common_grid): dict of rows
     (n_rows, 8), bands (8, 4), rg, u0lim, u1lim, u1start, row0, ubase (8,), rel_err / l1_err (30,),
-    ok. rgb: an rgbprofile table (rows 0..2 in every group)."""
+    ok. rgb: an rgbprofile table (rows 0..2 in every group). near_field: the LDS layout the grid is
+    built for (mpss_config.mo_near_field; 5088 is the default)."""
     table = np.ascontiguousarray(table, np.float32)
     rcp = np.ascontiguousarray(rcp, np.float32)
     L = table.shape[1]
@@ -319,12 +320,12 @@ def host_common_grid(table, rcp, snake=False, rgb=False):
     n = C.c_uint32(0)
     nul = [None] * 9
     ok = C.c_int()
-    check(_lib.mpss_host_common_grid(table, L, rcp, mode, None, C.byref(n), *nul, C.byref(ok)))
+    check(_lib.mpss_host_common_grid(table, L, rcp, mode, int(near_field), None, C.byref(n), *nul, C.byref(ok)))
     out = dict(rows=np.zeros((n.value, 8), np.float32), bands=np.zeros((8, 4), np.int32),
                rg=np.zeros(8, np.float32), u0lim=np.zeros(8, np.float32), u1lim=np.zeros(8, np.float32),
                u1start=np.zeros(8, np.float32), row0=np.zeros(8, np.uint32), ubase=np.zeros(8, np.uint32),
                rel_err=np.zeros(NB, np.float32), l1_err=np.zeros(NB, np.float32))
-    check(_lib.mpss_host_common_grid(table, L, rcp, mode, out["rows"].ctypes.data, C.byref(n),
+    check(_lib.mpss_host_common_grid(table, L, rcp, mode, int(near_field), out["rows"].ctypes.data, C.byref(n),
                                      *[out[k].ctypes.data for k in ("bands", "rg", "u0lim", "u1lim", "u1start", "row0",
                                                                     "ubase", "rel_err", "l1_err")], C.byref(ok)))
     out["ok"] = bool(ok.value)

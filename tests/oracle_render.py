@@ -105,6 +105,34 @@ def tables_from_ctx(ctx, n):
     return [ctx.material_tables(i)[:3] for i in range(n)]
 
 
+def tables_from_oracle(sc):
+    """Material tables built by the oracle itself (oracle/skin.c + mpc.c + kissfft.c, oracle/rho.c):
+    LayeredSkin's layers (layeredskin.cpp:47-89), ComputeMultipoleProfile at the material's
+    desiredlength with lerponthinslab (multipole.cpp:241-295), rgbprofile's three RGB profiles
+    (multipole.cpp:408-451: rows c % 3), and ComputeRhoDataFromBxDF (multipole.cpp:521-549). With
+    these and the oracle's own irradiance, an image comparison shares nothing with the product but
+    the scene description."""
+    import oracle_lib
+    out = []
+    for m in sc.materials:
+        th = tuple(m.get("layer_thickness_nm", (0.25e6, 20e6)))
+        ior = tuple(m.get("layer_ior", (1.4, 1.4)))
+        rough = m.get("roughness", 0.3)
+        mua, musp, thk, eta = oracle_lib.skin_layers(rough, m.get("nmperunit", 40e6), m.get("f_mel", 0.5),
+                                                     m.get("f_eu", 0.5), m.get("f_blood", 0.5), m.get("f_ohg", 0.5),
+                                                     th, ior)
+        if m.get("rgb_profile"):
+            ra = np.stack([oracle_lib.to_rgb(x) for x in mua])
+            rs = np.stack([oracle_lib.to_rgb(x) for x in musp])
+            idx = np.arange(NB) % 3
+            mua, musp = ra[:, idx].astype(np.float32), rs[:, idx].astype(np.float32)
+        tab, rcp, _, _ = oracle_lib.compute_profile(mua, musp, eta, thk, desired_length=int(m.get("desired_length", 512)),
+                                                    lerp=bool(m.get("lerp_on_thin_slab", 1)))
+        rho, _ = oracle_lib.rho_table(rough, ior[0], fixed=bool(m.get("double_ref_sslf", 0)))
+        out.append((tab, rcp, rho))
+    return out
+
+
 def tables_from_host(sc, mpss):
     """Material tables from the product's host builders (CPU only; no device needed)."""
     out = []

@@ -12,7 +12,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.npz")
-LDS_FLOATS = 4 * (10236 + 3)
+NEAR_FIELDS = (5088, 10236)  # mpss_config.mo_near_field: the default layout and the one-workgroup one
 ABS_TOL = 1e-13  # mo_kernel.h kCgAbsTol
 
 
@@ -36,9 +36,10 @@ def _R(T, r, u, L):
     return np.where((f - r > L - 1) | (u >= L), 0.0, v)
 
 
-def _check_layout(tab, rcp, cg, tol=2e-6, groups=None):
+def _check_layout(tab, rcp, cg, tol=2e-6, groups=None, near_field=5088):
     """Groups, the LDS split, the pair rows against numpy, and that every band knot the rows serve
     is within tol of the band's own value (unfloored)."""
+    lds_floats = 4 * (near_field + 3)
     L = tab.shape[1]
     T64 = tab.astype(np.float64)
     for g, bands in enumerate(groups or _groups(rcp)):
@@ -49,7 +50,7 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None):
         r = np.array([np.float64(rcp[c]) / np.float64(rg) if c >= 0 else 0.0 for c in slots])
         # every lane with u < u0lim has s_j < klim_j for every band: the split fits the LDS
         need = sum(int(np.ceil(cg["u0lim"][g] * rj)) + 2 for rj in r if rj > 0)
-        assert 0 < need <= LDS_FLOATS
+        assert 0 < need <= lds_floats
         u0, u1, ub, r0 = cg["u0lim"][g], cg["u1lim"][g], int(cg["ubase"][g]), int(cg["row0"][g])
         if u1 <= u0:
             continue
@@ -82,34 +83,38 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None):
             assert np.all(err <= bound * (1 + 1e-9)), (g, c, (err / bound).max())
 
 
-def test_common_grid_of_golden_profile(mpss):
+@pytest.mark.parametrize("near_field", NEAR_FIELDS)
+def test_common_grid_of_golden_profile(mpss, near_field):
     """desiredlength 64 skin profile (tests/golden): layout and pair rows vs numpy, the served range
     within the bound."""
     z = np.load(GOLDEN)
     tab, rcp = z["profile_64"], z["profile_64_rcp"]
-    cg = mpss.host_common_grid(tab, rcp)
-    _check_layout(tab, rcp, cg)
+    cg = mpss.host_common_grid(tab, rcp, near_field=near_field)
+    _check_layout(tab, rcp, cg, near_field=near_field)
     assert cg["rel_err"].max() <= 2e-6
 
 
-def test_common_grid_of_the_benched_skin_profile(mpss):
-    """C2's material (skin.pbrt, desiredlength 512): rows for 7 of the 8 groups, over more than one
-    doubling of distance past the near field for each."""
+@pytest.mark.parametrize("near_field", NEAR_FIELDS)
+def test_common_grid_of_the_benched_skin_profile(mpss, near_field):
+    """C2's material (skin.pbrt, desiredlength 512), for both LDS layouts (5088: the default the
+    render path uses): rows for 7 of the 8 groups, over more than one doubling of distance past the
+    near field for each, every served knot within the bound."""
     from mpss import pbrtscene
     sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"))
     m = sc.materials[0]
     kw = {k: v for k, v in m.items() if k not in ("Kr", "Kt", "albedo", "albedo_tex", "bump_tex")}
     tab, rcp, _ = mpss.host_build_profile(*mpss.host_skin_layers(mpss.default_skin(**kw)), 512)
-    cg = mpss.host_common_grid(tab, rcp)
+    cg = mpss.host_common_grid(tab, rcp, near_field=near_field)
     assert cg["ok"]
     span = np.log2(np.maximum(cg["u1lim"], 1) / cg["u0lim"])
     assert (span > 1.0).sum() >= 7, span
     assert cg["rel_err"].max() <= 2e-6 and cg["l1_err"].max() <= 1e-8
     assert len(cg["rows"]) <= 8 * 65536
-    _check_layout(tab, rcp, cg)
+    _check_layout(tab, rcp, cg, near_field=near_field)
 
 
-def test_common_grid_of_the_rgb_profile(mpss):
+@pytest.mark.parametrize("near_field", NEAR_FIELDS)
+def test_common_grid_of_the_rgb_profile(mpss, near_field):
     """rgbprofile at C2's length (desiredlength 512): the R, G, B profiles in slots 0..2 of every
     group, grid = G's (the longest reach). B reaches ~15x less far in d^2, its knots that much denser
     than the grid; past the near field its values are under 5e-5 of its peak, where the bound is
@@ -119,18 +124,20 @@ def test_common_grid_of_the_rgb_profile(mpss):
     mua, musp, th, eta = oracle_lib.skin_layers(0.3, 40e6, 0.5, 0.5, 0.5, 0.5, (0.25e6, 20e6), (1.4, 1.4))
     ra, rs = rgb_layers(mua, musp)
     tab, rcp, _, _ = oracle_lib.compute_profile(ra, rs, eta, th, desired_length=512)
-    cg = mpss.host_common_grid(tab, rcp, rgb=True)
+    cg = mpss.host_common_grid(tab, rcp, rgb=True, near_field=near_field)
     assert cg["ok"]
     assert np.all(cg["bands"] == np.array([0, 1, 2, -1]))
     assert np.all(cg["rg"] == np.float32(rcp[:3].min()))
-    # B is off near the field's end (its values there still above the floor): the rows start a little
-    # past it (u1start 4185 vs u0lim 2364) and serve all three to ~70 k of G's 120 k steps
-    assert np.all(cg["u1start"] >= cg["u0lim"]) and np.all(cg["u1start"] < 2 * cg["u0lim"])
+    # B is off near the field's end (its values there still above the floor): the rows start past it
+    # (10236 layout: u1start 4185 vs u0lim 2364) and serve all three to ~70 k of G's 120 k steps
+    assert np.all(cg["u1start"] >= cg["u0lim"])
+    if near_field == 10236:
+        assert np.all(cg["u1start"] < 2 * cg["u0lim"])
     assert np.all(cg["u1lim"] - cg["u1start"] > 60000)
     rows = cg["rows"].reshape(8, -1, 8)
     assert np.all(rows[:, :, 6:] == 0)  # the empty slot
     assert cg["rel_err"][:3].max() <= 2e-6 and cg["l1_err"][:3].max() <= 1e-8
-    _check_layout(tab, rcp, cg, groups=[[0, 1, 2]] * 8)
+    _check_layout(tab, rcp, cg, groups=[[0, 1, 2]] * 8, near_field=near_field)
 
 
 def test_common_grid_of_a_rough_table(mpss):

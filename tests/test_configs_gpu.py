@@ -2,17 +2,18 @@
 
   C2  scenes/skin.pbrt exactly as bench.py runs it (1024x1024, 64 spp, minsampledistance 0.0015,
       desiredlength 512, the production sharded Mo() gather): surface points bit-exact, the GPU
-      profile and rho tables vs the oracle, irradiance on a 300k-point prefix (the sampler's
-      random numbers depend only on the point's index, so a prefix is a valid subset), and two
+      profile and rho tables vs the oracle, irradiance of ALL 2.2 M points vs the oracle's, and two
       windows rendered by both: a 32x32 window on the cheek and a ragged 37x29 window across
       the silhouette, with the image tolerance of test_render_parity_gpu.py; and the WHOLE benched
-      frame (1024x1024 x 64 spp, every pixel) against the oracle on the host's CPUs.
+      frame (1024x1024 x 64 spp, every pixel) against the oracle on the host's CPUs. The oracle side
+      is end to end its own: its profile and rho tables (tables_from_oracle), its irradiance and
+      its octree built from that irradiance.
   C3  2048x2048 at 256 spp: a cheek window and a silhouette window at the config's own 256 spp vs
       the oracle; dealt over 8 ranks by cost (bench.py's multi-GPU deal), every rank's tile set
       rendered on this GPU and reassembled is bitwise the single-call frame.
   C4  scenes/mcprofile.pbrt's layers at 1e7 photons vs the oracle's random walk.
   C5  the 4.06 M-triangle subdivided head with the original tessellation as pointsfile: surface
-      irradiance on a prefix and a 32x32 cheek window at the config's own 512 spp against the oracle
+      irradiance of every point and a 32x32 cheek window at the config's own 512 spp against the oracle
       (at 512 spp a wave's 64 lanes are one pixel's samples: the gather's lane-coherent regime).
 """
 import os
@@ -64,7 +65,10 @@ def c2(mpss, oracle):
     assert float(sc.integrator["minsampledistance"]) == pytest.approx(0.0015)
     ctx = pbrtscene.build_context(sc)  # desiredlength 512 (CreateLayeredSkinMaterial's default)
     ctx.preprocess(seed=1)
-    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    # the oracle's own tables, irradiance and octree: nothing of the product's feeds its images
+    o = orr.OracleScene(sc, orr.tables_from_oracle(sc), ctx.cfg, mpss)
+    o.E = o.irradiance(ctx.surface_points(), 1, nthreads=NT)
+    o.set_octree(ctx.surface_points(), o.E)
     return torch, sc, ctx, o
 
 
@@ -91,21 +95,18 @@ def test_c2_surface_points_and_irradiance(c2):
     pts = ctx.surface_points()
     assert len(pts) > 2_000_000
     assert pts.tobytes() == o.tessellate().tobytes()
-    n = 300_000
-    E = o.irradiance(pts[:n], 1, nthreads=NT)
-    got = ctx.irradiance()[:n]
+    E = o.E  # every point (the fixture's oracle irradiance, from which the oracle's octree is built)
+    got = ctx.irradiance()
+    assert got.shape == E.shape == (len(pts), 30)
     np.testing.assert_allclose(got, E, rtol=1e-5, atol=1e-6 * float(E.max()))
     assert (got == E).mean() >= 0.99
 
 
 @pytest.mark.parametrize("where", ["cheek", "silhouette"])
 def test_c2_window_parity(c2, where):
-    """A window of the benched frame through the production gather (exact_mo = 0) vs the oracle.
-    The oracle's octree is built from the GPU's irradiance (checked on its own above)."""
+    """A window of the benched frame through the production gather (exact_mo = 0) vs the oracle
+    (its own tables, irradiance and octree)."""
     torch, sc, ctx, o = c2
-    if not getattr(o, "_octree_set", False):
-        o.set_octree(ctx.surface_points(), ctx.irradiance())
-        o._octree_set = True
     if where == "cheek":
         x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
     else:
@@ -119,11 +120,10 @@ def test_c2_window_parity(c2, where):
 def test_c2_full_frame_parity(c2):
     """Every pixel of the benched C2 frame (skin.pbrt 1024x1024, 64 spp, hash sampler, production
     sharded gather) vs the oracle's render of the same frame (multipolesubsurface.cpp:253-304 driven
-    by samplerrenderer.cpp:60-167's pixel loop), with tests/parity.py's unfloored 1e-4 relative L-inf."""
+    by samplerrenderer.cpp:60-167's pixel loop), with tests/parity.py's unfloored 1e-4 relative L-inf.
+    The oracle renders from its own profile / rho tables, its own irradiance of all 2.2 M points
+    and its own octree: the comparison is end to end."""
     torch, sc, ctx, o = c2
-    if not getattr(o, "_octree_set", False):
-        o.set_octree(ctx.surface_points(), ctx.irradiance())
-        o._octree_set = True
     got = _render(torch, ctx, sc.spp, 7, 0, sc.xres, 0, sc.yres)
     ref = o.render_tile(sc.spp, 7, 0, sc.xres, 0, sc.yres, nthreads=NT)
     st = parity.check_image(got, ref)
@@ -138,8 +138,11 @@ def c3(mpss):
     sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=2048, yres=2048, spp=256)
     ctx = pbrtscene.build_context(sc)
     ctx.preprocess(seed=1)
-    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
-    o.set_octree(ctx.surface_points(), ctx.irradiance())
+    o = orr.OracleScene(sc, orr.tables_from_oracle(sc), ctx.cfg, mpss)
+    pts = ctx.surface_points()
+    E = o.irradiance(pts, 1, nthreads=NT)
+    np.testing.assert_allclose(ctx.irradiance(), E, rtol=1e-5, atol=1e-6 * float(E.max()))
+    o.set_octree(pts, E)
     yield torch, sc, ctx, o
     ctx.close()
 
@@ -222,8 +225,9 @@ def test_c4_mcprofile_1e7_photons(mpss):
 
 def test_c5_dense_mesh_window(mpss):
     """C5's geometry (head.pbrt subdivided four times: 4.06 M triangles) with the original mesh's
-    2.2 M tessellated points as the pointsfile, at 4096x4096 and the config's 512 spp: irradiance on
-    a prefix and a 32x32 cheek window against the oracle (its own BVH over the same 4.06 M triangles)."""
+    2.2 M tessellated points as the pointsfile, at 4096x4096 and the config's 512 spp: irradiance of
+    every point and a 32x32 cheek window against the oracle (its own BVH over the same 4.06 M
+    triangles, its own tables, irradiance and octree)."""
     import torch
     from mpss import pbrtscene
     sc = pbrtscene.load(os.path.join(ROOT, "scenes", "skin.pbrt"), xres=4096, yres=4096, spp=512)
@@ -233,12 +237,12 @@ def test_c5_dense_mesh_window(mpss):
     ctx = pbrtscene.build_context(sc)
     ctx.set_surface_points(pts)
     ctx.preprocess(seed=3)
-    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
-    n = 100_000
-    E = o.irradiance(pts[:n], 3, nthreads=NT)
-    got = ctx.irradiance()[:n]
+    o = orr.OracleScene(sc, orr.tables_from_oracle(sc), ctx.cfg, mpss)
+    E = o.irradiance(pts, 3, nthreads=NT)  # every point, over the oracle's own 4.06 M-triangle BVH
+    got = ctx.irradiance()
     np.testing.assert_allclose(got, E, rtol=1e-5, atol=1e-6 * float(E.max()))
-    o.set_octree(pts, ctx.irradiance())
+    assert (got == E).mean() >= 0.99
+    o.set_octree(pts, E)
     x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
     _check(_render(torch, ctx, sc.spp, 5, x0, x1, y0, y1), o.render_tile(sc.spp, 5, x0, x1, y0, y1, nthreads=NT))
     ctx.close()

@@ -30,6 +30,14 @@ def _scene(name, lights=None, W=40, H=32, spp=4):
     if lights == "sky+area":
         from test_render_parity_gpu import _sky_light
         sc.lights = [sc.lights[0], _sky_light(40, [1, 1, 0], ns=2)]
+    elif lights == "24 spheres":
+        # 3 x 24 = 72 light-sample arrays per pixel: more than one wave's 63 shuffle lanes
+        # (replay_gen.hip strides the arrays' block shuffles over the lanes)
+        sc.lights = []
+        for k in range(24):
+            a = 2 * np.pi * k / 24
+            sc.lights.append(dict(center=np.array([5 * np.cos(a), -4 + 2 * np.sin(a), 3 + 0.1 * k], np.float32),
+                                  radius=0.1, L=[40.0 + k, 40.0, 40.0 - k], nsamples=1 + k % 3))
     return sc
 
 
@@ -65,7 +73,7 @@ def _render(torch, ctx, sc, rects):
 
 
 @pytest.mark.parametrize("name,lights,cores", [("skin.pbrt", None, 8), ("skin.pbrt", "sky+area", 8),
-                                               ("tissue.pbrt", None, 2)])
+                                               ("tissue.pbrt", None, 2), ("skin.pbrt", "24 spheres", 8)])
 def test_replay_table_bit_exact(mpss, oracle, name, lights, cores):
     sc = _scene(name, lights)
     torch, ctx, o = _pair(mpss, sc, cores)
@@ -126,3 +134,20 @@ def test_replay_depends_on_core_count_and_not_on_seed(mpss):
         ctx.close()
     assert np.array_equal(imgs[0], imgs[1])
     assert not np.array_equal(imgs[0], imgs[2])
+
+
+def test_replay_lds_limit_is_named(mpss):
+    """The generator keeps a pixel's draws, index arrays and shuffles of one pbrt task in one wave's
+    LDS: a pixel-sample count past that budget is refused up front, with the constraint named."""
+    import torch
+    from mpss import pbrtscene
+    sc = _scene("skin.pbrt", spp=4096)
+    ctx = pbrtscene.build_context(sc, sampler=mpss.SAMPLER_REFERENCE, replay_cores=8)
+    ctx.preprocess(seed=0)
+    out = torch.zeros((4 * 4 * 4,), dtype=torch.float32, device="cuda")
+    with pytest.raises(mpss.MpssError, match="KB"):
+        ctx.render_tile(4096, 0, 0, 4, 0, 4, out.data_ptr())
+    ctx.render_tile(1024, 0, 0, 4, 0, 4, out.data_ptr())  # 1024 spp x 4 light samples fits
+    torch.cuda.synchronize()
+    assert float(out.cpu()[3]) > 0
+    ctx.close()

@@ -1,0 +1,261 @@
+// valu_issue.hip -- how many wave64 vector instructions per second one MI355X (gfx950) SIMD issues,
+// by instruction and by waves per SIMD: the ceiling the Mo() gather's VALU count is priced against
+// (MI355X_MICROARCH.md gives 2 cycles per v_fma_f32 on a SIMD-32 with several
+// waves and 4 for one wave alone, but nothing for the packed f32 and conversion instructions the
+// gather's record loop is made of).
+//
+// Each variant is one instruction repeated over 8 independent register chains (so no dependency
+// wait), 32 per loop step, in inline asm (the compiler neither folds nor reorders it); "gather mix"
+// is the instruction mix of one common-grid point record of mo_band_wave_kernel<false,5088,true>
+// (counted from its ISA: hipcc -S of mo_wave_cg.hip) with its SALU beside it. Every wave stamps
+// s_memtime at its start and end, so cycles are the shader clock's, not an assumed 2.4 GHz.
+//
+// Launch: 256-thread workgroups (one wave per SIMD each), W workgroups per CU => W waves per SIMD;
+// W = 8 is the gather's occupancy (two 1024-thread workgroups per CU).
+//
+// Printed per (variant, W): wave64 instructions per second over the chip, and SIMD cycles per wave
+// instruction = (s_memtime span of the launch's waves) x 1024 SIMDs / instructions.
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/microbench/valu_issue.hip -o tools/microbench/valu_issue
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__);     \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+enum {
+    V_FMA = 0,  // v_fma_f32
+    V_ADD,      // v_add_f32
+    V_PKMUL,    // v_pk_mul_f32
+    V_PKADD,    // v_pk_add_f32
+    V_PKFMA,    // v_pk_fma_f32
+    V_CVT,      // v_cvt_u32_f32
+    V_FRACT,    // v_fract_f32
+    V_CND,      // v_cndmask_b32 (e64, SGPR-pair mask)
+    V_LSHLADD,  // v_lshl_add_u32
+    V_MIX,      // the gather's point-record mix (VALU only)
+    V_MIXS,     // the same plus its SALU
+    V_COUNT
+};
+static const char *kNames[V_COUNT] = {"v_fma_f32",      "v_add_f32",    "v_pk_mul_f32",   "v_pk_add_f32",
+                                      "v_pk_fma_f32",   "v_cvt_u32_f32", "v_fract_f32",   "v_cndmask_b32",
+                                      "v_lshl_add_u32", "gather mix (VALU)", "gather mix (VALU + SALU)"};
+// wave64 VALU instructions per loop step, and SALU
+static const int kValu[V_COUNT] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 94, 94};  // mix: 2 records x 47
+static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48};
+
+#define R8(X) X X X X X X X X
+#define R4(X) X X X X
+
+// 8 chains a0..a7 (f32 or packed pairs p0..p7), operands x (VGPR), s (SGPR pair)
+template <int V>
+__device__ __forceinline__ void step(float (&a)[8], float x, float y) {
+    if (V == V_FMA) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(x), "v"(y));
+    } else if (V == V_ADD) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_add_f32 %0, %0, %1" : "+v"(a[k]) : "v"(x));
+    } else if (V == V_CVT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(a[k]));
+    } else if (V == V_FRACT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_fract_f32 %0, %0" : "+v"(a[k]));
+    } else if (V == V_LSHLADD) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(a[k]) : "v"(x));
+    } else if (V == V_CND) {
+        uint64_t m;
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(y));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[k]) : "v"(x), "s"(m));
+    }
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+template <int V>
+__device__ __forceinline__ void step_pk(f2v (&p)[8], f2v x) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (V == V_PKMUL) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(p[k]) : "v"(x));
+            if (V == V_PKADD) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(p[k]) : "v"(x));
+            if (V == V_PKFMA) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(p[k]) : "v"(x));
+        }
+}
+
+// One point record of the common-grid gather (mo_band_wave_kernel<false,5088,true>, point-pair loop
+// per point): d2 (3 sub, 3 mul, 2 add as v_subrev/v_pk_add + v_mul/v_pk_mul + v_add), u and f (1 mul, 2
+// pk_mul), 5 cvt, 1 cmp + 1 lshl-add (row offset), 4 lshl-add (LDS addresses), 2 cmp + 2 cndmask + 1 cmp
+// (path), the lerp (4 fract, 4 sub, 4 pk_mul, 4 add), the tau test (1 cmp), products (4 pk_mul, 1
+// pk_add) -- 47 VALU with 24 SALU (exec-mask saves/restores, branches' scalar compares, the pair's
+// address increments). Two records interleaved (independent registers), as the pair loop runs them.
+template <bool SALU>
+__device__ __forceinline__ void step_mix(float (&a)[8], f2v (&p)[8], float x, f2v xv, uint32_t &s0, uint32_t &s1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float &d = a[4 * h], &u = a[4 * h + 1], &t = a[4 * h + 2], &w = a[4 * h + 3];
+        f2v &pa = p[4 * h], &pb = p[4 * h + 1], &pc = p[4 * h + 2], &pd = p[4 * h + 3];
+        uint64_t m;
+        // d2
+        asm volatile("v_subrev_f32 %0, %1, %0" : "+v"(d) : "v"(x));
+        asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(pa) : "v"(xv));
+        asm volatile("v_mul_f32 %0, %0, %0" : "+v"(d));
+        asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(pa));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        // u, f
+        asm volatile("v_mul_f32 %0, %1, %0" : "+v"(u) : "v"(x));
+        asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pb) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pc) : "v"(xv));
+        R4(asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(t));)
+        asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(w));
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_lshl_add_u32 %0, %0, 5, %1" : "+v"(w) : "v"(x));
+        R4(asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(t) : "v"(x));)
+        // path
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_cmp_le_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(w) : "v"(x), "s"(m));
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(w) : "v"(x), "s"(m));
+        asm volatile("v_cmp_lt_i32_e64 %0, 1, %1" : "=s"(m) : "v"(w));
+        // lerp
+        R4(asm volatile("v_fract_f32 %0, %0" : "+v"(u));)
+        R4(asm volatile("v_sub_f32 %0, 1.0, %0" : "+v"(u));)
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pd) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pd) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pb) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pc) : "v"(xv));
+        R4(asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));)
+        asm volatile("v_cmp_ge_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(d));
+        // products
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pa) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pb) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pc) : "v"(xv));
+        asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(pd) : "v"(xv));
+        asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(pa) : "v"(pb));
+        if (SALU) {
+            R4(asm volatile("s_add_u32 %0, %0, 32\n s_addc_u32 %1, %1, 0" : "+s"(s0), "+s"(s1) ::"scc");)
+            R4(asm volatile("s_cmp_ge_i32 %0, %1\n s_cselect_b32 %0, %0, %1" : "+s"(s0) : "s"(s1) : "scc");)
+            R4(asm volatile("s_mov_b32 %0, %1\n s_or_b32 %1, %1, %0" : "+s"(s0), "+s"(s1));)
+        }
+    }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void issue_kernel(int steps, float *out, unsigned long long *span) {
+    const float x = 1.0f + threadIdx.x * 1e-7f, y = 1e-3f;
+    float a[8];
+    f2v p[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        a[k] = 0.5f + k * 0.01f;
+        p[k] = f2v{a[k], a[k] + 1.f};
+    }
+    const f2v xv = f2v{x, y};
+    uint32_t s0 = blockIdx.x, s1 = steps;
+    unsigned long long t0;
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0));
+    for (int i = 0; i < steps; ++i) {
+        if (V == V_PKMUL || V == V_PKADD || V == V_PKFMA)
+            step_pk<V>(p, xv);
+        else if (V == V_MIX)
+            step_mix<false>(a, p, x, xv, s0, s1);
+        else if (V == V_MIXS)
+            step_mix<true>(a, p, x, xv, s0, s1);
+        else
+            step<V>(a, x, y);
+    }
+    unsigned long long t1;
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1));
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r += a[k] + p[k].x + p[k].y;
+    if (r == 12345.f) out[0] = r + (float)(s0 + s1);  // keep the chains
+    if ((threadIdx.x & 63) == 0) {
+        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+        span[2 * w] = t0;
+        span[2 * w + 1] = t1;
+    }
+}
+
+template <int V>
+void launch(int blocks, int steps, float *o, unsigned long long *sp) {
+    hipLaunchKernelGGL(issue_kernel<V>, dim3(blocks), dim3(256), 0, 0, steps, o, sp);
+}
+
+int main(int argc, char **argv) {
+    const int steps = argc > 1 ? atoi(argv[1]) : 4096;
+    hipDeviceProp_t prop;
+    CHECK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    const int wmax = 8;
+    float *o;
+    unsigned long long *sp;
+    CHECK(hipMalloc(&o, sizeof(float)));
+    CHECK(hipMalloc(&sp, sizeof(unsigned long long) * 2 * 4 * cus * wmax));
+    std::vector<unsigned long long> hs(2 * 4 * cus * wmax);
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    void (*fn[V_COUNT])(int, int, float *, unsigned long long *) = {
+        launch<0>, launch<1>, launch<2>, launch<3>, launch<4>, launch<5>,
+        launch<6>, launch<7>, launch<8>, launch<9>, launch<10>};
+    const int ws[3] = {1, 2, 8};
+    printf("{\"cus\": %d, \"clock_khz\": %d, \"steps\": %d, \"results\": [\n", cus, prop.clockRate, steps);
+    bool first = true;
+    for (int v = 0; v < V_COUNT; ++v) {
+        for (int wi = 0; wi < 3; ++wi) {
+            const int W = ws[wi], blocks = cus * W;
+            fn[v](blocks, 64, o, sp);  // warm-up (code, clocks)
+            CHECK(hipEventRecord(a));
+            fn[v](blocks, steps, o, sp);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            CHECK(hipGetLastError());
+            float ms = 0.f;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            CHECK(hipMemcpy(hs.data(), sp, sizeof(unsigned long long) * 2 * 4 * blocks, hipMemcpyDeviceToHost));
+            // the launch's span on the shader clock: s_memtime is one counter per XCD, so take each
+            // wave's own (end - start) and the mean over waves, which with all waves resident at once
+            // is the launch's busy span
+            double mean_span = 0.0;
+            for (int w = 0; w < 4 * blocks; ++w) mean_span += (double)(hs[2 * w + 1] - hs[2 * w]);
+            mean_span /= 4.0 * blocks;
+            const double waves = 4.0 * blocks;
+            const double vinsts = waves * steps * kValu[v];
+            // per SIMD: W waves, each issuing steps * kValu VALU, over mean_span cycles
+            const double cyc_per_inst = mean_span / ((double)W * steps * kValu[v]);
+            printf("%s{\"variant\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"valu_wave_insts_per_s\": %.4g, "
+                   "\"salu_per_valu\": %.2f, \"simd_cycles_per_valu_inst\": %.3f, \"clock_ghz_implied\": %.3f}",
+                   first ? "" : ",\n", kNames[v], W, ms, vinsts / (ms * 1e-3), (double)kSalu[v] / kValu[v],
+                   cyc_per_inst, mean_span / (ms * 1e-3) / 1e9);
+            first = false;
+        }
+    }
+    printf("\n]}\n");
+    return 0;
+}
