@@ -161,6 +161,19 @@ typedef struct {
                              profiles in every band group (its common grid built over them) and
                              takes FromRGB per record into the group's bands; exact_mo = 1 runs the
                              reference-order gather */
+    int gen_profile;      /* "genprofile" = true. false: no profile is prepared (preparedBSSRDFData =
+                             NULL, layeredskin.cpp:70,120-122) and the material carries no subsurface
+                             term: its surfaces get no Mo() term and its irradiance points are lit as
+                             a point without a MultipoleBSSRDF (Ft = 1, no albedo^mix:
+                             multipolesubsurface.cpp:100-107,139-140). (The reference would read the
+                             NULL profile through MultipoleBSSRDF::rho / reflectance,
+                             reflection.cpp:833-843; this is the no-BSSRDF branch it has for that.) */
+    int show_irradiance_points;   /* "showirradiancepoints" = false: the material's profile is
+                             ComputeIrradiancePointsProfile (multipole.cpp:551-567) -- every band a
+                             disc of radius irradiance_point_size, Rd = 1 / (pi r^2) for d < r -- and
+                             its rho table ComputeRoughRhoData's two zeros (:569-572, Ft = 1):
+                             each irradiance point shows as a disc of its irradiance */
+    float irradiance_point_size;  /* "irradiancepointsize" = 0.002 (world units) */
 } mpss_layeredskin;
 
 void mpss_layeredskin_defaults(mpss_layeredskin *m);

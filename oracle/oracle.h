@@ -210,6 +210,7 @@ void o_scene_free(o_scene *s);
 /* LayeredSkin "albedo" (which = 0, a spectrum imagemap) or "bumpmap" (which = 1, a float imagemap) */
 /* rgbprofile material: its rd table's rows 0..2 are the R, G, B profiles (o_mo_batch_rgb) */
 int o_scene_set_material_rgb(o_scene *s, int material, int rgb);
+int o_scene_set_material_no_bssrdf(o_scene *s, int material, int no_bssrdf);
 int o_scene_set_material_texture(o_scene *s, int material, int which, int W, int H, const float *texels,
                                  float shift, float scale, float gamma, int wrap, int trilinear, float max_aniso,
                                  float su, float sv, float du, float dv);

@@ -154,6 +154,7 @@ typedef struct {
     float rcp[O_NB];
     int rgb; /* rgbprofile: rd rows 0..2 = R, G, B (multipole.cpp:85-107) */
     int lambert; /* the area-light sphere's default "matte" material: one Lambertian(R) BxDF */
+    int no_bssrdf; /* LayeredSkin genprofile false: no MultipoleBSSRDF data (layeredskin.cpp:120-122) */
 } o_mat;
 
 typedef struct { float bmin[3], bmax[3]; int left, right, first, count; } o_bnode;
@@ -223,6 +224,15 @@ int o_scene_add_material(o_scene *s, const float *R, const float *T, const float
 int o_scene_set_material_rgb(o_scene *s, int material, int rgb) {
     if (material < 0 || material >= s->nmats) return -1;
     s->mats[material].rgb = rgb;
+    return 0;
+}
+
+/* genprofile false (layeredskin.cpp:70,120-122): preparedBSSRDFData = NULL. Li adds no Mo() term and
+ * IrradianceTask lights the material's points as points without a MultipoleBSSRDF
+ * (multipolesubsurface.cpp:100-107: Ft = 1, no albedo^mix). */
+int o_scene_set_material_no_bssrdf(o_scene *s, int material, int no_bssrdf) {
+    if (material < 0 || material >= s->nmats) return -1;
+    s->mats[material].no_bssrdf = no_bssrdf;
     return 0;
 }
 
@@ -1227,6 +1237,7 @@ static void *irr_worker(void *arg) {
         const o_surface_point *sp = &j->pts[i];
         v3 p = mk(sp->p[0], sp->p[1], sp->p[2]), n = mk(sp->n[0], sp->n[1], sp->n[2]);
         const o_mat *mat = sp->material < (uint32_t)s->nmats ? &s->mats[sp->material] : NULL;
+        if (mat && mat->no_bssrdf) mat = NULL; /* the bssrdf == NULL branch (multipolesubsurface.cpp:100-107) */
         float E[O_NB];
         for (int c = 0; c < O_NB; ++c) E[c] = 0.f;
         for (int l = 0; l < s->nlights; ++l) {
@@ -1492,7 +1503,7 @@ static void sample_li(const o_scene *s, int spp, uint32_t seed, int px, int py, 
     }
     if (!mat->has_alb) memcpy(alb1, mat->alb_1mmix, sizeof(alb1));
     /* Mo() term (multipolesubsurface.cpp:268-290) */
-    if (s->octree) {
+    if (s->octree && !mat->no_bssrdf) {
         float q[3] = {fr.p.x, fr.p.y, fr.p.z}, mo[O_NB];
         if (mat->rgb)
             o_mo_batch_rgb(s->octree, 1, q, mat->rd, mat->L, mat->rcp, s->max_error, mo, NULL, NULL, 1);

@@ -126,6 +126,8 @@ void Context::mo_batch(uint32_t mid, int q, const float *p_dev, float *out_dev, 
         if (!have_octree_) throw Error(MPSS_ERR_INVALID, "no irradiance points: call mpss_set_irradiance_points first");
         if (mid >= materials_.size()) throw Error(MPSS_ERR_INVALID, "unknown material id " + std::to_string(mid));
         m = materials_[mid].get();
+        if (m->no_bssrdf)
+            throw Error(MPSS_ERR_INVALID, "material " + std::to_string(mid) + " has no profile (genprofile false)");
         mode = cfg_.exact_mo;
         if (m->dipole) {
             mode = -1;  // closed-form functor: the reference-order gather (dipole.h)
@@ -218,13 +220,26 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
         mat->rgb = true;
     }
     const int distinct = m.rgb_profile ? 3 : NB;  // rgbprofile: 3 distinct channels (R, G, B)
-    if (m.use_monte_carlo && !m.rgb_profile)
+    if (!m.gen_profile) {
+        // preparedBSSRDFData = NULL: a zero placeholder profile and rho table (never read by a gather)
+        mat->no_bssrdf = true;
+        mat->rgb = false;
+        irradiance_points_profile(1.f, mat->profile, mat->rho);
+        std::fill(mat->profile.table.begin(), mat->profile.table.end(), 0.f);
+    } else if (m.show_irradiance_points) {
+        // ComputeIrradiancePointsProfile(irradiancePointSize) + ComputeRoughRhoData (layeredskin.cpp:
+        // 93-95), in place of the multipole profile (rgbprofile / usemontecarlo are not consulted)
+        mat->rgb = false;
+        irradiance_points_profile(m.irradiance_point_size, mat->profile, mat->rho);
+    } else if (m.use_monte_carlo && !m.rgb_profile)
         build_profile_mc(lp, m.photons, 89, mat->profile);
     else if (cfg_.profile_on_host || sp.desired_length > 1024)
         build_profile(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile, 0, distinct);
     else
         build_profile_gpu(lp, sp.desired_length, sp.lerp_on_thin_slab, mat->profile, 0, distinct);
-    if (cfg_.profile_on_host)
+    if (!m.gen_profile || m.show_irradiance_points)
+        ;  // (rho set above)
+    else if (cfg_.profile_on_host)
         build_rho_table(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
     else
         build_rho_table_gpu(sp.roughness, sp.ior[0], sp.double_ref_sslf, 1025, 256, mat->rho);
@@ -234,7 +249,9 @@ uint32_t Context::add_layeredskin(const mpss_layeredskin &m) {
     mat->roughness = m.roughness;
     mat->ior = m.layer_ior[0];
     mat->double_ref_sslf = m.double_ref_sslf != 0;
-    mat->is_monte_carlo = m.use_monte_carlo != 0;  // Ft = 1 in Li (multipolesubsurface.cpp:285)
+    // Ft = 1 in Li (multipolesubsurface.cpp:285); MultipoleBSSRDFData(..., useMonteCarloProfile) keeps the
+    // flag whichever profile was prepared (layeredskin.cpp:116)
+    mat->is_monte_carlo = m.use_monte_carlo != 0;
     mat->dev_profile.upload(mat->profile.table.data(), mat->profile.length, mat->profile.rcp, cfg_.mo_band_dealing == 1);
     if (mat->rgb) {
         mat->dev_rgb.upload(mat->profile.table.data(), 3 * (size_t)mat->profile.length);

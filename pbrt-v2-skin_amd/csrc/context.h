@@ -29,6 +29,9 @@ struct Material {
     float roughness = 0.4f, ior = 1.4f;
     bool double_ref_sslf = false;
     bool is_monte_carlo = false;
+    // "genprofile" false (layeredskin.cpp:70,120-122): no MultipoleBSSRDF data -- no Mo() term on its
+    // surfaces, its irradiance points lit as points without a BSSRDF; the tables are a zero placeholder
+    bool no_bssrdf = false;
     DeviceProfile dev_profile;
     DevBuf<float> dev_rho;  // [n_rho]
     int albedo_tex = -1, bump_tex = -1;  // ImageTexture ids ("texture albedo" / "texture bumpmap")

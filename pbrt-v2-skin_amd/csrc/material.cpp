@@ -615,6 +615,20 @@ float rho_hh(float roughness, float eta, bool fixed, int sqrt_samples) {
     return k.sum / (kPiF * n);
 }
 
+void irradiance_points_profile(float radius, ProfileTables &p, RhoTable &rho) {
+    const float area = (float)(M_PI * radius * radius);  // float area = M_PI * radius * radius (double product)
+    const float v = 1.f / area;                          // fullSpectrum[i] / area, fullSpectrum = Spectrum(1)
+    p.length = 2;
+    p.table.assign((size_t)NB * 2, v);
+    for (int c = 0; c < NB; ++c) {
+        p.spacing[c] = radius * radius;
+        p.rcp[c] = 1.f / p.spacing[c];
+        p.total_reflectance[c] = 1.f;
+    }
+    rho.hd.assign(2, 0.f);
+    rho.hh = 0.f;
+}
+
 void build_rho_table(float roughness, float eta, bool fixed, int n_entries, int sqrt_samples, RhoTable &out,
                      int nthreads) {
     const Microfacet m = rho_bxdf(roughness, eta, fixed);

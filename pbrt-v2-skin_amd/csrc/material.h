@@ -52,6 +52,10 @@ void build_rho_table_gpu(float roughness, float eta, bool fixed_fresnel, int n_e
                          RhoTable &out, hipStream_t stream = 0);
 // ComputeRhoHHFromBxDF (multipole.cpp:466-480)
 float rho_hh(float roughness, float eta, bool fixed_fresnel, int sqrt_samples);
+// LayeredSkin "showirradiancepoints": ComputeIrradiancePointsProfile(radius) (multipole.cpp:551-567) --
+// every band the two-entry table {1 / area, 1 / area}, area = (float)(M_PI * r * r), dsqSpacing = r * r,
+// so Rd(d^2) = 1 / area for d < r and 0 beyond -- and ComputeRoughRhoData (:569-572): rho_hd = {0, 0}.
+void irradiance_points_profile(float radius, ProfileTables &p, RhoTable &rho);
 void build_rho_table(float roughness, float eta, bool fixed_fresnel, int n_entries, int sqrt_samples,
                      RhoTable &out, int nthreads = 0);
 

@@ -43,7 +43,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 11; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 12; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
                                           // 6: GPU octree build (octree_on_host), mpss_octree_export;
@@ -56,6 +56,8 @@ int mpss_abi_version(void) { return 11; }  // 2: poisson point finder, infinite 
                                           //     lane-record counts in mpss_render_stats
                                           // 11: rgbprofile through the sharded gather (its own common
                                           //     grid), mpss_host_common_grid u1start / rgb mode
+                                          // 12: LayeredSkin genprofile / showirradiancepoints /
+                                          //     irradiancepointsize; mpss_host_common_grid near_field
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -116,6 +118,9 @@ void mpss_layeredskin_defaults(mpss_layeredskin *m) {
     m->use_monte_carlo = 0;
     m->photons = 10000000ull;
     m->rgb_profile = 0;
+    m->gen_profile = 1;
+    m->show_irradiance_points = 0;
+    m->irradiance_point_size = 0.002f;
 }
 
 int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {
@@ -123,6 +128,8 @@ int mpss_add_layeredskin(mpss_ctx *c, const mpss_layeredskin *m, uint32_t *id) {
         require(c && m && id, "mpss_add_layeredskin: null argument");
         require(m->desired_length >= 2 && m->desired_length <= 4096, "desiredlength out of range [2, 4096]");
         require(m->nmperunit > 0.f, "nmperunit must be positive");
+        require(!m->show_irradiance_points || m->irradiance_point_size > 0.f,
+                "irradiancepointsize must be positive with showirradiancepoints");
         *id = reinterpret_cast<Context *>(c)->add_layeredskin(*m);
     });
 }

@@ -263,7 +263,7 @@ void Context::upload_scene() {
         r.mf.fixed_fresnel = m.double_ref_sslf ? 1 : 0;
         r.rho = m.dev_rho.ptr;
         r.n_rho = (int)m.rho.hd.size();
-        r.has_bssrdf = 1;
+        r.has_bssrdf = m.no_bssrdf ? 0 : 1;
         r.is_mc = m.is_monte_carlo ? 1 : 0;
         r.mix = cfg_.mix;
         for (int c = 0; c < NB; ++c) r.band_pos[c] = m.dev_profile.groups.pos[c];
@@ -673,7 +673,7 @@ void Context::render_tiles(int spp, uint32_t seed, int n, const int32_t *rects, 
     std::vector<SssMat> sss;
     if (have_octree_)
         for (size_t i = 0; i < materials_.size(); ++i)
-            if (!materials_[i]->dipole)
+            if (!materials_[i]->dipole && !materials_[i]->no_bssrdf)
                 sss.push_back(SssMat{(int)i, materials_[i].get(),
                                      &dev_octree_.ensure_layout(materials_[i]->dev_profile.groups)});
     RenderScene sc = render_scene();
@@ -1056,7 +1056,7 @@ void Context::reset_render_stats() {
 
 int Context::first_bssrdf_material() const {
     for (size_t i = 0; i < materials_.size(); ++i)
-        if (!materials_[i]->dipole) return (int)i;
+        if (!materials_[i]->dipole && !materials_[i]->no_bssrdf) return (int)i;
     return -1;
 }
 

@@ -70,7 +70,8 @@ class LayeredSkin(C.Structure):
                 ("albedo", C.c_float * NB), ("Kr", C.c_float * NB), ("Kt", C.c_float * NB),
                 ("desired_length", C.c_int), ("lerp_on_thin_slab", C.c_int),
                 ("double_ref_sslf", C.c_int), ("use_monte_carlo", C.c_int), ("photons", C.c_uint64),
-                ("rgb_profile", C.c_int)]
+                ("rgb_profile", C.c_int), ("gen_profile", C.c_int), ("show_irradiance_points", C.c_int),
+                ("irradiance_point_size", C.c_float)]
 
 
 class Imagemap(C.Structure):

@@ -351,10 +351,13 @@ def _skin_params(ps, textures):
     for k in ("desiredlength",):
         if k in ps:
             p["desired_length"] = int(ps.one(k))
+    if "irradiancepointsize" in ps:
+        p["irradiance_point_size"] = float(ps.one("irradiancepointsize"))
     if "photons" in ps:  # a string parameter parsed with _strtoui64 (layeredskin.cpp:251-252)
         p["photons"] = int(str(ps.one("photons")))
     for k, dst in (("lerponthinslab", "lerp_on_thin_slab"), ("doublerefsslf", "double_ref_sslf"),
-                   ("usemontecarlo", "use_monte_carlo"), ("rgbprofile", "rgb_profile")):
+                   ("usemontecarlo", "use_monte_carlo"), ("rgbprofile", "rgb_profile"), ("genprofile", "gen_profile"),
+                   ("showirradiancepoints", "show_irradiance_points")):
         if k in ps:
             v = ps.one(k)
             p[dst] = int(v in (True, "true", 1))

@@ -30,6 +30,8 @@ def _lib():
                                        C.c_int, C.c_int, f32p, C.c_int, f32p]
     L.o_scene_set_material_rgb.restype = C.c_int
     L.o_scene_set_material_rgb.argtypes = [vp, C.c_int, C.c_int]
+    L.o_scene_set_material_no_bssrdf.restype = C.c_int
+    L.o_scene_set_material_no_bssrdf.argtypes = [vp, C.c_int, C.c_int]
     L.o_scene_add_mesh.restype = C.c_int
     L.o_scene_add_mesh.argtypes = [vp, C.c_int, f32p, vp, vp, vp, C.c_int, oracle_lib.i32p, f32p, f32p, C.c_int,
                                    C.c_int]
@@ -115,6 +117,12 @@ def tables_from_oracle(sc):
     import oracle_lib
     out = []
     for m in sc.materials:
+        if not m.get("gen_profile", 1):  # preparedBSSRDFData = NULL: nothing is read (o_mat.no_bssrdf)
+            out.append((np.zeros((NB, 2), np.float32), np.ones(NB, np.float32), np.zeros(2, np.float32)))
+            continue
+        if m.get("show_irradiance_points"):
+            out.append(irradiance_points_tables(m.get("irradiance_point_size", 0.002)))
+            continue
         th = tuple(m.get("layer_thickness_nm", (0.25e6, 20e6)))
         ior = tuple(m.get("layer_ior", (1.4, 1.4)))
         rough = m.get("roughness", 0.3)
@@ -131,6 +139,17 @@ def tables_from_oracle(sc):
         rho, _ = oracle_lib.rho_table(rough, ior[0], fixed=bool(m.get("double_ref_sslf", 0)))
         out.append((tab, rcp, rho))
     return out
+
+
+def irradiance_points_tables(radius):
+    """ComputeIrradiancePointsProfile(radius) (multipole.cpp:551-567) and ComputeRoughRhoData
+    (:569-572), restated: each band {1/area, 1/area} with area = float(M_PI * r * r) (a double
+    product), dsqSpacing = r * r (float), rcp = 1 / dsqSpacing; rho_hd = {0, 0}."""
+    r = np.float32(radius)
+    area = np.float32(np.float64(np.pi) * np.float64(r) * np.float64(r))
+    v = np.float32(1.0) / area
+    rcp = np.float32(1.0) / (r * r)
+    return (np.full((NB, 2), v, np.float32), np.full(NB, rcp, np.float32), np.zeros(2, np.float32))
 
 
 def tables_from_host(sc, mpss):
@@ -169,8 +188,10 @@ class OracleScene:
             L.o_scene_add_material(self.h, Kr, Kt, alb, cfg.mix, skin.roughness, skin.layer_ior[0],
                                    int(skin.double_ref_sslf), rho, len(rho), int(skin.use_monte_carlo),
                                    np.ascontiguousarray(tab, np.float32), tab.shape[1], rcp)
-            if skin.rgb_profile:
+            if skin.rgb_profile and skin.gen_profile and not skin.show_irradiance_points:
                 assert L.o_scene_set_material_rgb(self.h, mid, 1) == 0
+            if not skin.gen_profile:
+                assert L.o_scene_set_material_no_bssrdf(self.h, mid, 1) == 0
             for which, key in ((0, "albedo_tex"), (1, "bump_tex")):
                 if m.get(key) is not None:
                     W, H, ptr, arr, rest = _tex_args(m[key])

@@ -10,11 +10,13 @@
 // (counted from its ISA: hipcc -S of mo_wave_cg.hip) with its SALU beside it. Every wave stamps
 // s_memtime at its start and end, so cycles are the shader clock's, not an assumed 2.4 GHz.
 //
-// Launch: 256-thread workgroups (one wave per SIMD each), W workgroups per CU => W waves per SIMD;
-// W = 8 is the gather's occupancy (two 1024-thread workgroups per CU).
+// Launch: W waves per SIMD as the gather runs them -- one workgroup of 64 x 4 x W threads per CU for
+// W = 1, 2, 4, and two 1024-thread workgroups per CU for W = 8 (mo_band_wave_kernel's shape); each
+// workgroup holds enough dynamic LDS that no third fits, so every wave of a CU is resident at once.
 //
-// Printed per (variant, W): wave64 instructions per second over the chip, and SIMD cycles per wave
-// instruction = (s_memtime span of the launch's waves) x 1024 SIMDs / instructions.
+// Printed per (variant, W): wave64 instructions per second over the chip; the shader clock the waves
+// ran at (s_memtime ticks over s_memrealtime's 100 MHz); and SIMD cycles per wave instruction = the
+// waves' mean s_memtime span / (W x instructions per wave).
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/microbench/valu_issue.hip -o tools/microbench/valu_issue
 #include <hip/hip_runtime.h>
@@ -160,13 +162,13 @@ __device__ __forceinline__ void step_mix(float (&a)[8], f2v (&p)[8], float x, f2
         if (SALU) {
             R4(asm volatile("s_add_u32 %0, %0, 32\n s_addc_u32 %1, %1, 0" : "+s"(s0), "+s"(s1) ::"scc");)
             R4(asm volatile("s_cmp_ge_i32 %0, %1\n s_cselect_b32 %0, %0, %1" : "+s"(s0) : "s"(s1) : "scc");)
-            R4(asm volatile("s_mov_b32 %0, %1\n s_or_b32 %1, %1, %0" : "+s"(s0), "+s"(s1));)
+            R4(asm volatile("s_mov_b32 %0, %1\n s_or_b32 %1, %1, %0" : "+s"(s0), "+s"(s1) ::"scc");)
         }
     }
 }
 
 template <int V>
-__global__ __launch_bounds__(256) void issue_kernel(int steps, float *out, unsigned long long *span) {
+__global__ __launch_bounds__(1024) void issue_kernel(int steps, float *out, unsigned long long *span) {
     const float x = 1.0f + threadIdx.x * 1e-7f, y = 1e-3f;
     float a[8];
     f2v p[8];
@@ -177,8 +179,8 @@ __global__ __launch_bounds__(256) void issue_kernel(int steps, float *out, unsig
     }
     const f2v xv = f2v{x, y};
     uint32_t s0 = blockIdx.x, s1 = steps;
-    unsigned long long t0;
-    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t0));
+    unsigned long long t0, r0;
+    asm volatile("s_memtime %0\n s_memrealtime %1\n s_waitcnt lgkmcnt(0)" : "=s"(t0), "=s"(r0));
     for (int i = 0; i < steps; ++i) {
         if (V == V_PKMUL || V == V_PKADD || V == V_PKFMA)
             step_pk<V>(p, xv);
@@ -189,22 +191,27 @@ __global__ __launch_bounds__(256) void issue_kernel(int steps, float *out, unsig
         else
             step<V>(a, x, y);
     }
-    unsigned long long t1;
-    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t1));
+    unsigned long long t1, r1;
+    asm volatile("s_memtime %0\n s_memrealtime %1\n s_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1));
     float r = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) r += a[k] + p[k].x + p[k].y;
     if (r == 12345.f) out[0] = r + (float)(s0 + s1);  // keep the chains
     if ((threadIdx.x & 63) == 0) {
-        const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-        span[2 * w] = t0;
-        span[2 * w + 1] = t1;
+        const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        span[2 * w] = t1 - t0;
+        span[2 * w + 1] = r1 - r0;
     }
 }
 
 template <int V>
-void launch(int blocks, int steps, float *o, unsigned long long *sp) {
-    hipLaunchKernelGGL(issue_kernel<V>, dim3(blocks), dim3(256), 0, 0, steps, o, sp);
+void launch(int blocks, int threads, size_t lds, int steps, float *o, unsigned long long *sp) {
+    static bool attr = false;
+    if (!attr) {
+        CHECK(hipFuncSetAttribute((const void *)issue_kernel<V>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(issue_kernel<V>, dim3(blocks), dim3(threads), lds, 0, steps, o, sp);
 }
 
 int main(int argc, char **argv) {
@@ -217,42 +224,51 @@ int main(int argc, char **argv) {
     unsigned long long *sp;
     CHECK(hipMalloc(&o, sizeof(float)));
     CHECK(hipMalloc(&sp, sizeof(unsigned long long) * 2 * 4 * cus * wmax));
-    std::vector<unsigned long long> hs(2 * 4 * cus * wmax);
+    std::vector<unsigned long long> hs(2 * 4 * cus * wmax);  // (wave span, real-time span) per wave
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    void (*fn[V_COUNT])(int, int, float *, unsigned long long *) = {
+    void (*fn[V_COUNT])(int, int, size_t, int, float *, unsigned long long *) = {
         launch<0>, launch<1>, launch<2>, launch<3>, launch<4>, launch<5>,
         launch<6>, launch<7>, launch<8>, launch<9>, launch<10>};
-    const int ws[3] = {1, 2, 8};
+    const int ws[4] = {1, 2, 4, 8};
     printf("{\"cus\": %d, \"clock_khz\": %d, \"steps\": %d, \"results\": [\n", cus, prop.clockRate, steps);
     bool first = true;
     for (int v = 0; v < V_COUNT; ++v) {
-        for (int wi = 0; wi < 3; ++wi) {
-            const int W = ws[wi], blocks = cus * W;
-            fn[v](blocks, 64, o, sp);  // warm-up (code, clocks)
+        for (int wi = 0; wi < 4; ++wi) {
+            const int W = ws[wi];
+            // W <= 4: one workgroup of 4 W waves per CU; W = 8: two of 16 (the gather's shape). The LDS
+            // keeps a further workgroup off the CU.
+            const int threads = W <= 4 ? 256 * W : 1024, per_cu = W <= 4 ? 1 : 2, blocks = cus * per_cu;
+            const size_t lds = per_cu == 1 ? 96 * 1024 : 64 * 1024;
+            fn[v](blocks, threads, lds, 64, o, sp);  // warm-up (code, clocks)
             CHECK(hipEventRecord(a));
-            fn[v](blocks, steps, o, sp);
+            fn[v](blocks, threads, lds, steps, o, sp);
             CHECK(hipEventRecord(b));
             CHECK(hipEventSynchronize(b));
             CHECK(hipGetLastError());
             float ms = 0.f;
             CHECK(hipEventElapsedTime(&ms, a, b));
-            CHECK(hipMemcpy(hs.data(), sp, sizeof(unsigned long long) * 2 * 4 * blocks, hipMemcpyDeviceToHost));
-            // the launch's span on the shader clock: s_memtime is one counter per XCD, so take each
-            // wave's own (end - start) and the mean over waves, which with all waves resident at once
-            // is the launch's busy span
-            double mean_span = 0.0;
-            for (int w = 0; w < 4 * blocks; ++w) mean_span += (double)(hs[2 * w + 1] - hs[2 * w]);
-            mean_span /= 4.0 * blocks;
-            const double waves = 4.0 * blocks;
+            const int waves_n = blocks * threads / 64;
+            CHECK(hipMemcpy(hs.data(), sp, sizeof(unsigned long long) * 2 * waves_n, hipMemcpyDeviceToHost));
+            // each wave's own span on the shader clock (s_memtime) and on the 100 MHz real-time clock;
+            // every wave of a CU is resident from the start, so the mean span is the SIMDs' busy time
+            double mean_span = 0.0, mean_real = 0.0;
+            for (int w = 0; w < waves_n; ++w) {
+                mean_span += (double)hs[2 * w];
+                mean_real += (double)hs[2 * w + 1];
+            }
+            mean_span /= waves_n;
+            mean_real /= waves_n;
+            const double waves = waves_n;
             const double vinsts = waves * steps * kValu[v];
             // per SIMD: W waves, each issuing steps * kValu VALU, over mean_span cycles
             const double cyc_per_inst = mean_span / ((double)W * steps * kValu[v]);
             printf("%s{\"variant\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"valu_wave_insts_per_s\": %.4g, "
-                   "\"salu_per_valu\": %.2f, \"simd_cycles_per_valu_inst\": %.3f, \"clock_ghz_implied\": %.3f}",
+                   "\"salu_per_valu\": %.2f, \"simd_cycles_per_valu_inst\": %.3f, \"clock_ghz\": %.3f, "
+                   "\"span_over_launch\": %.3f}",
                    first ? "" : ",\n", kNames[v], W, ms, vinsts / (ms * 1e-3), (double)kSalu[v] / kValu[v],
-                   cyc_per_inst, mean_span / (ms * 1e-3) / 1e9);
+                   cyc_per_inst, mean_span / (mean_real * 10.0), mean_real * 1e-8 / (ms * 1e-3));
             first = false;
         }
     }

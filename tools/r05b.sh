@@ -1,0 +1,8 @@
+# round 5, second GPU session: the corrected VALU-issue microbenchmark, then the whole -m gpu suite
+# (pigment sweep, end-to-end independent C2/C3/C5, reference-sampler full frame, LayeredSkin switches).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/microbench/valu_issue 4096 > gpurun_out/micro_valu_issue_b.json 2>&1 || { echo valu_issue failed; cat gpurun_out/micro_valu_issue_b.json; exit 1; }
+bash tools/gpu.sh r05b tests
