@@ -14,22 +14,40 @@
 // per group, so consecutive pre-order records share lines); only the table lookups are per-lane
 // gathers (one 8-byte load per band: the lerp pair).
 //
-// What bounds it: the L2 request rate of the per-lane table gathers (the texture
-// address units are ~90 % busy and the requests run at ~0.93 of the rate a pure gather
-// microbenchmark sustains). The traversal is the UNION of the wave's 64 pruned traversals, so the
-// 64 queries of a wave should be neighbours: each 1024-query chunk is sorted by a Morton key of
-// the query position before queries are dealt to lanes (mo_kernel.hip), and the per-record work
-// below is kept to packed-f32 arithmetic on 32-bit table offsets.
+// What bounds it: with the common grid (the default, CommonGrid below) VALU issue -- the record loop's
+// instruction count (SQ_ACTIVE_INST_VALU busy ~0.9 of the SIMDs' cycles, the measured
+// issue ceiling of this instruction mix in tools/microbench/valu_issue.hip); with the per-band tables
+// (mo_common_grid 0) the L2 request rate of the per-lane table gathers. The traversal is the UNION of
+// the wave's 64 pruned traversals, so the 64 queries of a wave should be neighbours: each 1024-query
+// chunk is sorted by a Morton key of the query position before queries are dealt to lanes
+// (mo_kernel.hip), and the per-record work below is kept to a few VALU on 32-bit table offsets.
 //
 // Each query walks exactly the node set of SubsurfaceOctreeNode::Mo (diffusionutil.h:175-210)
 // minus subtrees that lie past the end of all of the group's profiles (they add +0 for these
-// bands), in pre-order, with the packet kernel's summation order: results are bit-identical
-// to mo_packet_traverse (one running sum per band, a leaf's points summed first).
+// bands), in pre-order, with the packet kernel's summation order. With the per-band tables the
+// results are bit-identical to mo_packet_traverse (one running sum per band, a leaf's points summed
+// first); the common grid resamples the far lookups (within kCgRelTol / kCgAbsTol per value) and, with
+// MPSS_MO_FUSED, forms each term with FMAs, so its sums are within the float-summation bound of the
+// reference (tests/test_mo_gpu.py) rather than bit-identical to it.
 #pragma once
 #include <cstdlib>
 
 #include "common.h"
 #include "octree.h"
+
+// MPSS_MO_FUSED (default 1): the common-grid gather forms each Rd as a + t (b - a) with one FMA and
+// accumulates Rd * (E * area) with one FMA per band (cg_combine) -- fewer and cheaper VALU
+// instructions on the record loop the gather's time is made of. 0: the reference's operation order,
+// (1 - t) a + t b and (Rd * E) * area, as the per-band gather keeps (for A/B builds).
+#ifndef MPSS_MO_FUSED
+#define MPSS_MO_FUSED 1
+#endif
+// MPSS_MO_TPATH (default 1, with MPSS_MO_FUSED): each path of the common-grid fetch forms its own lerp
+// parameters -- the rows one fract(u) for the four bands, the LDS and own-table lanes fract(d2 rcp_j)
+// per band -- so a wave whose lanes all read rows pays one fract instead of four (CgRec::f then holds t).
+#ifndef MPSS_MO_TPATH
+#define MPSS_MO_TPATH 1
+#endif
 
 namespace mpss {
 
@@ -130,6 +148,7 @@ struct BandTree {
     const float4 *__restrict__ band_et;  // [kGroups][n_nodes]
     const float4 *__restrict__ pt_hdr;   // [n_points] {p, area (sign bit: E black)}
     const float4 *__restrict__ band_e;   // [kGroups][n_points]
+    const float4 *__restrict__ band_ew;  // [kGroups][n_points]: E * area (the common-grid gather)
     const float *__restrict__ table;     // [NB][L] + 2 trailing zeros (DeviceProfile::upload)
     BandGroups groups;
     float grcp[kGroups][4];              // rcpDsqSpacing of each group slot (0 for an empty slot)
@@ -400,29 +419,43 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // earlier step's loads target only once those have returned, and LDS returns first (the
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
     // issue order (vector memory returns in order), so the second does not wait for the first.
-    const int path = u < c.u0lim ? 1 : ((u < c.u1lim && u >= c.u1start) ? 0 : 2);
+    // The paths as lane masks (two compares and scalar mask logic; u1start >= u0lim, so a lane on
+    // the rows is never on the LDS path)
+    const bool p_lds = u < c.u0lim;
+    const bool p_row = u >= c.u1start && u < c.u1lim;
+    const bool p_own = !(p_lds || p_row);
+    const int path = p_lds ? 1 : (p_row ? 0 : 2);  // (COUNT only)
     // the row step's address up front, as a 32-bit byte offset from the (wave-uniform) grid base: one
     // VGPR, a global load in saddr form. (The own-table step's four addresses are formed in its branch:
     // with the gather VALU-bound, a wave whose lanes all take the rows or the LDS does not pay them.)
     uint32_t orow = 32u * ((uint32_t)u + c.rowoff);
     asm volatile("" : "+v"(orow));
-    if (path == 1) {  // s_j < klim_j for every band: inside its LDS row
+    if (p_lds) {  // s_j < klim_j for every band: inside its LDS row
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
         const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+#if MPSS_MO_FUSED && MPSS_MO_TPATH
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+#endif
     }
     // (keeps the LDS step ahead of the global ones: the compiler otherwise orders the three steps its
     // own way and puts the LDS step last)
     asm volatile("" : "+v"(r.p01), "+v"(r.p23)::"memory");
-    if (path == 0) {
+    if (p_row) {
         gf4v *row = (gf4v *)((const __attribute__((address_space(1))) char *)c.tab + orow);
         r.p01 = row[0];
         r.p23 = row[1];
+#if MPSS_MO_FUSED && MPSS_MO_TPATH
+        const float t = __builtin_amdgcn_fractf(u);  // one lerp parameter for the four bands
+#else
+        const float t = u;
+#endif
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r.f[j] = u;
+        for (int j = 0; j < 4; ++j) r.f[j] = t;
     }
-    if (path == 2) {
+    if (p_own) {
         uint32_t otp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -434,6 +467,10 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
         const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+#if MPSS_MO_FUSED && MPSS_MO_TPATH
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+#endif
     }
     cg_count<COUNT>(b, c, d2, path, hist);
     return r;
@@ -452,6 +489,10 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
     const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
     r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
     r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+#if MPSS_MO_FUSED && MPSS_MO_TPATH
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+#endif
     return r;
 }
 
@@ -459,23 +500,43 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 // gather's, the group rows' on the group grid -- then its range test (multipole.cpp:65-66) as
 // d2 >= tau: only lanes off the LDS path can be past a band's end, and only at the group's reach, so
 // the test runs when some lane of the wave is past the group's first end.
+// MPSS_MO_FUSED: e is E * area for a point (BandTree::band_ew) and Et for a node, w unused.
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
                                            f2v acc[2], lds_float *rk = nullptr) {
     float rd[4];
     const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
+#if MPSS_MO_FUSED
+    // a + t (b - a), one rounding after the product: within an ulp or two of the reference's
+    // (1 - t) a + t b (the far values are a resampling already)
+    // (written out: packed, the four bands' (a, b) pairs would first be shuffled into (a0, a1), (b0, b1)
+    // register pairs -- three v_mov per two bands, more than the packing saves)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float t = MPSS_MO_TPATH ? r.f[j] : __builtin_amdgcn_fractf(r.f[j]);  // (TPATH: fetched as t)
+        float d;
+        asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(v[j].b), "v"(v[j].a));
+        asm("v_fma_f32 %0, %1, %2, %3" : "=v"(rd[j]) : "v"(t), "v"(d), "v"(v[j].a));
+    }
+#else
     band_rd_lerp(r.f, v, rd);
+#endif
     if (__builtin_amdgcn_ballot_w64(d2 >= c.tau_min) != 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
     }
-    if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
-        float o[4];
+    float o[4];
+    if (RGB)  // slots 0..2: the R, G, B profiles on the grid
         from_rgb4(rk, rd[0], rd[1], rd[2], o);
-        band_rd_products<POINT>(o, e, w, acc);
-        return;
-    }
-    band_rd_products<POINT>(rd, e, w, acc);
+    const float *x = RGB ? o : rd;
+#if MPSS_MO_FUSED
+    (void)w;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)  // acc += Rd * (E area), one packed FMA per two bands
+        acc[h] = __builtin_elementwise_fma(f2v{x[2 * h], x[2 * h + 1]}, f2v{e[2 * h], e[2 * h + 1]}, acc[h]);
+#else
+    band_rd_products<POINT>(x, e, w, acc);
+#endif
 }
 
 template <bool POINT, bool COUNT, int KLDS, bool RGB = false>
@@ -554,7 +615,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     // far above the rounding of the quotient (rcp_min 0: pruning off, INF)
     const float box_lim = a.prune_f / a.groups.rcp_min[grp];
     const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
-    const cptr<float4> e_g = as_const(a.band_e + (size_t)grp * a.n_points);
+    // (the common-grid gather's fused products read E * area)
+    const cptr<float4> e_g = as_const(((CG && MPSS_MO_FUSED) ? a.band_ew : a.band_e) + (size_t)grp * a.n_points);
     const cptr<NodeHdr> nodes = as_const(a.nodes);
     const cptr<float4> pt_hdr = as_const(a.pt_hdr);
     int resume = valid ? 0 : 0x7fffffff;

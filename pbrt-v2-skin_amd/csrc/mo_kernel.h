@@ -14,6 +14,7 @@ namespace mpss {
 struct BandLayout {
     BandGroups groups{};
     DevBuf<float4> et, e;
+    DevBuf<float4> ew;  // e scaled by each point's area (the common-grid gather's products, mo_band.h)
 };
 
 struct DeviceOctree {

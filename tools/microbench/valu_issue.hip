@@ -16,7 +16,9 @@
 //
 // Printed per (variant, W): wave64 instructions per second over the chip; the shader clock the waves
 // ran at (s_memtime ticks over s_memrealtime's 100 MHz); and SIMD cycles per wave instruction = the
-// waves' mean s_memtime span / (W x instructions per wave).
+// launch time at that clock / (W x instructions per wave). (A SIMD issues its waves oldest first:
+// with W > 1 a wave's own span is shorter than the launch -- span_over_launch -- so it is not the
+// SIMD's busy time.)
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/microbench/valu_issue.hip -o tools/microbench/valu_issue
 #include <hip/hip_runtime.h>
@@ -45,14 +47,25 @@ enum {
     V_LSHLADD,  // v_lshl_add_u32
     V_MIX,      // the gather's point-record mix (VALU only)
     V_MIXS,     // the same plus its SALU
+    V_ADDU,     // v_add_u32
+    V_MINU,     // v_min_u32
+    V_MINF,     // v_min_f32
+    V_MOV,      // v_mov_b32
+    V_CMP,      // v_cmp_gt_f32 (e64, to an SGPR pair)
+    V_MUL,      // v_mul_f32
+    V_MAX3,     // v_max3_f32
+    V_RCP,      // v_rcp_f32
     V_COUNT
 };
 static const char *kNames[V_COUNT] = {"v_fma_f32",      "v_add_f32",    "v_pk_mul_f32",   "v_pk_add_f32",
                                       "v_pk_fma_f32",   "v_cvt_u32_f32", "v_fract_f32",   "v_cndmask_b32",
-                                      "v_lshl_add_u32", "gather mix (VALU)", "gather mix (VALU + SALU)"};
+                                      "v_lshl_add_u32", "gather mix (VALU)", "gather mix (VALU + SALU)",
+                                      "v_add_u32",      "v_min_u32",    "v_min_f32",      "v_mov_b32",
+                                      "v_cmp_gt_f32 (e64)", "v_mul_f32", "v_max3_f32",   "v_rcp_f32"};
 // wave64 VALU instructions per loop step, and SALU
-static const int kValu[V_COUNT] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 94, 94};  // mix: 2 records x 47
-static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48};
+static const int kValu[V_COUNT] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 94, 94,  // mix: 2 records x 47
+                                   32, 32, 32, 32, 32, 32, 32, 32};
+static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48, 0, 0, 0, 0, 0, 0, 0, 0};
 
 #define R8(X) X X X X X X X X
 #define R4(X) X X X X
@@ -85,6 +98,28 @@ __device__ __forceinline__ void step(float (&a)[8], float x, float y) {
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int k = 0; k < 8; ++k) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(a[k]) : "v"(x));
+    } else if (V == V_ADDU || V == V_MINU || V == V_MINF || V == V_MOV || V == V_MUL || V == V_MAX3 || V == V_RCP) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (V == V_ADDU) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[k]) : "v"(x));
+                if (V == V_MINU) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[k]) : "v"(x));
+                if (V == V_MINF) asm volatile("v_min_f32 %0, %0, %1" : "+v"(a[k]) : "v"(x));
+                if (V == V_MOV) asm volatile("v_mov_b32 %0, %1" : "=v"(a[k]) : "v"(a[(k + 1) & 7]));
+                if (V == V_MUL) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[k]) : "v"(x));
+                if (V == V_MAX3) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(x), "v"(y));
+                if (V == V_RCP) asm volatile("v_rcp_f32 %0, %0" : "+v"(a[k]));
+            }
+    } else if (V == V_CMP) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                uint64_t m;
+                asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(a[k]), "v"(x));
+                asm volatile("" ::"s"(m));
+            }
     } else if (V == V_CND) {
         uint64_t m;
         asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(y));
@@ -229,8 +264,9 @@ int main(int argc, char **argv) {
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     void (*fn[V_COUNT])(int, int, size_t, int, float *, unsigned long long *) = {
-        launch<0>, launch<1>, launch<2>, launch<3>, launch<4>, launch<5>,
-        launch<6>, launch<7>, launch<8>, launch<9>, launch<10>};
+        launch<0>,  launch<1>,  launch<2>,  launch<3>,  launch<4>,  launch<5>,  launch<6>,
+        launch<7>,  launch<8>,  launch<9>,  launch<10>, launch<11>, launch<12>, launch<13>,
+        launch<14>, launch<15>, launch<16>, launch<17>, launch<18>};
     const int ws[4] = {1, 2, 4, 8};
     printf("{\"cus\": %d, \"clock_khz\": %d, \"steps\": %d, \"results\": [\n", cus, prop.clockRate, steps);
     bool first = true;
@@ -262,13 +298,16 @@ int main(int argc, char **argv) {
             mean_real /= waves_n;
             const double waves = waves_n;
             const double vinsts = waves * steps * kValu[v];
-            // per SIMD: W waves, each issuing steps * kValu VALU, over mean_span cycles
-            const double cyc_per_inst = mean_span / ((double)W * steps * kValu[v]);
+            // per SIMD: W waves, each issuing steps * kValu VALU, over the launch (the SIMD issues its
+            // waves oldest first, so one wave's own span is shorter than the SIMD's busy time): the
+            // launch time at the waves' clock
+            const double clk = mean_span / (mean_real * 10.0);  // GHz
+            const double cyc_per_inst = (ms * 1e-3) * clk * 1e9 / ((double)W * steps * kValu[v]);
             printf("%s{\"variant\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"valu_wave_insts_per_s\": %.4g, "
                    "\"salu_per_valu\": %.2f, \"simd_cycles_per_valu_inst\": %.3f, \"clock_ghz\": %.3f, "
                    "\"span_over_launch\": %.3f}",
                    first ? "" : ",\n", kNames[v], W, ms, vinsts / (ms * 1e-3), (double)kSalu[v] / kValu[v],
-                   cyc_per_inst, mean_span / (mean_real * 10.0), mean_real * 1e-8 / (ms * 1e-3));
+                   cyc_per_inst, clk, mean_real * 1e-8 / (ms * 1e-3));
             first = false;
         }
     }
