@@ -48,6 +48,11 @@
 #ifndef MPSS_MO_TPATH
 #define MPSS_MO_TPATH 1
 #endif
+// MPSS_MO_LAZYF (default 1, with MPSS_MO_TPATH): the per-band indices d2 * rcp_j are formed inside the
+// LDS and own-table steps that use them, so a wave whose lanes all read rows forms none.
+#ifndef MPSS_MO_LAZYF
+#define MPSS_MO_LAZYF 1
+#endif
 
 namespace mpss {
 
@@ -404,16 +409,22 @@ __device__ __forceinline__ f2v lds_pair(const BandLane &b, uint32_t k) {
     return f2v{q[0], q[1]};
 }
 
+// the per-band indices d2 * rcp_j (multipole.cpp:63: the float product)
+__device__ __forceinline__ void band_f(const BandLane &b, float d2, float f[4]) {
+    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
+    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
+    f[0] = f01.x;
+    f[1] = f01.y;
+    f[2] = f23.x;
+    f[3] = f23.y;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, const float *table, float d2,
                                           int hist[7]) {
     CgRec r;
-    const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
-    const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
-    r.f[0] = f01.x;
-    r.f[1] = f01.y;
-    r.f[2] = f23.x;
-    r.f[3] = f23.y;
+    constexpr bool lazy = MPSS_MO_FUSED && MPSS_MO_TPATH && MPSS_MO_LAZYF;
+    if (!lazy) band_f(b, d2, r.f);
     const float u = d2 * c.rg;
     // Three sequential masked steps, LDS first: a later step's loads may overwrite registers an
     // earlier step's loads target only once those have returned, and LDS returns first (the
@@ -431,6 +442,7 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     uint32_t orow = 32u * ((uint32_t)u + c.rowoff);
     asm volatile("" : "+v"(orow));
     if (p_lds) {  // s_j < klim_j for every band: inside its LDS row
+        if (lazy) band_f(b, d2, r.f);
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
         const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
@@ -456,6 +468,7 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
         for (int j = 0; j < 4; ++j) r.f[j] = t;
     }
     if (p_own) {
+        if (lazy) band_f(b, d2, r.f);
         uint32_t otp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

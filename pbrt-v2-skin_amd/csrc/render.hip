@@ -1112,6 +1112,44 @@ template __global__ void direct_combine_kernel<true>(RenderScene, SampleRecs, in
 // wave-uniform (its tables are scalar loads), the lane's Ld row and the band-ordered Mo() values
 // are all issued up front, and the 30-band loop is unrolled -- the same float operations, in the
 // same order, as the general path below.
+// Pow(FromRGB(rgb), e) for all 30 bands of a textured albedo, the branches of refl_band (FromRGB,
+// spectrum.cpp:103-187) decided once per lane instead of per band: the minimum / middle / maximum
+// components and the rows of their secondary (X: Cyan, Magenta, Yellow) and primary (Y: Red, Green,
+// Blue) spectra; then per band the same products and sums in the same order. e = 0.5 (the default mix)
+// as sqrtf (tex_albedo_pow).
+__device__ __forceinline__ void tex_albedo_pow_all(const float4 rgb, float e, float out[NB]) {
+    const float R = rgb.x, G = rgb.y, B = rgb.z;
+    float mn, md, mx;
+    int xi, yi;
+    if (R <= G && R <= B) {
+        mn = R;
+        xi = 1;
+        if (G <= B) { md = G; mx = B; yi = 6; } else { md = B; mx = G; yi = 5; }
+    } else if (G <= R && G <= B) {
+        mn = G;
+        xi = 2;
+        if (R <= B) { md = R; mx = B; yi = 6; } else { md = B; mx = R; yi = 4; }
+    } else {
+        mn = B;
+        xi = 3;
+        if (R <= G) { md = R; mx = G; yi = 5; } else { md = G; mx = R; yi = 4; }
+    }
+    const float d1 = md - mn, d2 = mx - md;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+        const float X = xi == 1 ? kRefl[1][c] : (xi == 2 ? kRefl[2][c] : kRefl[3][c]);
+        const float Y = yi == 4 ? kRefl[4][c] : (yi == 5 ? kRefl[5][c] : kRefl[6][c]);
+        float r = 0.f;
+        r += kRefl[0][c] * mn;
+        r += X * d1;
+        r += Y * d2;
+        float v = r * .94f;
+        v = v < 0.f ? 0.f : v;
+        out[c] = e == 0.5f ? __builtin_sqrtf(v) : tex_pow_general(v, e);
+    }
+}
+
+template <bool TEX>
 __device__ __forceinline__ void assemble_uniform(const RenderScene &sc, const SampleRecs &rec, int slot, int mid) {
     const RenderMaterial &mat = sc.materials[mid];
     const float4 q = rec.hit_q[slot];
@@ -1130,12 +1168,19 @@ __device__ __forceinline__ void assemble_uniform(const RenderScene &sc, const Sa
     }
 #pragma unroll
     for (int c = 0; c < NB; ++c) m[c] = mo[mat.band_pos[c]];
+    float ab[NB];
+    if (TEX) {  // the hit's albedo texture value (shade_tex_kernel): Pow(albedo, 1 - mix) per lane
+        tex_albedo_pow_all(rec.hit_alb[slot], 1.f - mat.mix, ab);
+    } else {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) ab[c] = mat.alb_1mmix[c];
+    }
     float X = 0.f, Y = 0.f, Z = 0.f;
     bool nan = false;
 #pragma unroll
     for (int c = 0; c < NB; ++c) {
         float L = 0.f;
-        float t = (kss * m[c]) * mat.alb_1mmix[c];
+        float t = (kss * m[c]) * ab[c];
         t = t < 0.f ? 0.f : t;  // Spectrum::Clamp(0, INFINITY)
         L += t;
         L += ld[c];
@@ -1161,10 +1206,15 @@ __global__ __launch_bounds__(256) void assemble_kernel(RenderScene sc, SampleRec
         const uint32_t hs0 = in ? rec.hit_s[slot] : 0u;
         const int mid = (int)((hs0 >> REC_MAT_SHIFT) & 0xffu);
         const int mid0 = __builtin_amdgcn_readfirstlane(mid);
-        // SSS hit (bit 31, not a light) of material mid0, without an albedo texture
+        // SSS hit (bit 31, not a light) of material mid0 (with or without an albedo texture)
         const bool fast = in && (hs0 >> 31) && mid == mid0;
-        if (__builtin_amdgcn_ballot_w64(in && !fast) == 0 && !sc.materials[mid0].has_alb_tex) {
-            if (in) assemble_uniform(sc, rec, slot, mid0);
+        if (__builtin_amdgcn_ballot_w64(in && !fast) == 0) {
+            if (in) {
+                if (sc.materials[mid0].has_alb_tex)
+                    assemble_uniform<true>(sc, rec, slot, mid0);
+                else
+                    assemble_uniform<false>(sc, rec, slot, mid0);
+            }
             return;
         }
     }

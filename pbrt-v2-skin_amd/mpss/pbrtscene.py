@@ -8,7 +8,9 @@ for the directives scenes/skin.pbrt and its relatives contain:
   Sampler (pixelsamples), SurfaceIntegrator "multipolesubsurface" (maxdepth, maxerror,
   minsampledistance, mix, showirradiancepoints, incenter), WorldBegin/WorldEnd,
   AttributeBegin/End, TransformBegin/End, Translate, Rotate, Scale, Identity,
-  Texture "constant" / "imagemap" (albedo, bumpmap), Material "layeredskin", AreaLightSource "area", LightSource "infinite"
+  Texture "constant" / "imagemap" (albedo, bumpmap), Material "layeredskin" (every parameter of
+  CreateLayeredSkinMaterial, layeredskin.cpp:222-262, incl. genprofile / showirradiancepoints /
+  irradiancepointsize / rgbprofile / usemontecarlo), AreaLightSource "area", LightSource "infinite"
   (L, scale, nsamples, mapname: .exr / .pfm / .tga via mpss.imageio), Shape "sphere" (as an area light only) and Shape "trianglemesh" (inline arrays, or "string npzfile" -- this
   package's stand-in for huge inline arrays, see tools/make_scene.py), Include.
 
