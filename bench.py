@@ -40,11 +40,20 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # query-record, as the reference reads them once). Re-reads the sharding adds are not counted.
 REC_HDR_BYTES = 16
 REF_RECORD_BYTES = 12 + 4 + 4 * 30  # position, area / sumArea, 30-band E / Et
-# The gather's real ceiling: L2 requests of per-lane 8-byte table gathers (64 lanes on 64 distinct lines
-# per instruction), the best rate any load form sustains on MI355X: tools/microbench/l2_policy.hip,
-# profiles/r03_l2_policy.json (2.69e11 lane loads/s; round 2's l2_gather.hip, with hash arithmetic per
-# load, reached 2.46e11).
-L2_GATHER_CEILING_REQ_S = 2.69e11
+# The L2 request ceiling of the gather's far lookups in the common grid's shape: one group row = two
+# 16-byte loads from one 32-byte sector per lane, 64 distinct lines per instruction (the second load of a
+# sector hits the vector L1): tools/microbench/l2_width.hip, profiles/r05a_l2_width.json (2.48e11 lane
+# lookups/s, 158.6 CU cycles per 64 lane lookups; per-lane 8-byte gathers: 2.53e11, and 2.69e11 in
+# their best load form, profiles/r03_l2_policy.json).
+L2_GATHER_CEILING_REQ_S = 2.48e11
+# The gather's binding resource since the common grid (round 4): VALU issue. Its ceiling is measured, not
+# assumed: tools/microbench/valu_issue.hip runs the record loop's instruction mix (with its SALU) at the
+# gather's occupancy (two 1024-thread workgroups per CU, 8 waves per SIMD) and reports wave64 VALU
+# instructions per second over the chip. Plain f32 add / mul / fma issue every ~2.3 cycles per SIMD there,
+# packed f32, conversions, compares, selects and integer shifts every ~4.2, v_rcp every ~8.2
+# (profiles/r05c_valu_issue.json), so the ceiling is the mix's, not a per-instruction constant.
+VALU_CEILING_JSON = "profiles/r05c_valu_issue.json"
+VALU_CEILING_VARIANT = "gather mix (VALU + SALU)"
 # sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
 KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
                   "pbrt-v2-skin_amd/csrc/mo_wave.h", "pbrt-v2-skin_amd/csrc/octree.h")
@@ -320,9 +329,9 @@ def main(a):
     roofline = {"kernel": "mo_sort_kernel + mo_band_wave_kernel (Mo gather, spectrally sharded, wave queue)",
                 "bound": "l2_requests", "achieved": None, "peak": L2_GATHER_CEILING_REQ_S / 1e9, "unit": "Greq/s",
                 "frac": None, "traffic": None, "avg_launch_ms": round(shade_launch_ms, 4),
-                "peak_source": "tools/microbench/l2_policy.hip: per-lane 8-byte gathers from a per-XCD-resident "
-                               "table, 64 distinct lines per instruction, best load form "
-                               "(profiles/r03_l2_policy.json)",
+                "peak_source": "tools/microbench/l2_width.hip: per-lane group-row lookups (two 16-byte loads from "
+                               "one 32-byte sector) from a per-XCD-resident table, 64 distinct lines per "
+                               "instruction (profiles/r05a_l2_width.json)",
                 "algorithmic": {"achieved_gbs": round(mo_gbs, 1), "peak_gbs": HBM_PEAK_GBS,
                                 "frac": round(mo_gbs / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": mo_bytes_step / launches_per_step,
@@ -345,8 +354,6 @@ def main(a):
             roofline["l2_requests_per_sss_sample"] = round(l2["requests_per_launch"] * launches_per_step /
                                                            max(1, cnt["sss_samples"]), 1)
             roofline["l2_hit_rate"] = l2["hit_rate"]
-        if "valu" in pt:  # the other resource the gather can run out of
-            roofline["valu_issue_frac"] = round(pt["valu"]["issue_frac"], 4)
         if roofline["traffic"] is not None:
             roofline["hbm_gbs"] = round(roofline["traffic"] / (shade_launch_ms * 1e-3) / 1e9, 1)
             roofline["hbm_frac"] = round(roofline["hbm_gbs"] / HBM_PEAK_GBS, 4)
@@ -430,22 +437,50 @@ def c3_strong_secondary(a, rank, world, local):
                           "tiles": len(tiles), "deal_balance": round(balance, 4), "scaling": "strong"}}
 
 
+def valu_ceiling():
+    """(wave64 VALU instructions / s over the chip, shader clock GHz, source) of the gather's record mix
+    at 8 waves per SIMD, from the committed microbenchmark run (VALU_CEILING_JSON), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, VALU_CEILING_JSON)))
+    except (OSError, ValueError):
+        return None
+    for r in d.get("results", []):
+        if r.get("variant") == VALU_CEILING_VARIANT and r.get("waves_per_simd") == 8:
+            return (r["valu_wave_insts_per_s"], r.get("clock_ghz"),
+                    "%s, variant \"%s\" at 8 waves per SIMD: %.4g wave64 VALU/s (%.2f SIMD cycles per instruction "
+                    "at %.2f GHz)" % (VALU_CEILING_JSON, VALU_CEILING_VARIANT, r["valu_wave_insts_per_s"],
+                                      r["simd_cycles_per_valu_inst"], r.get("clock_ghz") or 0.0))
+    return None
+
+
 def headline_bound(roofline, pt, launch_ms):
     """The headline names the resource that binds the gather: the L2 request rate of its lookups
-    (rounds 2-3), or VALU issue once the common grid cut the lookups (round 4: 0.92 of issue vs 0.74
-    of the request ceiling). The other figure stays beside it."""
+    (rounds 2-3), or VALU issue once the common grid cut the lookups (round 4 on). The VALU peak is the
+    measured issue rate of the record loop's instruction mix at the kernel's occupancy (valu_ceiling),
+    cross-checked by the counters' own VALU busy fraction (SQ_ACTIVE_INST_VALU over SQ_BUSY_CU_CYCLES:
+    the SIMDs' cycles with a VALU instruction in flight, from the same PMC summary). The L2 request
+    figure stays beside it."""
     v = pt.get("valu") if pt else None
-    if not v or roofline.get("frac") is None or launch_ms <= 0 or v["issue_frac"] <= roofline["frac"]:
+    ceil = valu_ceiling()
+    if not v or not ceil or launch_ms <= 0:
         return
-    roofline["l2_requests"] = {"achieved": roofline["achieved"], "peak": roofline["peak"], "unit": "Greq/s",
-                               "frac": roofline["frac"], "peak_source": roofline.get("peak_source")}
+    achieved = v["insts_per_launch"] / (launch_ms * 1e-3)
+    frac = achieved / ceil[0]
+    if roofline.get("frac") is not None and frac <= roofline["frac"]:
+        return
+    if roofline.get("achieved") is not None:
+        roofline["l2_requests"] = {"achieved": roofline["achieved"], "peak": roofline["peak"], "unit": "Greq/s",
+                                   "frac": roofline["frac"], "peak_source": roofline.get("peak_source")}
     roofline["bound"] = "valu_issue"
-    roofline["achieved"] = round(v["insts_per_launch"] / (launch_ms * 1e-3) / 1e9, 1)
-    roofline["peak"] = round(1024 * 2.4 / 4, 1)
+    roofline["achieved"] = round(achieved / 1e9, 1)
+    roofline["peak"] = round(ceil[0] / 1e9, 1)
     roofline["unit"] = "G wave64 VALU instructions/s"
-    roofline["frac"] = round(v["issue_frac"], 4)
-    roofline["peak_source"] = ("MI355X: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at "
-                               "2.4 GHz; SQ_INSTS_VALU per launch from the committed PMC summary")
+    roofline["frac"] = round(frac, 4)
+    roofline["peak_source"] = ceil[2] + "; achieved = SQ_INSTS_VALU per launch (committed PMC summary) / this run's launch time"
+    if "busy" in v:
+        roofline["valu_busy_pmc"] = round(v["busy"], 4)
+        roofline["valu_busy_source"] = ("SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES per launch (quad-cycles with a VALU "
+                                        "instruction in flight per SIMD over the CUs' busy cycles / 4 SIMDs x 4)")
 
 
 def pmc_traffic(path, launch_ms, config):
@@ -483,10 +518,13 @@ def pmc_traffic(path, launch_ms, config):
     out = {"traffic": e["fetch_bytes_corrected_mean"],
            "source": os.path.relpath(f, ROOT) + " (FETCH_SIZE x 2 per launch, includes Infinity-Cache hits)"}
     if "SQ_INSTS_VALU" in e and launch_ms > 0:
-        # VALU issue: wave64 instructions per launch over what 256 CUs x 4 SIMDs issue in the launch
-        # (one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz)
+        # VALU issue: wave64 instructions per launch (against the measured mix ceiling: headline_bound)
         v = e["SQ_INSTS_VALU"]["mean"]
-        out["valu"] = {"insts_per_launch": v, "issue_frac": v / (launch_ms * 1e-3 * 2.4e9 * 1024 / 4)}
+        out["valu"] = {"insts_per_launch": v}
+        if "SQ_ACTIVE_INST_VALU" in e and e.get("SQ_BUSY_CU_CYCLES", {}).get("mean"):
+            # quad-cycles with a VALU instruction in flight, summed over waves (per SIMD), over the CUs'
+            # busy cycles: 4 SIMDs x quad-cycles / (4 x cycles) -> the fraction of SIMD cycles
+            out["valu"]["busy"] = e["SQ_ACTIVE_INST_VALU"]["mean"] / e["SQ_BUSY_CU_CYCLES"]["mean"]
     if "TCP_TCC_READ_REQ_sum" in e and launch_ms > 0:
         req = e["TCP_TCC_READ_REQ_sum"]["mean"]
         out["l2"] = {"requests_per_launch": req, "achieved_req_per_s": req / (launch_ms * 1e-3),

@@ -55,17 +55,19 @@ enum {
     V_MUL,      // v_mul_f32
     V_MAX3,     // v_max3_f32
     V_RCP,      // v_rcp_f32
+    V_MIX5,     // the round-5 fused record (one group-row lookup + one LDS lookup), VALU + SALU
     V_COUNT
 };
 static const char *kNames[V_COUNT] = {"v_fma_f32",      "v_add_f32",    "v_pk_mul_f32",   "v_pk_add_f32",
                                       "v_pk_fma_f32",   "v_cvt_u32_f32", "v_fract_f32",   "v_cndmask_b32",
                                       "v_lshl_add_u32", "gather mix (VALU)", "gather mix (VALU + SALU)",
                                       "v_add_u32",      "v_min_u32",    "v_min_f32",      "v_mov_b32",
-                                      "v_cmp_gt_f32 (e64)", "v_mul_f32", "v_max3_f32",   "v_rcp_f32"};
+                                      "v_cmp_gt_f32 (e64)", "v_mul_f32", "v_max3_f32",   "v_rcp_f32",
+                                      "gather mix r05 (fused: row + LDS record, VALU + SALU)"};
 // wave64 VALU instructions per loop step, and SALU
 static const int kValu[V_COUNT] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 94, 94,  // mix: 2 records x 47
-                                   32, 32, 32, 32, 32, 32, 32, 32};
-static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48, 0, 0, 0, 0, 0, 0, 0, 0};
+                                   32, 32, 32, 32, 32, 32, 32, 32, 64};
+static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48, 0, 0, 0, 0, 0, 0, 0, 0, 24};
 
 #define R8(X) X X X X X X X X
 #define R4(X) X X X X
@@ -202,6 +204,53 @@ __device__ __forceinline__ void step_mix(float (&a)[8], f2v (&p)[8], float x, f2
     }
 }
 
+// The round-5 fused common-grid record (mo_band.h cg_fetch / cg_combine with MPSS_MO_FUSED, TPATH,
+// LAZYF; counted from the hipcc -S of mo_wave_cg.hip): a group-row record -- d2 (4 plain + 2 packed),
+// u, its cvt, the LDS-path compare, the row offset, the two path compares, fract(u) and three moves,
+// the lerp (4 sub + 4 fma), the tau compare, two packed FMAs (27 VALU) -- and an LDS record -- the same
+// head, then 2 packed muls, 4 cvt, 4 LDS addresses, 4 fract, the compares, lerp, tau, products (37
+// VALU); with the exec-mask SALU of the three path steps (12 per record).
+__device__ __forceinline__ void step_mix5(float (&a)[8], f2v (&p)[8], float x, f2v xv, uint32_t &s0, uint32_t &s1) {
+    float &d = a[0], &u = a[1], &t = a[2], &w = a[3], &e = a[4], &g = a[5], &h = a[6], &k = a[7];
+    f2v &pa = p[0], &pb = p[1], &pc = p[2], &pd = p[3];
+    uint64_t m;
+#pragma unroll
+    for (int rec = 0; rec < 2; ++rec) {
+        asm volatile("v_subrev_f32 %0, %1, %0" : "+v"(d) : "v"(x));
+        asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(pa) : "v"(xv));
+        asm volatile("v_mul_f32 %0, %0, %0" : "+v"(d));
+        asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(pa));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        asm volatile("v_mul_f32 %0, %1, %0" : "+v"(u) : "v"(x));
+        asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(w));
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_add_lshl_u32 %0, %0, %1, 5" : "+v"(w) : "v"(x));
+        asm volatile("v_cmp_le_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        if (rec == 0) {  // group rows
+            asm volatile("v_fract_f32 %0, %0" : "+v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(e) : "v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(g) : "v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(h) : "v"(t));
+        } else {  // LDS
+            asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pb) : "v"(xv));
+            asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pc) : "v"(xv));
+            R4(asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(k));)
+            R4(asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(k) : "v"(x));)
+            R4(asm volatile("v_fract_f32 %0, %0" : "+v"(t));)
+        }
+        R4(asm volatile("v_sub_f32 %0, %0, %1" : "+v"(e) : "v"(x));)
+        R4(asm volatile("v_fma_f32 %0, %1, %0, %2" : "+v"(g) : "v"(t), "v"(x));)
+        asm volatile("v_cmp_ge_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(d));
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(pd) : "v"(pb), "v"(xv));
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(pa) : "v"(pc), "v"(xv));
+        R4(asm volatile("s_add_u32 %0, %0, 32\n s_addc_u32 %1, %1, 0" : "+s"(s0), "+s"(s1) ::"scc");)
+        R4(asm volatile("s_mov_b32 %0, %1\n s_or_b32 %1, %1, %0" : "+s"(s0), "+s"(s1) ::"scc");)
+        R4(asm volatile("s_cmp_ge_i32 %0, %1\n s_cselect_b32 %0, %0, %1" : "+s"(s0) : "s"(s1) : "scc");)
+    }
+}
+
 template <int V>
 __global__ __launch_bounds__(1024) void issue_kernel(int steps, float *out, unsigned long long *span) {
     const float x = 1.0f + threadIdx.x * 1e-7f, y = 1e-3f;
@@ -223,6 +272,8 @@ __global__ __launch_bounds__(1024) void issue_kernel(int steps, float *out, unsi
             step_mix<false>(a, p, x, xv, s0, s1);
         else if (V == V_MIXS)
             step_mix<true>(a, p, x, xv, s0, s1);
+        else if (V == V_MIX5)
+            step_mix5(a, p, x, xv, s0, s1);
         else
             step<V>(a, x, y);
     }
@@ -266,7 +317,7 @@ int main(int argc, char **argv) {
     void (*fn[V_COUNT])(int, int, size_t, int, float *, unsigned long long *) = {
         launch<0>,  launch<1>,  launch<2>,  launch<3>,  launch<4>,  launch<5>,  launch<6>,
         launch<7>,  launch<8>,  launch<9>,  launch<10>, launch<11>, launch<12>, launch<13>,
-        launch<14>, launch<15>, launch<16>, launch<17>, launch<18>};
+        launch<14>, launch<15>, launch<16>, launch<17>, launch<18>, launch<19>};
     const int ws[4] = {1, 2, 4, 8};
     printf("{\"cus\": %d, \"clock_khz\": %d, \"steps\": %d, \"results\": [\n", cus, prop.clockRate, steps);
     bool first = true;
