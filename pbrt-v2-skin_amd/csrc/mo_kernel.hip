@@ -531,6 +531,11 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
+// (MPSS_CG_MAX_ROWS overrides the cap: the row-cap experiments of tools/x_ab_val.sh)
+static int cg_max_rows() {
+    const char *e = getenv("MPSS_CG_MAX_ROWS");
+    return e && atoi(e) > 0 ? atoi(e) : kCgMaxRows;
+}
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field,
@@ -666,7 +671,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             double from = u0f;  // the current stretch's first servable u
             for (const double ub : bad) {
                 if (ub >= from) {
-                    const double len = std::min(std::floor(ub) - 1.0, from + (double)kCgMaxRows) - from;
+                    const double len = std::min(std::floor(ub) - 1.0, from + (double)cg_max_rows()) - from;
                     if (len > best) {
                         best = len;
                         start = from;
@@ -697,7 +702,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         }
         const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
         int64_t u1 = (int64_t)std::floor(ubad) - 1;
-        u1 = std::min<int64_t>(u1, ubase + kCgMaxRows);
+        u1 = std::min<int64_t>(u1, ubase + cg_max_rows());
         u1 = std::min<int64_t>(u1, (int64_t)L - 1);
         cg.ubase[g] = (uint32_t)ubase;
         if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
