@@ -111,7 +111,8 @@ def parse(argv=None):
                     help="mpss_config.mo_near_field (default: the library's)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the C3 strong-scaling figure at N > 1")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary figures (C3 strong scaling at N > 1; the reference-sampler C2 frame at N = 1)")
     ap.add_argument("--out", default=None, help="write rank 0's first frame as .pfm/.exr")
     ap.add_argument("--pmc-json", default=None,
                     help="rocprofv3 PMC summary (tools/summarize_prof.py) of this bench command; default: the "
@@ -362,6 +363,8 @@ def main(a):
     secondary = None
     if world > 1 and a.config == "c2" and not a.no_secondary:
         secondary = c3_strong_secondary(a, rank, world, local)
+    if world == 1 and a.config == "c2" and a.sampler == "hash" and not a.no_secondary:
+        secondary = reference_sampler_secondary(a, local)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -451,6 +454,31 @@ def valu_ceiling():
                     "at %.2f GHz)" % (VALU_CEILING_JSON, VALU_CEILING_VARIANT, r["valu_wave_insts_per_s"],
                                       r["simd_cycles_per_valu_inst"], r.get("clock_ghz") or 0.0))
     return None
+
+
+def reference_sampler_secondary(a, local):
+    """The same C2 frame with pbrt's own sampler replayed (mpss_config.sampler = MPSS_SAMPLER_REFERENCE,
+    --replay-cores emulated cores: SamplerRendererTask's per-task MT19937 streams, samplerrenderer.cpp:
+    60-167), timed like the headline: the replay window's generation (replay_window_kernel) is inside every
+    step. This is the mode whose output is pbrt's own, sample for sample."""
+    import argparse
+    b = argparse.Namespace(**vars(a))
+    b.sampler = "reference"
+    sc, ctx, _, _, _, _, _ = build_scene(b, "c2", local)
+    T = a.tile
+    tiles, items_by_rank, _, _ = deal(ctx, sc, T, 1, 1)
+    steps = max(1, min(a.steps, 5))
+    ctx.set_instrumentation(kernel_timing=True, count_traversal=False)
+    dt, _, _ = timed_steps(b, ctx, sc, tiles, items_by_rank, 1, T, 0, 1, steps, 1)
+    st = ctx.render_stats()
+    ctx.close()
+    return {"reference_sampler": {
+        "value": round(sc.xres * sc.yres * sc.spp * steps / dt / 1e6, 3), "unit": "Msamples/s",
+        "ms_per_step": round(dt / steps * 1e3, 3), "replay_cores": a.replay_cores,
+        "kernel_ms_per_step": {"replay": round(st["ms_replay"] / steps, 3), "mo_band": round(st["ms_shade"] / steps, 3),
+                               "primary": round(st["ms_camera"] / steps, 3),
+                               "shade_direct": round(st["ms_direct"] / steps, 3), "film": round(st["ms_film"] / steps, 3)},
+        "note": "C2 with pbrt's per-task MT19937 sample streams replayed (the window generation timed in every step)"}}
 
 
 def headline_bound(roofline, pt, launch_ms):

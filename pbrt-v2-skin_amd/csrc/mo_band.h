@@ -345,6 +345,32 @@ __device__ __forceinline__ void from_rgb4(lds_float *rk, float R, float G, float
     }
 }
 
+// from_rgb4 for the common-grid gather (MPSS_MO_FUSED): rk holds the weights times .94, the LDS offsets of
+// the X and Y rows come from two selects each, and each band is .94 W min + .94 X (mid - min) + .94 Y
+// (max - mid) as one multiply and two FMAs (packed, two bands per instruction), clamped at 0 -- within an
+// ulp or two of FromRGB's own sum (the far values are a resampling already).
+__device__ __forceinline__ void from_rgb4_fused(lds_float *rk, float R, float G, float B, float o[4]) {
+    const float mn = __builtin_fminf(R, __builtin_fminf(G, B));
+    const float mx = __builtin_fmaxf(R, __builtin_fmaxf(G, B));
+    const float md = __builtin_amdgcn_fmed3f(R, G, B);
+    const uint32_t ox = R == mn ? 4u : (G == mn ? 8u : 12u);   // X: Cyan, Magenta, Yellow
+    const uint32_t oy = R == mx ? 16u : (G == mx ? 20u : 24u);  // Y: Red, Green, Blue
+    typedef __attribute__((address_space(3))) const f4v lds_f4v;
+    const f4v w = *(lds_f4v *)rk, x = *(lds_f4v *)(rk + ox), y = *(lds_f4v *)(rk + oy);
+    const float d1 = md - mn, d2 = mx - md;
+    const f2v wv[2] = {f2v{w.x, w.y}, f2v{w.z, w.w}};
+    const f2v xv[2] = {f2v{x.x, x.y}, f2v{x.z, x.w}};
+    const f2v yv[2] = {f2v{y.x, y.y}, f2v{y.z, y.w}};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        f2v r = wv[h] * f2v{mn, mn};
+        r = __builtin_elementwise_fma(xv[h], f2v{d1, d1}, r);
+        r = __builtin_elementwise_fma(yv[h], f2v{d2, d2}, r);
+        o[2 * h] = __builtin_fmaxf(r.x, 0.f);
+        o[2 * h + 1] = __builtin_fmaxf(r.y, 0.f);
+    }
+}
+
 // The combine half: lerp, the Mo() products and the running sums (one point or node). RGB: the
 // slots hold the R, G, B lookups, and the group's output bands take FromRGB (rk: their weights).
 template <bool POINT, bool RGB = false>
@@ -539,8 +565,13 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
         for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
     }
     float o[4];
-    if (RGB)  // slots 0..2: the R, G, B profiles on the grid
+    if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
+#if MPSS_MO_FUSED
+        from_rgb4_fused(rk, rd[0], rd[1], rd[2], o);
+#else
         from_rgb4(rk, rd[0], rd[1], rd[2], o);
+#endif
+    }
     const float *x = RGB ? o : rd;
 #if MPSS_MO_FUSED
     (void)w;
@@ -561,15 +592,27 @@ __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, 
     band_rd_combine<POINT, RGB>(f, v, e, w, acc, rk);
 }
 
-// sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d)
-// (v_rcp_f32, <= 1 ulp; product <= ~2.5 ulp) is trusted when it clears max_error by 2^-20
-// relative either way; the rare near-ties (and NaN/inf) take the exact division, so the decision
-// is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
-__device__ __forceinline__ bool dw_below(float a, float d, float m) {
+// sum_area / d2 < max_error decided without an IEEE division in the common case. MPSS_MO_DWMUL (default):
+// a against the products d * m (1 -+ 2^-20) (two plain multiplies; m_lo, m_hi wave-uniform): a < fl(d m_lo)
+// puts the true quotient below m (1 - 2^-21), so fl(a / d) < m; a > fl(d m_hi) puts it above m (1 + 2^-21).
+// Otherwise: a * rcp(d) (v_rcp_f32, <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20
+// relative either way. The rare near-ties (and NaN / inf) take the exact division, so the decision is
+// always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
+#ifndef MPSS_MO_DWMUL
+#define MPSS_MO_DWMUL 1
+#endif
+__device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, float m_hi) {
+#if MPSS_MO_DWMUL
+    bool below = a < d * m_lo;
+    const bool sure = below || a > d * m_hi;
+#else
+    (void)m_lo;
+    (void)m_hi;
     const float r = a * __builtin_amdgcn_rcpf(d);
     const float lo = m * (1.f - 0x1p-20f), hi = m * (1.f + 0x1p-20f);
     bool below = r < lo;
     const bool sure = below || r > hi;
+#endif
     if (!sure) below = (a / d) < m;
     return below;
 }
@@ -633,6 +676,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     const cptr<NodeHdr> nodes = as_const(a.nodes);
     const cptr<float4> pt_hdr = as_const(a.pt_hdr);
     int resume = valid ? 0 : 0x7fffffff;
+    const float m_lo = a.max_error * (1.f - 0x1p-20f), m_hi = a.max_error * (1.f + 0x1p-20f);  // (dw_below)
     int node = 0;
     while (node < a.n_nodes) {
         node = __builtin_amdgcn_readfirstlane(node);
@@ -660,7 +704,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 const float d2 = dx * dx + dy * dy + dz * dz;
                 // nodeBound.Inside(p) <=> every per-axis distance is 0 (the subtractions' signs are exact)
                 const bool inside = fmaxf(fmaxf(bx, by), bz) == 0.f;
-                if (dw_below(h.sum_area, d2, a.max_error) && !inside) {
+                if (dw_below(h.sum_area, d2, a.max_error, m_lo, m_hi) && !inside) {
                     resume = skip;
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};

@@ -118,7 +118,8 @@ void mo_band_wave_kernel(BandArgs a) {
             lt[i] = (c >= 0 && k <= kmax) ? a.t.table[(size_t)c * a.t.L + k] : 0.f;
         }
     }
-    if (RGB && tid < 28) lt[4 * ROWF - 28 + tid] = (&a.t.rgb_k[grp].w[0])[tid];
+    // (the common-grid gather's fused FromRGB takes the weights with FromRGB's .94 folded in: from_rgb4_fused)
+    if (RGB && tid < 28) lt[4 * ROWF - 28 + tid] = (&a.t.rgb_k[grp].w[0])[tid] * ((CG && MPSS_MO_FUSED) ? .94f : 1.f);
     __syncthreads();  // the near field is read-only from here on
     for (;;) {
         int u = 0;

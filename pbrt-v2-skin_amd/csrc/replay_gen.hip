@@ -27,6 +27,20 @@ namespace mpss {
 
 namespace {
 
+// MPSS_REPLAY_PROFILE (a diagnostic build only): each wave accumulates its shader-clock cycles per
+// section of the pixel loop and prints them for a sample of tasks (where a C2 task's time goes).
+#ifdef MPSS_REPLAY_PROFILE
+__device__ __forceinline__ uint64_t rp_clock() { return __builtin_readcyclecounter(); }
+#define RP_MARK(k)                         \
+    do {                                   \
+        const uint64_t t_ = rp_clock();    \
+        rp_acc[k] += t_ - rp_t;            \
+        rp_t = t_;                         \
+    } while (0)
+#else
+#define RP_MARK(k) (void)0
+#endif
+
 constexpr int kMaxWaves = 4;  // waves per workgroup (fewer when a wave's LDS needs more room)
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
@@ -198,6 +212,11 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
     }
     const V3 cam_o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
     const int64_t npix = (int64_t)g.w * g.h;
+#ifdef MPSS_REPLAY_PROFILE
+    uint64_t rp_acc[6] = {0, 0, 0, 0, 0, 0}, rp_t = rp_clock();
+    const uint64_t rp_t0 = rp_t;
+    int rp_hits = 0, rp_pix = 0;
+#endif
     for (; ord <= last; ++ord) {
         const int x = x0 + ord % tw, y = y0 + ord / tw;
         const bool keep = x >= g.x0 && x < g.x0 + g.w && y >= g.y0 && y < g.y0 + g.h;
@@ -223,6 +242,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             const ReplayArray A = array(a);
             mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
+        RP_MARK(0);
         // each sample's own shuffle (lane per sample) and every block shuffle's partners
         shuffle_partners(dimg, idx0, spp);
         for (int a = 0; a < na; ++a) {
@@ -241,6 +261,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             shuffle_partners(A.d + A.hdr + spp * A.n, A.idx, spp);
         }
         wave_sync();
+        RP_MARK(1);
         // the block shuffles side by side: the image's swaps on lane 0, array a's on lane 1 + a % 63
         // (lanes 1..63 take arrays a, a + 63, ... in turn: any light count)
         if (lane == 0) {
@@ -252,6 +273,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             }
         }
         wave_sync();
+        RP_MARK(2);
         // the image samples and the camera rays (samplerrenderer.cpp:97-103): only whether they hit
         int hits = 0;
         for (int c = 0; c < spp; c += 64) {
@@ -270,6 +292,7 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
                 hits += __popcll(__ballot(hit && i < spp));
             }
         }
+        RP_MARK(3);
         if (keep)
             for (int a = 0; a < na; ++a) {
                 const ReplayArray A = array(a);
@@ -285,8 +308,23 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
                 }
             }
         wave_sync();
+        RP_MARK(4);
         mt.skip((int64_t)g.li_draws * hits);  // Li, per camera ray that hits
+        RP_MARK(5);
+#ifdef MPSS_REPLAY_PROFILE
+        rp_hits += hits;
+        ++rp_pix;
+#endif
     }
+#ifdef MPSS_REPLAY_PROFILE
+    const uint64_t rp_tot = rp_clock() - rp_t0;
+    if (lane == 0 && (task % 97 == 0 || rp_tot > 20000000ull))
+        printf("replay task %d: pixels %d hits %d total %llu | draws %llu own+partners %llu swaps %llu image+trace %llu "
+               "values %llu li-skip %llu\n",
+               task, rp_pix, rp_hits, (unsigned long long)rp_tot, (unsigned long long)rp_acc[0],
+               (unsigned long long)rp_acc[1], (unsigned long long)rp_acc[2], (unsigned long long)rp_acc[3],
+               (unsigned long long)rp_acc[4], (unsigned long long)rp_acc[5]);
+#endif
     for (int k = lane; k < 624; k += 64) gst[k] = mt.st[k];
     if (lane == 0) {
         g.cur.cur_pix[task] = last + 1;

@@ -25,7 +25,7 @@ for r in $(seq 1 $ROUNDS); do
       timeout -k 10 300 python -u tools/bench_mc.py --cpu-seconds 0 > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
       python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["seconds"], d["total_r"], d["total_t"])' $log $v$r | tee -a $out
     else
-      timeout -k 10 600 python -u bench.py --config $CFG "${steps[@]}" --no-cpu-baseline > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
+      timeout -k 10 600 python -u bench.py --config $CFG "${steps[@]}" --no-cpu-baseline --no-secondary > $log 2>&1 || { echo "run $v$r failed"; tail -20 $log; cp ab/libmpss_orig.so $lib; exit 1; }
       python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["roofline"]["kernel_ms_per_step"])' $log $v$r | tee -a $out
     fi
   done

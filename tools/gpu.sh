@@ -51,7 +51,7 @@ for step in "$@"; do
       cfg=${arg:-c2}
       log=gpurun_out/${TAG}_bench_${cfg}.log
       extra=(--steps 5 --warmup 1)
-      [ $name = quick ] && extra=(--steps 3 --warmup 1 --no-cpu-baseline)
+      [ $name = quick ] && extra=(--steps 3 --warmup 1 --no-cpu-baseline --no-secondary)
       [ $cfg = c5 ] && extra=(--steps 1 --warmup 1 --no-cpu-baseline)
       echo "== $name $cfg"
       timeout -k 10 600 python -u bench.py --config $cfg "${extra[@]}" > $log 2>&1 || fail bench $log
@@ -74,7 +74,7 @@ for step in "$@"; do
       steps=(--steps 3 --warmup 1)
       [ $cfg = c5 ] && steps=(--steps 1 --warmup 1)
       echo "== kernel trace $cfg"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/kt -o run --output-format csv -- python3 bench.py --config $cfg "${steps[@]}" --no-cpu-baseline $BENCH_ARGS > $d/kt.log 2>&1 || fail kt $d/kt.log 30
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d/kt -o run --output-format csv -- python3 bench.py --config $cfg "${steps[@]}" --no-cpu-baseline --no-secondary $BENCH_ARGS > $d/kt.log 2>&1 || fail kt $d/kt.log 30
       grep '"metric"' $d/kt.log > $d/kt_bench.jsonl || true ;;
     pmc)
       cfg=${arg:-c2}
@@ -85,7 +85,7 @@ for step in "$@"; do
         [ -z "$line" ] && continue
         i=$((i+1))
         echo "== pmc $cfg $i: $line"
-        timeout -s KILL 300 rocprofv3 --pmc $line -d $d/pmc_$i -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline $BENCH_ARGS > $d/pmc_$i.log 2>&1 || fail "pmc pass $i" $d/pmc_$i.log 20
+        timeout -s KILL 300 rocprofv3 --pmc $line -d $d/pmc_$i -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline --no-secondary $BENCH_ARGS > $d/pmc_$i.log 2>&1 || fail "pmc pass $i" $d/pmc_$i.log 20
       done <<< "${PMC_SETS:-$DEFAULT_PMC}" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
