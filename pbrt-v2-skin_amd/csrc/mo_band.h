@@ -592,14 +592,14 @@ __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, 
     band_rd_combine<POINT, RGB>(f, v, e, w, acc, rk);
 }
 
-// sum_area / d2 < max_error decided without an IEEE division in the common case. MPSS_MO_DWMUL (default):
-// a against the products d * m (1 -+ 2^-20) (two plain multiplies; m_lo, m_hi wave-uniform): a < fl(d m_lo)
-// puts the true quotient below m (1 - 2^-21), so fl(a / d) < m; a > fl(d m_hi) puts it above m (1 + 2^-21).
-// Otherwise: a * rcp(d) (v_rcp_f32, <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20
-// relative either way. The rare near-ties (and NaN / inf) take the exact division, so the decision is
-// always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
+// sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d) (v_rcp_f32,
+// <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20 relative either way. (MPSS_MO_DWMUL = 1:
+// a against the products d * m (1 -+ 2^-20) instead -- a < fl(d m_lo) puts the true quotient below
+// m (1 - 2^-21), a > fl(d m_hi) above m (1 + 2^-21) -- two plain multiplies for v_rcp; measured equal,
+// profiles/r05g_dwmul_ab.txt.) The rare near-ties (and NaN / inf) take the exact division, so the decision
+// is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
 #ifndef MPSS_MO_DWMUL
-#define MPSS_MO_DWMUL 1
+#define MPSS_MO_DWMUL 0
 #endif
 __device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, float m_hi) {
 #if MPSS_MO_DWMUL

@@ -125,6 +125,47 @@ struct WaveMt {
     }
 };
 
+// Whether a camera ray hits the scene (SamplerRenderer::Li's scene->Intersect, samplerrenderer.cpp:
+// 97-112: a hit is what makes Li draw its 6 values). A ray that meets one of the wave's cached triangles
+// (the previous pixel's hits, cache[]) hits; the others walk the BVH (trace_any_wave: the light spheres,
+// then the threaded any-hit walk), whose first hit triangles refill the cache when `refill`. The answer
+// is the same either way: a ray meeting a triangle is a hit whatever else it meets.
+constexpr int kCamCache = 4;
+__device__ bool cam_hit(const RenderScene &sc, V3 o, V3 d, bool active, int cache[kCamCache], bool refill) {
+    bool hit = false;
+    const cptr<TriRec> tris = as_const(sc.tris);
+#pragma unroll
+    for (int c = 0; c < kCamCache; ++c) {
+        const int t = cache[c];  // (wave-uniform)
+        if (t < 0) continue;
+        const TriRec tr = tris[t];
+        float th, b1, b2;
+        if (active && !hit &&
+            tri_intersect(o, d, 0.f, INFINITY, V3{tr.p1[0], tr.p1[1], tr.p1[2]}, V3{tr.e1[0], tr.e1[1], tr.e1[2]},
+                          V3{tr.e2[0], tr.e2[1], tr.e2[2]}, th, b1, b2))
+            hit = true;
+    }
+    int tw = -1;
+    if (__builtin_amdgcn_ballot_w64(active && !hit) != 0)
+        hit = trace_any_wave(sc, o, d, 0.f, INFINITY, active && !hit, false, true, &tw) || hit;
+    if (refill) {  // the walk's hit triangles become the cache (kept when no lane walked)
+        uint64_t m = __builtin_amdgcn_ballot_w64(tw >= 0);
+        if (m != 0) {
+#pragma unroll
+            for (int c = 0; c < kCamCache; ++c) {
+                if (m == 0) {
+                    cache[c] = -1;
+                    continue;
+                }
+                const int t = __builtin_amdgcn_readlane(tw, __builtin_ctzll(m));
+                cache[c] = t;
+                m &= ~__builtin_amdgcn_ballot_w64(tw == t);
+            }
+        }
+    }
+    return hit;
+}
+
 // Shuffle(samples, count, dims) of whole samples replayed on idx (idx[i] = the original sample at
 // position i afterwards), from its count draws already in d: first each draw becomes its swap
 // partner i + d[i] % (count - i) (all lanes), then the swaps run in order on lane `who`
@@ -175,7 +216,12 @@ __device__ ReplayArray replay_array(const RenderScene &sc, int spp, int nmax, ui
     return ReplayArray{adraw + off, aidx + (size_t)a * spp, asig + (size_t)a * spp * nmax, n, hdr, col};
 }
 
-__global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderScene sc, ReplayWindow g, int words) {
+// skip: a diagnostic only (MPSS_REPLAY_SKIP, launch_replay_window; the values are then wrong): bit 0
+// the per-sample own shuffles and the block shuffles' partners, 1 the block swaps, 2 the camera-ray
+// trace, 3 the light arrays' values, 4 the draws' copies (the stream still advances) -- the cost of each
+// section of the pixel loop, measured by leaving it out.
+__global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderScene sc, ReplayWindow g, int words,
+                                                                       int skip) {
     extern __shared__ uint32_t smem[];
     const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
     const int nwv = (int)(blockDim.x >> 6);
@@ -212,6 +258,12 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
     }
     const V3 cam_o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
     const int64_t npix = (int64_t)g.w * g.h;
+    // the triangles this wave's camera rays hit in the previous pixel (a pixel's rays are a pixel's
+    // footprint apart and consecutive pixels of a task are neighbours: they usually hit the same few
+    // triangles). Rays are first tested against those; only the rest walk the BVH (cam_tri below).
+    int ctri[kCamCache];
+#pragma unroll
+    for (int c = 0; c < kCamCache; ++c) ctri[c] = -1;
 #ifdef MPSS_REPLAY_PROFILE
     uint64_t rp_acc[6] = {0, 0, 0, 0, 0, 0}, rp_t = rp_clock();
     const uint64_t rp_t0 = rp_t;
@@ -229,21 +281,22 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         // integrator's two 1D(1) arrays (advance), per light the light position and BSDF direction
         const uint2 si = mt.two();
         mt.skip(spp);
-        mt.fetch(dimg, spp);
+        if (skip & 16) mt.skip(spp); else mt.fetch(dimg, spp);
         mt.skip(2 + 2 * (int64_t)spp);  // lens: LDShuffleScrambled2D(1, spp)
         mt.skip(1 + 2 * (int64_t)spp);  // time: LDShuffleScrambled1D(1, spp)
         for (int l = 0; l < sc.nlights; ++l) {
             mt.skip(1 + (int64_t)spp * sc.lights[l].nsamples_round + spp);
             const ReplayArray A = array(l);
-            mt.fetch(A.d, A.hdr + spp * A.n + spp);
+            if (skip & 16) mt.skip(A.hdr + spp * A.n + spp); else mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
         mt.skip(2 * (1 + 2 * (int64_t)spp));
         for (int a = sc.nlights; a < na; ++a) {
             const ReplayArray A = array(a);
-            mt.fetch(A.d, A.hdr + spp * A.n + spp);
+            if (skip & 16) mt.skip(A.hdr + spp * A.n + spp); else mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
         RP_MARK(0);
         // each sample's own shuffle (lane per sample) and every block shuffle's partners
+        if (!(skip & 1)) {
         shuffle_partners(dimg, idx0, spp);
         for (int a = 0; a < na; ++a) {
             const ReplayArray A = array(a);
@@ -260,11 +313,13 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             }
             shuffle_partners(A.d + A.hdr + spp * A.n, A.idx, spp);
         }
+        }
         wave_sync();
         RP_MARK(1);
         // the block shuffles side by side: the image's swaps on lane 0, array a's on lane 1 + a % 63
         // (lanes 1..63 take arrays a, a + 63, ... in turn: any light count)
-        if (lane == 0) {
+        if (skip & 2) {
+        } else if (lane == 0) {
             shuffle_swaps(dimg, idx0, spp);
         } else {
             for (int a = lane - 1; a < na; a += 63) {
@@ -284,16 +339,16 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
                 put(0, i, u);
                 put(1, i, v);
             }
-            if (g.li_draws > 0) {
+            if (g.li_draws > 0 && !(skip & 4)) {
                 const float X = (float)x + u, Y = (float)y + v;
                 const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
                 const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
-                const bool hit = trace_any_wave(sc, cam_o, d, 0.f, INFINITY, i < spp, false, true);
+                const bool hit = cam_hit(sc, cam_o, d, i < spp, ctri, c == 0);
                 hits += __popcll(__ballot(hit && i < spp));
             }
         }
         RP_MARK(3);
-        if (keep)
+        if (keep && !(skip & 8))
             for (int a = 0; a < na; ++a) {
                 const ReplayArray A = array(a);
                 const uint32_t s0 = A.d[0], s1 = A.d[A.hdr - 1];
@@ -411,8 +466,9 @@ void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStrea
     if (lds > 64 * 1024)
         MPSS_HIP(hipFuncSetAttribute((const void *)replay_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
+    static const int skip = getenv("MPSS_REPLAY_SKIP") ? atoi(getenv("MPSS_REPLAY_SKIP")) : 0;
     hipLaunchKernelGGL(replay_window_kernel, dim3((unsigned)((nw + nwv - 1) / nwv)), dim3(64 * nwv), lds, stream, sc,
-                       w, words);
+                       w, words, skip);
     MPSS_HIP(hipGetLastError());
 }
 

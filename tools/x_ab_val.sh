@@ -11,7 +11,7 @@ for r in $(seq 1 $R); do
     if [ "$v" = "-" ]; then unset $VAR; else export $VAR=$v; fi
     log=gpurun_out/${TAG}_${v}_$r.log
     timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary $ARGS > $log 2>&1 || { echo "run $v $r failed"; tail -5 $log; exit 1; }
-    python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["roofline"]["kernel_ms_per_step"]["mo_band"])' $log "$VAR=$v#$r" | tee -a gpurun_out/${TAG}_ab.txt
+    python3 -c 'import json,sys; d=json.loads([l for l in open(sys.argv[1]) if "\"metric\"" in l][0]); print(sys.argv[2], d["value"], d["roofline"]["kernel_ms_per_step"]["mo_band"], d["roofline"]["kernel_ms_per_step"].get("replay"))' $log "$VAR=$v#$r" | tee -a gpurun_out/${TAG}_ab.txt
   done
 done
 unset $VAR
