@@ -51,9 +51,9 @@ L2_GATHER_CEILING_REQ_S = 2.48e11
 # gather's occupancy (two 1024-thread workgroups per CU, 8 waves per SIMD) and reports wave64 VALU
 # instructions per second over the chip. Plain f32 add / mul / fma issue every ~2.3 cycles per SIMD there,
 # packed f32, conversions, compares, selects and integer shifts every ~4.2, v_rcp every ~8.2
-# (profiles/r05c_valu_issue.json), so the ceiling is the mix's, not a per-instruction constant.
-VALU_CEILING_JSON = "profiles/r05c_valu_issue.json"
-VALU_CEILING_VARIANT = "gather mix (VALU + SALU)"
+# (profiles/r05c_valu_issue.json, r05e_valu_issue.json), so the ceiling is the mix's, not a per-instruction constant.
+VALU_CEILING_JSON = "profiles/r05e_valu_issue.json"
+VALU_CEILING_VARIANT = "gather mix r05 (fused: row + LDS record, VALU + SALU)"
 # sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
 KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
                   "pbrt-v2-skin_amd/csrc/mo_wave.h", "pbrt-v2-skin_amd/csrc/octree.h")
@@ -322,10 +322,11 @@ def main(a):
     shade_launch_ms = st["ms_shade"] / max(1, st["n_shade"])
     launches_per_step = max(1, st["n_shade"] // max(1, a.steps))
     mo_gbs = mo_bytes_step / launches_per_step / (shade_launch_ms * 1e-3) / 1e9 if shade_launch_ms > 0 else 0.0
-    # The gather's binding resource is the L2 request rate of its per-lane table gathers:
-    # the headline roofline is requests per second against the rate tools/microbench/l2_policy.hip
-    # sustains. Its request count comes from the committed PMC pass of the same config and kernel
-    # sources (TCP_TCC_READ_REQ per launch), its duration from this run's HIP events.
+    # The gather's roofline: its L2 request rate against the rate
+    # tools/microbench/l2_width.hip sustains in the grid's load shape, and its VALU issue against the
+    # rate tools/microbench/valu_issue.hip measures for its instruction mix (headline_bound: the larger
+    # fraction leads). The counts come from the committed PMC pass of the same config and kernel
+    # sources (TCP_TCC_READ_REQ, SQ_INSTS_VALU per launch), the duration from this run's HIP events.
     pt = pmc_traffic(a.pmc_json, shade_launch_ms, a.config)
     roofline = {"kernel": "mo_sort_kernel + mo_band_wave_kernel (Mo gather, spectrally sharded, wave queue)",
                 "bound": "l2_requests", "achieved": None, "peak": L2_GATHER_CEILING_REQ_S / 1e9, "unit": "Greq/s",
@@ -482,33 +483,39 @@ def reference_sampler_secondary(a, local):
 
 
 def headline_bound(roofline, pt, launch_ms):
-    """The headline names the resource that binds the gather: the L2 request rate of its lookups
-    (rounds 2-3), or VALU issue once the common grid cut the lookups (round 4 on). The VALU peak is the
-    measured issue rate of the record loop's instruction mix at the kernel's occupancy (valu_ceiling),
-    cross-checked by the counters' own VALU busy fraction (SQ_ACTIVE_INST_VALU over SQ_BUSY_CU_CYCLES:
-    the SIMDs' cycles with a VALU instruction in flight, from the same PMC summary). The L2 request
-    figure stays beside it."""
+    """The headline names the resource that binds the gather hardest: the L2 request rate of its
+    lookups (rounds 2-3) or VALU issue (round 4 on), whichever runs at the larger fraction of its
+    measured ceiling; the other stays beside it (`roofline.l2_requests` / `roofline.valu_issue`). The
+    VALU peak is the measured issue rate of the record loop's instruction mix at the kernel's
+    occupancy (valu_ceiling), cross-checked by the counters' own VALU busy fraction
+    (SQ_ACTIVE_INST_VALU over SQ_BUSY_CU_CYCLES: the SIMDs' cycles with a VALU instruction in flight,
+    from the same PMC summary)."""
     v = pt.get("valu") if pt else None
     ceil = valu_ceiling()
     if not v or not ceil or launch_ms <= 0:
         return
     achieved = v["insts_per_launch"] / (launch_ms * 1e-3)
     frac = achieved / ceil[0]
+    valu = {"achieved": round(achieved / 1e9, 1), "peak": round(ceil[0] / 1e9, 1),
+            "unit": "G wave64 VALU instructions/s", "frac": round(frac, 4),
+            "peak_source": ceil[2] + "; achieved = SQ_INSTS_VALU per launch (committed PMC summary) / this run's "
+                                     "launch time"}
+    if "busy" in v:
+        valu["busy_pmc"] = round(v["busy"], 4)
+        valu["busy_source"] = ("SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES per launch (quad-cycles with a VALU "
+                               "instruction in flight per SIMD over the CUs' busy cycles / 4 SIMDs x 4)")
     if roofline.get("frac") is not None and frac <= roofline["frac"]:
+        roofline["valu_issue"] = valu
         return
     if roofline.get("achieved") is not None:
         roofline["l2_requests"] = {"achieved": roofline["achieved"], "peak": roofline["peak"], "unit": "Greq/s",
                                    "frac": roofline["frac"], "peak_source": roofline.get("peak_source")}
     roofline["bound"] = "valu_issue"
-    roofline["achieved"] = round(achieved / 1e9, 1)
-    roofline["peak"] = round(ceil[0] / 1e9, 1)
-    roofline["unit"] = "G wave64 VALU instructions/s"
-    roofline["frac"] = round(frac, 4)
-    roofline["peak_source"] = ceil[2] + "; achieved = SQ_INSTS_VALU per launch (committed PMC summary) / this run's launch time"
-    if "busy" in v:
-        roofline["valu_busy_pmc"] = round(v["busy"], 4)
-        roofline["valu_busy_source"] = ("SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES per launch (quad-cycles with a VALU "
-                                        "instruction in flight per SIMD over the CUs' busy cycles / 4 SIMDs x 4)")
+    for k in ("achieved", "peak", "unit", "frac", "peak_source"):
+        roofline[k] = valu[k]
+    if "busy_pmc" in valu:
+        roofline["valu_busy_pmc"] = valu["busy_pmc"]
+        roofline["valu_busy_source"] = valu["busy_source"]
 
 
 def pmc_traffic(path, launch_ms, config):

@@ -82,10 +82,8 @@ __device__ __noinline__ bool sphere_hit_ool(const SphereView &s, V3 o, V3 d, flo
 // reaches with the fixed maxt (any-hit prunes only by the box test, so the order does not change
 // the answer). strict: a triangle counts only when t < maxt (the BSDF ray toward an area light,
 // whose own surface is at maxt). spheres: test the area-light spheres first, as trace_any does.
-// tri_out (nullable): the lane's hit triangle (its index in RenderScene::tris), -1 for a miss or a sphere.
 __device__ bool trace_any_wave(const RenderScene &sc, V3 o, V3 d, float mint, float maxt, bool active, bool strict,
-                               bool spheres, int *tri_out = nullptr) {
-    if (tri_out) *tri_out = -1;
+                               bool spheres) {
     bool hit = false;
     if (active && spheres)
         for (int l = 0; l < sc.nlights; ++l) {
@@ -115,10 +113,8 @@ __device__ bool trace_any_wave(const RenderScene &sc, V3 o, V3 d, float mint, fl
                     float t, b1, b2;
                     if (in && !found &&
                         tri_intersect(o, d, mint, maxt, V3{tr.p1[0], tr.p1[1], tr.p1[2]},
-                                      V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2)) {
+                                      V3{tr.e1[0], tr.e1[1], tr.e1[2]}, V3{tr.e2[0], tr.e2[1], tr.e2[2]}, t, b1, b2))
                         found = !strict || t < maxt;
-                        if (found && tri_out) *tri_out = (int)n.offset + i;
-                    }
                 }
                 if (found) {
                     hit = true;

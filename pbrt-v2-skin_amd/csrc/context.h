@@ -167,8 +167,10 @@ private:
     uint64_t scene_gen_ = 0;
     // the window [x0, x1) x [y0, y1) of the sample extent at spp into ws->rp_table (the cursors in ws
     // reset when the scene, spp or task count changed); on `stream`
+    // all_values: every sample's light-sample values (the whole table, replay_samples), not only those
+    // of samples whose camera ray hits (all a render reads)
     void replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp, int x0, int x1, int y0, int y1,
-                       hipStream_t stream);
+                       hipStream_t stream, bool all_values = false);
     SceneData scene_;
     bool scene_dirty_ = true, have_points_ = false;
     std::vector<SurfacePoint> points_;
@@ -176,6 +178,10 @@ private:
     DevBuf<BvhNode> d_bvh_;
     DevBuf<BvhNode> d_bvh_thread_;  // threaded copy (interior offset = end of subtree), any-hit walks
     DevBuf<TriRec> d_tris_;
+    // reference sampler: the camera rays' candidate triangles per pixel (scene.h CameraBins)
+    DevBuf<uint32_t> d_bin_off_;
+    DevBuf<int32_t> d_bin_tri_, d_bin_all_;
+    int bin_w_ = 0, bin_nall_ = 0;
     DevBuf<int32_t> d_tri_mesh_, d_tri_local_;
     std::vector<std::unique_ptr<DevBuf<float>>> d_mesh_bufs_;
     DevBuf<struct RenderMesh> d_meshes_;

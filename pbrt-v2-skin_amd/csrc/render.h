@@ -101,6 +101,13 @@ struct ReplayWindow {
                                  // lights of 3 (spp n + spp) + 5
     ReplayCursors cur;
     float *out;                // the window table (RenderScene::replay layout)
+    // the camera rays' candidate triangles per pixel of the sample extent (scene.h CameraBins)
+    const uint32_t *bin_off;   // [bin_w * (yres + 1) + 1]
+    const int32_t *bin_tri, *bin_all;
+    int bin_w, bin_nall;
+    // 1: every sample's light-sample values (replay_samples: the whole table); 0: only those of
+    // samples whose camera ray hits (a render: the others are never shaded)
+    int all_values;
 };
 // Launches the generation on `stream` (the host picks the task ranges: replay_window_tasks).
 void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStream_t stream);

@@ -134,6 +134,15 @@ void Context::upload_scene() {
         d_bvh_thread_.upload(th.data(), th.size());
     }
     d_tris_.upload(scene_.tris.data(), scene_.tris.size());
+    if (cfg_.sampler == MPSS_SAMPLER_REFERENCE && scene_.camera.xres > 0) {
+        CameraBins b;
+        build_camera_bins(scene_, b);
+        d_bin_off_.upload(b.off.data(), b.off.size());
+        d_bin_tri_.upload(b.tri.data(), b.tri.size());
+        d_bin_all_.upload(b.all.data(), b.all.size());
+        bin_w_ = b.w;
+        bin_nall_ = (int)b.all.size();
+    }
     d_tri_mesh_.upload(scene_.tri_mesh.data(), scene_.tri_mesh.size());
     d_tri_local_.upload(scene_.tri_local.data(), scene_.tri_local.size());
     d_mesh_bufs_.clear();
@@ -566,7 +575,7 @@ void Context::find_poisson_points(uint32_t seed) {
 // The reference sampler's values over [x0, x1) x [y0, y1) of the sample extent at `spp`
 // (replay_gen.hip) into ws->rp_table, continuing the workspace's task streams.
 void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp, int x0, int x1, int y0, int y1,
-                            hipStream_t stream) {
+                            hipStream_t stream, bool all_values) {
     const int W = sc.xres, H = sc.yres;
     const int T = replay_render_tasks(W, H, std::max(1, cfg_.replay_cores));
     const uint64_t key[3] = {scene_gen_, (uint64_t)spp, (uint64_t)T};
@@ -601,6 +610,13 @@ void Context::replay_window(RenderWorkspace *ws, const RenderScene &sc, int spp,
     }
     w.cur = ReplayCursors{ws->rp_mt.ptr, ws->rp_pix.ptr, ws->rp_mti.ptr};
     w.out = ws->rp_table.ptr;
+    if (!d_bin_off_.ptr || bin_w_ != W + 1) throw Error(MPSS_ERR_INTERNAL, "replay: no camera-ray bins for this camera");
+    w.bin_off = d_bin_off_.ptr;
+    w.bin_tri = d_bin_tri_.ptr;
+    w.bin_all = d_bin_all_.ptr;
+    w.bin_w = bin_w_;
+    w.bin_nall = bin_nall_;
+    w.all_values = all_values ? 1 : 0;
     launch_replay_window(sc, w, stream);
 }
 
@@ -631,7 +647,7 @@ void Context::replay_samples(int spp, float *out, uint64_t *n_floats, int *k) {
     RenderScene sc = render_scene();
     lk.unlock();
     InflightGuard guard{this, ws, nullptr};
-    replay_window(ws, sc, spp, 0, W + 1, 0, H + 1, nullptr);
+    replay_window(ws, sc, spp, 0, W + 1, 0, H + 1, nullptr, true);
     std::vector<float> col((size_t)npix * spp * K);
     MPSS_HIP(hipMemcpy(col.data(), ws->rp_table.ptr, sizeof(float) * col.size(), hipMemcpyDeviceToHost));
     ws->rp_key[0] = ~0ull;  // (its cursors now sit at the end of every stream)

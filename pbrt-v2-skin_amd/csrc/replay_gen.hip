@@ -16,7 +16,14 @@
 // block shuffle, sequential over the spp swaps, on one lane; each sample's own shuffle on its
 // lane), and every value is then computed at its final place from the index it ends up holding --
 // the (0,2) point of that index. The arrays the kernels read (image, light position, BSDF
-// component, BSDF direction) are written to the window table; the others only advance the stream.
+// component, BSDF direction) are written to the window table -- the light arrays only for samples
+// whose camera ray hits, the only ones shaded -- and the others only advance the stream.
+//
+// Whether a camera ray hits decides how far its pixel's Li advances the stream, so each is tested
+// here, against the pixel's candidate triangles (scene.h CameraBins: the triangles whose projection
+// can contain a point of the pixel) rather than by a BVH walk: the walks of the rays that pass close
+// by the head without hitting it made the tasks around its silhouette the launch's longest
+// (profiles/r05l_bins_ab.txt: 13.5 -> 7.5 ms per C2 frame).
 #include "../../include/mpss.h"
 #include "bvh_trace.h"
 #include "render.h"
@@ -27,19 +34,9 @@ namespace mpss {
 
 namespace {
 
-// MPSS_REPLAY_PROFILE (a diagnostic build only): each wave accumulates its shader-clock cycles per
-// section of the pixel loop and prints them for a sample of tasks (where a C2 task's time goes).
-#ifdef MPSS_REPLAY_PROFILE
-__device__ __forceinline__ uint64_t rp_clock() { return __builtin_readcyclecounter(); }
-#define RP_MARK(k)                         \
-    do {                                   \
-        const uint64_t t_ = rp_clock();    \
-        rp_acc[k] += t_ - rp_t;            \
-        rp_t = t_;                         \
-    } while (0)
-#else
-#define RP_MARK(k) (void)0
-#endif
+// MPSS_REPLAY_TASKTIME (a diagnostic build only): each wave prints its task's wall time (the
+// real-time counter), pixel and camera-hit counts at the end (tools/replay_tasktime.py): the spread
+// of task times against the launch, which ends with its slowest task.
 
 constexpr int kMaxWaves = 4;  // waves per workgroup (fewer when a wave's LDS needs more room)
 
@@ -125,43 +122,43 @@ struct WaveMt {
     }
 };
 
-// Whether a camera ray hits the scene (SamplerRenderer::Li's scene->Intersect, samplerrenderer.cpp:
-// 97-112: a hit is what makes Li draw its 6 values). A ray that meets one of the wave's cached triangles
-// (the previous pixel's hits, cache[]) hits; the others walk the BVH (trace_any_wave: the light spheres,
-// then the threaded any-hit walk), whose first hit triangles refill the cache when `refill`. The answer
-// is the same either way: a ray meeting a triangle is a hit whatever else it meets.
-constexpr int kCamCache = 4;
-__device__ bool cam_hit(const RenderScene &sc, V3 o, V3 d, bool active, int cache[kCamCache], bool refill) {
+// Whether a camera ray through pixel (x, y) of the sample extent hits the scene (SamplerRenderer::Li's
+// scene->Intersect, samplerrenderer.cpp:97-112: a hit is what makes Li draw its 6 values): the light
+// spheres, then the pixel's candidate triangles (scene.h CameraBins: every triangle a ray through the
+// pixel can meet in front of the camera) and the triangles every pixel tests. The answer is the BVH
+// walk's: a ray hits iff it meets some triangle, whichever the walk would have found first. The
+// candidates are wave-uniform (one pixel per wave), so each is one scalar load and one test per lane;
+// the wave stops once every lane has hit.
+__device__ bool cam_hit(const RenderScene &sc, const ReplayWindow &g, int x, int y, V3 o, V3 d, bool active) {
     bool hit = false;
+    if (active)
+        for (int l = 0; l < sc.nlights; ++l) {
+            float t;
+            if (!sc.lights[l].kind && sphere_hit_ool(sc.lights[l].s, o, d, 0.f, INFINITY, t, nullptr)) {
+                hit = true;
+                break;
+            }
+        }
     const cptr<TriRec> tris = as_const(sc.tris);
-#pragma unroll
-    for (int c = 0; c < kCamCache; ++c) {
-        const int t = cache[c];  // (wave-uniform)
-        if (t < 0) continue;
+    auto test = [&](int t) {
         const TriRec tr = tris[t];
         float th, b1, b2;
         if (active && !hit &&
             tri_intersect(o, d, 0.f, INFINITY, V3{tr.p1[0], tr.p1[1], tr.p1[2]}, V3{tr.e1[0], tr.e1[1], tr.e1[2]},
                           V3{tr.e2[0], tr.e2[1], tr.e2[2]}, th, b1, b2))
             hit = true;
+    };
+    const cptr<int32_t> all = as_const(g.bin_all), cand = as_const(g.bin_tri);
+    for (int k = 0; k < g.bin_nall; ++k) {
+        if (__builtin_amdgcn_ballot_w64(active && !hit) == 0) return hit;
+        test(all[k]);
     }
-    int tw = -1;
-    if (__builtin_amdgcn_ballot_w64(active && !hit) != 0)
-        hit = trace_any_wave(sc, o, d, 0.f, INFINITY, active && !hit, false, true, &tw) || hit;
-    if (refill) {  // the walk's hit triangles become the cache (kept when no lane walked)
-        uint64_t m = __builtin_amdgcn_ballot_w64(tw >= 0);
-        if (m != 0) {
-#pragma unroll
-            for (int c = 0; c < kCamCache; ++c) {
-                if (m == 0) {
-                    cache[c] = -1;
-                    continue;
-                }
-                const int t = __builtin_amdgcn_readlane(tw, __builtin_ctzll(m));
-                cache[c] = t;
-                m &= ~__builtin_amdgcn_ballot_w64(tw == t);
-            }
-        }
+    const int p = __builtin_amdgcn_readfirstlane(y * g.bin_w + x);
+    const cptr<uint32_t> off = as_const(g.bin_off);
+    const uint32_t lo = off[p], hi = off[p + 1];
+    for (uint32_t k = lo; k < hi; ++k) {
+        if (__builtin_amdgcn_ballot_w64(active && !hit) == 0) break;
+        test(cand[k]);
     }
     return hit;
 }
@@ -217,8 +214,8 @@ __device__ ReplayArray replay_array(const RenderScene &sc, int spp, int nmax, ui
 }
 
 // skip: a diagnostic only (MPSS_REPLAY_SKIP, launch_replay_window; the values are then wrong): bit 0
-// the per-sample own shuffles and the block shuffles' partners, 1 the block swaps, 2 the camera-ray
-// trace, 3 the light arrays' values, 4 the draws' copies (the stream still advances) -- the cost of each
+// the per-sample own shuffles and the block shuffles' partners, 1 the block swaps, 2 the camera rays'
+// hit tests, 3 the light arrays' values, 4 the draws' copies (the stream still advances) -- the cost of each
 // section of the pixel loop, measured by leaving it out.
 __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderScene sc, ReplayWindow g, int words,
                                                                        int skip) {
@@ -258,16 +255,9 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
     }
     const V3 cam_o = xform_point(sc.camera_to_world, V3{0.f, 0.f, 0.f});
     const int64_t npix = (int64_t)g.w * g.h;
-    // the triangles this wave's camera rays hit in the previous pixel (a pixel's rays are a pixel's
-    // footprint apart and consecutive pixels of a task are neighbours: they usually hit the same few
-    // triangles). Rays are first tested against those; only the rest walk the BVH (cam_tri below).
-    int ctri[kCamCache];
-#pragma unroll
-    for (int c = 0; c < kCamCache; ++c) ctri[c] = -1;
-#ifdef MPSS_REPLAY_PROFILE
-    uint64_t rp_acc[6] = {0, 0, 0, 0, 0, 0}, rp_t = rp_clock();
-    const uint64_t rp_t0 = rp_t;
-    int rp_hits = 0, rp_pix = 0;
+#ifdef MPSS_REPLAY_TASKTIME
+    const uint64_t tt0 = __builtin_amdgcn_s_memrealtime();
+    int tt_hits = 0, tt_pix = 0;
 #endif
     for (; ord <= last; ++ord) {
         const int x = x0 + ord % tw, y = y0 + ord / tw;
@@ -294,7 +284,6 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             const ReplayArray A = array(a);
             if (skip & 16) mt.skip(A.hdr + spp * A.n + spp); else mt.fetch(A.d, A.hdr + spp * A.n + spp);
         }
-        RP_MARK(0);
         // each sample's own shuffle (lane per sample) and every block shuffle's partners
         if (!(skip & 1)) {
         shuffle_partners(dimg, idx0, spp);
@@ -315,7 +304,6 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         }
         }
         wave_sync();
-        RP_MARK(1);
         // the block shuffles side by side: the image's swaps on lane 0, array a's on lane 1 + a % 63
         // (lanes 1..63 take arrays a, a + 63, ... in turn: any light count)
         if (skip & 2) {
@@ -328,9 +316,12 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             }
         }
         wave_sync();
-        RP_MARK(2);
         // the image samples and the camera rays (samplerrenderer.cpp:97-103): only whether they hit
         int hits = 0;
+        // which of this lane's samples (lane + 64 m: bit m) hit: only those are shaded, so only their
+        // light-sample values are read (render.hip); the others' are not written unless g.all_values
+        uint64_t hm = 0;
+        const bool traced = g.li_draws > 0 && !(skip & 4);
         for (int c = 0; c < spp; c += 64) {
             const int i = c + lane;
             const uint32_t b = idx0[i < spp ? i : 0];
@@ -339,20 +330,21 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
                 put(0, i, u);
                 put(1, i, v);
             }
-            if (g.li_draws > 0 && !(skip & 4)) {
+            if (traced) {
                 const float X = (float)x + u, Y = (float)y + v;
                 const V3 pcam = xform_point(sc.raster_to_camera, V3{X, Y, 0.f});
                 const V3 d = xform_vector(sc.camera_to_world, normalize(pcam));
-                const bool hit = cam_hit(sc, cam_o, d, i < spp, ctri, c == 0);
+                const bool hit = cam_hit(sc, g, x, y, cam_o, d, i < spp);
                 hits += __popcll(__ballot(hit && i < spp));
+                if (hit) hm |= 1ull << (c >> 6);
             }
         }
-        RP_MARK(3);
         if (keep && !(skip & 8))
             for (int a = 0; a < na; ++a) {
                 const ReplayArray A = array(a);
                 const uint32_t s0 = A.d[0], s1 = A.d[A.hdr - 1];
-                for (int i = lane; i < spp; i += 64) {
+                for (int i = lane, m = 0; i < spp; i += 64, ++m) {
+                    if (traced && !g.all_values && !((hm >> m) & 1)) continue;
                     const uint32_t b = A.idx[i];
                     const uint8_t *sg = A.sig + (size_t)b * A.n;
                     for (int j = 0; j < A.n; ++j) {
@@ -363,22 +355,16 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
                 }
             }
         wave_sync();
-        RP_MARK(4);
         mt.skip((int64_t)g.li_draws * hits);  // Li, per camera ray that hits
-        RP_MARK(5);
-#ifdef MPSS_REPLAY_PROFILE
-        rp_hits += hits;
-        ++rp_pix;
+#ifdef MPSS_REPLAY_TASKTIME
+        tt_hits += hits;
+        ++tt_pix;
 #endif
     }
-#ifdef MPSS_REPLAY_PROFILE
-    const uint64_t rp_tot = rp_clock() - rp_t0;
-    if (lane == 0 && (task % 97 == 0 || rp_tot > 20000000ull))
-        printf("replay task %d: pixels %d hits %d total %llu | draws %llu own+partners %llu swaps %llu image+trace %llu "
-               "values %llu li-skip %llu\n",
-               task, rp_pix, rp_hits, (unsigned long long)rp_tot, (unsigned long long)rp_acc[0],
-               (unsigned long long)rp_acc[1], (unsigned long long)rp_acc[2], (unsigned long long)rp_acc[3],
-               (unsigned long long)rp_acc[4], (unsigned long long)rp_acc[5]);
+#ifdef MPSS_REPLAY_TASKTIME
+    if (lane == 0)
+        printf("tasktime %d %d %d %d %d %llu\n", task, x0, y0, tt_pix, tt_hits,
+               (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tt0));
 #endif
     for (int k = lane; k < 624; k += 64) gst[k] = mt.st[k];
     if (lane == 0) {

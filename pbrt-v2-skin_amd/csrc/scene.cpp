@@ -7,6 +7,7 @@
 #include "texture.h"
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstring>
 #include <thread>
@@ -231,6 +232,124 @@ void tessellate_surface_points(const SceneData &s, float min_dist, bool incenter
     for (auto &j : jobs) total += j.pts.size();
     out.reserve(total);
     for (auto &j : jobs) out.insert(out.end(), j.pts.begin(), j.pts.end());
+}
+
+// ------------------------------------------------------------------------------- camera bins
+namespace {
+bool invert4(const double *m, double *out) {  // Gauss-Jordan with partial pivoting
+    double a[4][8];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 8; ++c) a[r][c] = c < 4 ? m[4 * r + c] : (c - 4 == r ? 1.0 : 0.0);
+    for (int c = 0; c < 4; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < 4; ++r)
+            if (std::fabs(a[r][c]) > std::fabs(a[piv][c])) piv = r;
+        if (a[piv][c] == 0.0) return false;
+        if (piv != c)
+            for (int k = 0; k < 8; ++k) std::swap(a[c][k], a[piv][k]);
+        const double inv = 1.0 / a[c][c];
+        for (int k = 0; k < 8; ++k) a[c][k] *= inv;
+        for (int r = 0; r < 4; ++r)
+            if (r != c && a[r][c] != 0.0) {
+                const double f = a[r][c];
+                for (int k = 0; k < 8; ++k) a[r][k] -= f * a[c][k];
+            }
+    }
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) out[4 * r + c] = a[r][c + 4];
+    return true;
+}
+void xform4(const double *m, const double *p, double *o) {  // o = m (p, 1), 4 components
+    for (int r = 0; r < 4; ++r) o[r] = m[4 * r] * p[0] + m[4 * r + 1] * p[1] + m[4 * r + 2] * p[2] + m[4 * r + 3];
+}
+}  // namespace
+
+void build_camera_bins(const SceneData &s, CameraBins &b) {
+    const Camera &cam = s.camera;
+    b.w = cam.xres + 1;
+    b.h = cam.yres + 1;
+    b.off.assign((size_t)b.w * b.h + 1, 0u);
+    b.tri.clear();
+    b.all.clear();
+    double c2w[16], r2c[16], w2c[16], c2r[16];
+    for (int k = 0; k < 16; ++k) {
+        c2w[k] = cam.camera_to_world[k];
+        r2c[k] = cam.raster_to_camera[k];
+    }
+    const bool ok = invert4(c2w, w2c) && invert4(r2c, c2r);
+    // per triangle: its pixel box [x0, x1] x [y0, y1] (inclusive), or a list tag
+    enum { kNone = 0, kBox = 1, kAll = 2 };
+    const size_t n = s.tris.size();
+    std::vector<int> box(4 * n), tag(n, kNone);
+    for (size_t i = 0; i < n; ++i) {
+        if (!ok) {
+            tag[i] = kAll;
+            continue;
+        }
+        const TriRec &t = s.tris[i];
+        double v[3][3];
+        for (int k = 0; k < 3; ++k) {
+            v[0][k] = t.p1[k];
+            v[1][k] = (double)t.p1[k] + (double)t.e1[k];
+            v[2][k] = (double)t.p1[k] + (double)t.e2[k];
+        }
+        int behind = 0, near = 0;
+        double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
+        for (int j = 0; j < 3; ++j) {
+            double pc[4], pr[4];
+            xform4(w2c, v[j], pc);
+            const double dist = std::sqrt(pc[0] * pc[0] + pc[1] * pc[1] + pc[2] * pc[2]);
+            const double eps = 1e-3 * dist;  // (camera rays leave the origin with a positive z)
+            if (pc[2] < -eps) ++behind;
+            if (pc[2] <= eps) {
+                ++near;
+                continue;
+            }
+            xform4(c2r, pc, pr);
+            if (!(pr[3] != 0.0)) {
+                ++near;
+                continue;
+            }
+            for (int k = 0; k < 2; ++k) {
+                const double q = pr[k] / pr[3];
+                lo[k] = std::min(lo[k], q);
+                hi[k] = std::max(hi[k], q);
+            }
+        }
+        if (behind == 3) continue;  // no point of it has a positive camera z: no camera ray reaches it
+        if (near > 0) {
+            tag[i] = kAll;
+            continue;
+        }
+        const double x0 = std::floor(lo[0] - kCamBinMargin), x1 = std::floor(hi[0] + kCamBinMargin);
+        const double y0 = std::floor(lo[1] - kCamBinMargin), y1 = std::floor(hi[1] + kCamBinMargin);
+        if (x1 < 0 || y1 < 0 || x0 > b.w - 1 || y0 > b.h - 1) continue;  // off the sample extent
+        const int ix0 = (int)std::max(0.0, x0), ix1 = (int)std::min((double)b.w - 1, x1);
+        const int iy0 = (int)std::max(0.0, y0), iy1 = (int)std::min((double)b.h - 1, y1);
+        if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > kCamBinMaxArea) {
+            tag[i] = kAll;
+            continue;
+        }
+        tag[i] = kBox;
+        box[4 * i] = ix0;
+        box[4 * i + 1] = ix1;
+        box[4 * i + 2] = iy0;
+        box[4 * i + 3] = iy1;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        if (tag[i] == kAll) b.all.push_back((int32_t)i);
+        if (tag[i] != kBox) continue;
+        for (int y = box[4 * i + 2]; y <= box[4 * i + 3]; ++y)
+            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x) ++b.off[(size_t)y * b.w + x + 1];
+    }
+    for (size_t p = 1; p < b.off.size(); ++p) b.off[p] += b.off[p - 1];
+    b.tri.resize(b.off.back());
+    std::vector<uint32_t> cur(b.off.begin(), b.off.end() - 1);
+    for (size_t i = 0; i < n; ++i) {  // (in triangle order: each pixel's list ascending)
+        if (tag[i] != kBox) continue;
+        for (int y = box[4 * i + 2]; y <= box[4 * i + 3]; ++y)
+            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x) b.tri[cur[(size_t)y * b.w + x]++] = (int32_t)i;
+    }
 }
 
 }  // namespace mpss

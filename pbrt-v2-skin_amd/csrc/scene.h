@@ -72,6 +72,24 @@ struct SceneData {
 
 void build_bvh(SceneData &s);
 
+// Candidate triangles per pixel for the reference sampler's camera rays (replay_gen.hip: whether a
+// camera ray hits anything decides how many Li draws its sample consumes). For each pixel of the
+// (xres + 1) x (yres + 1) sample extent (a sample's raster point lies in [x, x + 1) x [y, y + 1)):
+// the triangles (indices into SceneData::tris) whose raster projection's bounding box, widened by
+// kCamBinMargin pixels, meets it -- a ray through a point of the pixel can hit no other triangle in
+// front of the camera. Triangles with a vertex near or behind the camera plane, or whose box spans
+// more than kCamBinMaxArea pixels, go to `all` (tested for every pixel); triangles entirely behind
+// the camera or off the extent to neither list.
+struct CameraBins {
+    int w = 0, h = 0;            // xres + 1, yres + 1
+    std::vector<uint32_t> off;   // [w * h + 1]: pixel p's triangles are tri[off[p] .. off[p + 1])
+    std::vector<int32_t> tri;
+    std::vector<int32_t> all;
+};
+constexpr double kCamBinMargin = 1.0 / 64;
+constexpr int kCamBinMaxArea = 4096;
+void build_camera_bins(const SceneData &s, CameraBins &b);
+
 // SurfacePoint (renderers/surfacepoints.h:45-55): p, n, u, v, materialId, area, rayEpsilon.
 struct SurfacePoint {
     float p[3], n[3], u, v;

@@ -38,6 +38,10 @@ def _scene(name, lights=None, W=40, H=32, spp=4):
             a = 2 * np.pi * k / 24
             sc.lights.append(dict(center=np.array([5 * np.cos(a), -4 + 2 * np.sin(a), 3 + 0.1 * k], np.float32),
                                   radius=0.1, L=[40.0 + k, 40.0, 40.0 - k], nsamples=1 + k % 3))
+    elif lights and lights.startswith("ns="):
+        # the light's sample count (rounded up to a power of 2 by LDShuffleScrambled): the generator
+        # keeps each sample's own shuffle in registers up to 8 values, in LDS past that
+        sc.lights[0]["nsamples"] = int(lights[3:])
     return sc
 
 
@@ -73,7 +77,8 @@ def _render(torch, ctx, sc, rects):
 
 
 @pytest.mark.parametrize("name,lights,cores", [("skin.pbrt", None, 8), ("skin.pbrt", "sky+area", 8),
-                                               ("tissue.pbrt", None, 2), ("skin.pbrt", "24 spheres", 8)])
+                                               ("tissue.pbrt", None, 2), ("skin.pbrt", "24 spheres", 8),
+                                               ("skin.pbrt", "ns=5", 8), ("skin.pbrt", "ns=16", 8)])
 def test_replay_table_bit_exact(mpss, oracle, name, lights, cores):
     sc = _scene(name, lights)
     torch, ctx, o = _pair(mpss, sc, cores)

@@ -84,8 +84,9 @@ def test_texture_changes_the_image(mpss, oracle):
 def test_textured_c2_window_parity(mpss, oracle):
     """scenes/skin_textured.pbrt at the benched C2 parameters (1024x1024, 64 spp, desiredlength 512,
     minsampledistance 0.0015): imagemap albedo (gamma 2.2, scale 2, clamp) and bumpmap on the head,
-    a 32x32 cheek window through the production path vs the oracle; the tessellation with the bumped
-    normals bit-exact."""
+    a 32x32 cheek window through the production path (the common-grid gather, the textured assemble
+    fast path) vs the oracle with its own tables, irradiance and octree; the tessellation with the
+    bumped normals bit-exact."""
     import torch
     import oracle_lib
     from mpss import pbrtscene
@@ -96,10 +97,13 @@ def test_textured_c2_window_parity(mpss, oracle):
     assert m["albedo_tex"]["texels"] is not None and m["bump_tex"]["texels"] is not None
     ctx = pbrtscene.build_context(sc)
     ctx.preprocess(seed=1)
-    o = orr.OracleScene(sc, orr.tables_from_ctx(ctx, len(sc.materials)), ctx.cfg, mpss)
+    assert ctx.gather_info(0)["common_grid"]  # the production gather: far lookups from the common grid
+    o = orr.OracleScene(sc, orr.tables_from_oracle(sc), ctx.cfg, mpss)
     pts = ctx.surface_points()
     assert pts.tobytes() == o.tessellate().tobytes()
-    o.set_octree(pts, ctx.irradiance())
+    E = o.irradiance(pts, 1, nthreads=oracle_lib.nthreads())  # the oracle's own irradiance and octree
+    np.testing.assert_allclose(ctx.irradiance(), E, rtol=1e-5, atol=1e-6 * float(E.max()))
+    o.set_octree(pts, E)
     x0, x1, y0, y1 = _windows(ctx, sc.xres, sc.yres, 32, 32, lambda f: f == 1.0)
     got = _render_gpu(torch, ctx, sc, x0, x1, y0, y1, 7)
     ref = o.render_tile(sc.spp, 7, x0, x1, y0, y1, nthreads=oracle_lib.nthreads())
