@@ -172,8 +172,22 @@ __device__ void shuffle_partners(uint32_t *d, uint32_t *idx, int count) {
         d[i] = (uint32_t)i + d[i] % (uint32_t)(count - i);
     }
 }
+// The swaps are a chain through idx (one LDS round trip each); the partners are not, so they are read
+// eight at a time ahead of their swaps.
 __device__ void shuffle_swaps(const uint32_t *o, uint32_t *idx, int count) {
-    for (int i = 0; i < count; ++i) {
+    int i = 0;
+    for (; i + 8 <= count; i += 8) {
+        uint32_t p[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[k] = o[i + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t t = idx[i + k];
+            idx[i + k] = idx[p[k]];
+            idx[p[k]] = t;
+        }
+    }
+    for (; i < count; ++i) {
         const uint32_t p = o[i];
         const uint32_t t = idx[i];
         idx[i] = idx[p];
@@ -304,17 +318,19 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
         }
         }
         wave_sync();
-        // the block shuffles side by side: the image's swaps on lane 0, array a's on lane 1 + a % 63
-        // (lanes 1..63 take arrays a, a + 63, ... in turn: any light count)
-        if (skip & 2) {
-        } else if (lane == 0) {
-            shuffle_swaps(dimg, idx0, spp);
-        } else {
-            for (int a = lane - 1; a < na; a += 63) {
-                const ReplayArray A = array(a);
-                shuffle_swaps(A.d + A.hdr + spp * A.n, A.idx, spp);
+        // the block shuffles side by side, one per lane in one pass: unit 0 the image's, unit 1 + a array
+        // a's, lane l taking units l, l + 64, ... (any light count)
+        if (!(skip & 2))
+            for (int u = lane; u <= na; u += 64) {
+                const uint32_t *o = dimg;
+                uint32_t *ix = idx0;
+                if (u > 0) {
+                    const ReplayArray A = array(u - 1);
+                    o = A.d + A.hdr + spp * A.n;
+                    ix = A.idx;
+                }
+                shuffle_swaps(o, ix, spp);
             }
-        }
         wave_sync();
         // the image samples and the camera rays (samplerrenderer.cpp:97-103): only whether they hit
         int hits = 0;
