@@ -445,9 +445,7 @@ __device__ __forceinline__ void band_f(const BandLane &b, float d2, float f[4]) 
     f[3] = f23.y;
 }
 
-// RGB: slots 0..2 only (the R, G, B profiles; slot 3 is empty): no lookup for slot 3 on the LDS and
-// own-table paths (the rows carry it in the second 16-byte half either way).
-template <bool COUNT, bool RGB = false>
+template <bool COUNT>
 __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, const float *table, float d2,
                                           int hist[7]) {
     CgRec r;
@@ -472,13 +470,12 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     if (p_lds) {  // s_j < klim_j for every band: inside its LDS row
         if (lazy) band_f(b, d2, r.f);
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
-        const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]);
-        const f2v q3 = RGB ? f2v{0.f, 0.f} : lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
+        const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
 #if MPSS_MO_FUSED && MPSS_MO_TPATH
 #pragma unroll
-        for (int j = 0; j < (RGB ? 3 : 4); ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+        for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
 #endif
     }
     // (keeps the LDS step ahead of the global ones: the compiler otherwise orders the three steps its
@@ -498,21 +495,20 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     }
     if (p_own) {
         if (lazy) band_f(b, d2, r.f);
-        uint32_t otp[4] = {0u, 0u, 0u, 0u};
+        uint32_t otp[4];
 #pragma unroll
-        for (int j = 0; j < (RGB ? 3 : 4); ++j) {
+        for (int j = 0; j < 4; ++j) {
             const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
             otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
         }
         const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
         const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
-        const f2v q2 = *(gf2v *)(tb + otp[2]);
-        const f2v q3 = RGB ? f2v{0.f, 0.f} : *(gf2v *)(tb + otp[3]);
+        const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
 #if MPSS_MO_FUSED && MPSS_MO_TPATH
 #pragma unroll
-        for (int j = 0; j < (RGB ? 3 : 4); ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+        for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
 #endif
     }
     cg_count<COUNT>(b, c, d2, path, hist);
@@ -520,7 +516,6 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
 }
 
 // A record the caller has proven near for every lane (leaf_r2 < CommonGrid::lds_r2): LDS only.
-template <bool RGB = false>
 __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &c, float d2) {
     CgRec r;
     const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
@@ -530,13 +525,12 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
     r.f[2] = f23.x;
     r.f[3] = f23.y;
     const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
-    const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]);
-    const f2v q3 = RGB ? f2v{0.f, 0.f} : lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
+    const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
     r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
     r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
 #if MPSS_MO_FUSED && MPSS_MO_TPATH
 #pragma unroll
-    for (int j = 0; j < (RGB ? 3 : 4); ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+    for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
 #endif
     return r;
 }
@@ -715,7 +709,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
-                        const CgRec r = cg_fetch<COUNT, RGB>(b, cl, a.table, d2, hist);
+                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
                         cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, rk);
                     } else {
                         band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, rk);
@@ -745,7 +739,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
                         const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                         if (CG) {
-                            const CgRec ra = cg_fetch_near<RGB>(b, cl, d2a), rb = cg_fetch_near<RGB>(b, cl, d2b);
+                            const CgRec ra = cg_fetch_near(b, cl, d2a), rb = cg_fetch_near(b, cl, d2b);
                             cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, rk);
                             cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, rk);
                             continue;
@@ -776,8 +770,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float d2a = ax * ax + ay * ay + az * az;
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
                         if (CG) {
-                            const CgRec ra = cg_fetch<COUNT, RGB>(b, cl, a.table, d2a, hist);
-                            const CgRec rb = cg_fetch<COUNT, RGB>(b, cl, a.table, d2b, hist);
+                            const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
+                            const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
                             const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                             cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, rk);
                             cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, rk);
@@ -807,7 +801,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
-                        const CgRec r = cg_fetch<COUNT, RGB>(b, cl, a.table, d2, hist);
+                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
                         cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, rk);
                     } else {
                         band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, rk);

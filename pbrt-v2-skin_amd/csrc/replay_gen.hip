@@ -195,6 +195,21 @@ __device__ void shuffle_swaps(const uint32_t *o, uint32_t *idx, int count) {
     }
 }
 
+// A sample's own shuffle of 4 values (Shuffle(samp, 4, 1), the usual light-sample count): the four
+// swaps on 2-bit places of one register, the partners j + dd[j] % (4 - j) with constant divisors,
+// the result stored as one 4-byte word (sg is 4-byte aligned: the arrays' sig rows are n bytes).
+__device__ __forceinline__ void own_shuffle4(const uint32_t *dd, uint8_t *sg) {
+    const uint32_t r0 = dd[0], r1 = dd[1], r2 = dd[2];  // (dd[3] % 1 = 0: the last swap is with itself)
+    const uint32_t o[3] = {r0 & 3u, 1u + r1 % 3u, 2u + (r2 & 1u)};
+    uint32_t perm = 0xe4u;  // places 0..3 hold 0, 1, 2, 3
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const uint32_t t = ((perm >> (2 * j)) ^ (perm >> (2 * o[j]))) & 3u;
+        perm ^= (t << (2 * j)) | (t << (2 * o[j]));
+    }
+    *(uint32_t *)sg = (perm & 3u) | ((perm & 0xcu) << 6) | ((perm & 0x30u) << 12) | ((perm & 0xc0u) << 18);
+}
+
 // One of a pixel's light-sample arrays (LDShuffleScrambled1D/2D(n, spp)): its draws in stream order
 // at d -- hdr scrambles, spp x n own-shuffle draws, spp block-shuffle draws.
 struct ReplayArray {
@@ -306,6 +321,10 @@ __global__ __launch_bounds__(64 * kMaxWaves) void replay_window_kernel(RenderSce
             for (int i = lane; i < spp; i += 64) {
                 uint8_t *sg = A.sig + (size_t)i * A.n;
                 const uint32_t *dd = A.d + A.hdr + i * A.n;
+                if (A.n == 4) {
+                    own_shuffle4(dd, sg);
+                    continue;
+                }
                 for (int j = 0; j < A.n; ++j) sg[j] = (uint8_t)j;
                 for (int j = 0; j < A.n; ++j) {
                     const int o = j + (int)(dd[j] % (uint32_t)(A.n - j));

@@ -1,0 +1,20 @@
+# round 5, final measurements on the final tree: kernel trace of the C2 bench; the default bench line
+# (C2, CPU baseline, reference-sampler secondary); rgbprofile and textured C2; C3 and C5 on one GPU;
+# kernel trace of the reference-sampler C2 frame.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=r05z
+bash tools/gpu.sh $T kt bench || exit 1
+run() {  # name, bench args
+  echo "== $1"
+  timeout -k 10 600 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-secondary ${@:2} > gpurun_out/${T}_bench_$1.log 2>&1 || { echo "$1 failed"; tail -20 gpurun_out/${T}_bench_$1.log; exit 1; }
+  grep '"metric"' gpurun_out/${T}_bench_$1.log > gpurun_out/${T}_bench_$1.jsonl
+  python3 -c 'import json,sys; d=json.loads(open(sys.argv[1]).readline()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms_per_step"])' gpurun_out/${T}_bench_$1.jsonl
+}
+run c2_rgb --rgb-profile && \
+run c2_textured --scene scenes/skin_textured.pbrt && \
+run c2_replay --sampler reference && \
+bash tools/gpu.sh $T bench=c3 bench=c5 && \
+BENCH_ARGS="--sampler reference" bash tools/gpu.sh ${T}_ref kt
