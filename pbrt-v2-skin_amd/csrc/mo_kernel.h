@@ -69,7 +69,8 @@ struct DeviceProfile {
     void upload(const float *table, int L, const float *rcp, bool snake = false);
     // (upload calls it with groups, set_rgb with rows 0..2 in every group; host table [NB][L])
     // lds_reserve: floats at the end of the LDS near field the grid's split leaves free
-    void build_common(const float *table, const BandGroups &slots, int lds_reserve);
+    // rgb: the slots are the rgbprofile's R, G, B (build_common_grid)
+    void build_common(const float *table, const BandGroups &slots, int lds_reserve, bool rgb);
     // rgbprofile material: rows 0..2 of the table are its R, G, B profiles; the sharded gather looks
     // up those three for every group and converts them with FromRGB (rgb_refl: the device copy of
     // the rgbRefl2Spect tables, [7][NB]; set_rgb after upload)
@@ -89,10 +90,11 @@ constexpr double kCgAbsTol = 1e-13;
 
 // The host half of DeviceProfile::build_common: the layout (cg, without tab), the pair rows h (two
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group
-// has rows.
+// has rows. rgb: the slots are the rgbprofile's R, G, B, whose knots' errors are relative to the
+// largest of the three at that distance (the scale of FromRGB's outputs) instead of their own value.
 bool build_common_grid(const float *tab, int L, const float *rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float rel_err[NB], float l1_err[NB], int near_field = 10236,
-                       int lds_reserve = 0);
+                       int lds_reserve = 0, bool rgb = false);
 
 // Choices of the sharded gather (mpss_config.mo_near_field / mo_work_stealing; count_noprune =
 // mpss_config.count_traversal == 2, instrumented passes only).

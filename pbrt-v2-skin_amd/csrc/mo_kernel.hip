@@ -513,7 +513,7 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
     for (int c = 0; c < NB; ++c) host_rcp[c] = rcp_[c];
     groups = make_band_groups(rcp_, snake);
     rgb_refl.release();
-    build_common(tab, groups, 0);
+    build_common(tab, groups, 0, false);
 }
 
 // The common grid (mo_band.h CommonGrid), on the host from the band tables:
@@ -527,7 +527,8 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //     largest error lies on a knot of one of the two grids, and at the group grid's knots R is T's own
 //     lerp; every band knot s >= u0lim rcp_j / rg - 1 is compared (R's lerp at u = s rg / rcp_j against
 //     T[s]), and the rows end one cell before the first knot whose error exceeds kCgRelTol of |T[s]|
-//     (unfloored: a zero or a sign change ends it) -- past it every lookup reads the exact tables;
+//     (unfloored: a zero or a sign change ends it) -- past it every lookup reads the exact tables; for
+//     the rgbprofile's R, G, B (rgb) of the largest of the three at that distance instead of |T[s]|;
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
@@ -539,7 +540,7 @@ static int cg_max_rows() {
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field,
-                       int lds_reserve) {
+                       int lds_reserve, bool rgb) {
     cg = CommonGrid{};
     h.clear();
     for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
@@ -649,6 +650,27 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 const float *T = tab + (size_t)groups.band[g][j] * L;
                 for (int k = 0; k < L; ++k) peak[j] = std::max(peak[j], std::fabs((double)T[k]));
             }
+        // the value a knot's error is relative to: the band's own |T[s]|; for the rgbprofile's R, G, B
+        // (rgb) the largest of the three at that distance -- FromRGB's outputs are sums of the three
+        // with weights of order one, so each component's error counts against their scale, not its own
+        // (B, ~15x shorter reach, falls orders of magnitude under R and G soon past the near field)
+        auto scale = [&](int j, int k) -> double {
+            const float *T = tab + (size_t)groups.band[g][j] * L;
+            double v = std::fabs((double)T[k]);
+            if (!rgb) return v;
+            const double u = (double)k / r[j];
+            for (int q = 0; q < 4; ++q) {
+                const int c = groups.band[g][q];
+                if (c < 0 || q == j) continue;
+                const double f = u * r[q];
+                if (f > (double)(L - 1)) continue;
+                const int sidx = std::min((int)std::floor(f), L - 2);
+                const double t = f - sidx;
+                const float *Tq = tab + (size_t)c * L;
+                v = std::max(v, std::fabs((1.0 - t) * (double)Tq[sidx] + t * (double)Tq[sidx + 1]));
+            }
+            return v;
+        };
         auto knot_err = [&](int j, int k) -> double {  // |rows - T| at band j's knot k, inf = bad
             const float *T = tab + (size_t)groups.band[g][j] * L;
             const double u = (double)k / r[j];
@@ -656,7 +678,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             const double t = u - (double)ui;
             const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
             const double err = std::fabs(approx - (double)T[k]);
-            return err > std::max(kCgRelTol * std::fabs((double)T[k]), kCgAbsTol * peak[j]) ? INFINITY : err;
+            return err > std::max(kCgRelTol * scale(j, k), kCgAbsTol * peak[j]) ? INFINITY : err;
         };
         std::vector<double> bad;
         for (int j = 0; j < 4; ++j) {
@@ -692,9 +714,10 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 if (u < start) continue;
                 if (u >= ubad) break;
                 const double e = knot_err(j, k);
-                // (relative error where the relative bound governs: |T| >= kCgAbsTol / kCgRelTol of the peak)
-                if (kCgRelTol * std::fabs((double)T[k]) >= kCgAbsTol * peak[j])
-                    emax = std::max(emax, e / std::fabs((double)T[k]));
+                // (relative error -- to scale(): the band's own value, or the largest of R, G, B -- where
+                // the relative bound governs: scale >= kCgAbsTol / kCgRelTol of the peak)
+                const double sc = scale(j, k);
+                if (kCgRelTol * sc >= kCgAbsTol * peak[j]) emax = std::max(emax, e / sc);
                 esum += e;
             }
             cg_rel_err[c] = (float)emax;
@@ -737,20 +760,20 @@ void DeviceProfile::set_rgb(const float *tab) {
     BandGroups g3 = groups;
     for (int g = 0; g < kGroups; ++g)
         for (int j = 0; j < 4; ++j) g3.band[g][j] = j < 3 ? j : -1;
-    build_common(tab, g3, 28);  // (the LDS's last 28 floats: the groups' FromRGB weights)
+    build_common(tab, g3, 28, true);  // (the LDS's last 28 floats: the groups' FromRGB weights)
 }
 
-void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int lds_reserve) {
+void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int lds_reserve, bool rgb) {
     ctab.release();
     ctab_half.release();
     std::vector<float4> h;
-    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, cg_rel_err[1], cg_l1_err[1], 5088, lds_reserve)) {
+    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, cg_rel_err[1], cg_l1_err[1], 5088, lds_reserve, rgb)) {
         ctab_half.upload(h.data(), h.size());
         cg_half.tab = ctab_half.ptr;
     } else {
         cg_half.on = 0;
     }
-    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err[0], cg_l1_err[0], 10236, lds_reserve)) {
+    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err[0], cg_l1_err[0], 10236, lds_reserve, rgb)) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }

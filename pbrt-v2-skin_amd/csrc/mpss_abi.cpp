@@ -203,7 +203,7 @@ int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int 
         CommonGrid cg;
         std::vector<float4> h;
         float rel[NB], l1[NB];
-        *ok = build_common_grid(table, (int)L, rcp, g, cg, h, rel, l1, near_field, snake == 2 ? 28 : 0) ? 1 : 0;
+        *ok = build_common_grid(table, (int)L, rcp, g, cg, h, rel, l1, near_field, snake == 2 ? 28 : 0, snake == 2) ? 1 : 0;
         if (n_rows) {
             if (rows) require(*n_rows >= h.size() / 2, "mpss_host_common_grid: rows too small");
             *n_rows = (uint32_t)(h.size() / 2);

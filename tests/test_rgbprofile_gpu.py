@@ -89,9 +89,10 @@ def test_rgb_mo_vs_oracle(mpss, exact_mo, common_grid):
         assert np.array_equal(got == 0, ref == 0)
     else:
         # the common grid of the three profiles: the same traversal and order as the sharded gather
-        # without it (its counters equal), each far R, G, B lookup off by <= 2e-6 relative (gather_info),
-        # FromRGB's differences of the three scaling that by at most ~5: 1e-5 of each band, floored at
-        # 1e-3 of the query's largest band (_rel_close, as the spectral grid's test)
+        # without it (its counters equal), each far R, G, B lookup off by <= 2e-6 of the largest of the
+        # three at that distance (gather_info; build_common_grid's rgb scale), FromRGB's weighted
+        # differences of the three scaling that by at most ~5: 1e-5 of each band, floored at 1e-3 of
+        # the query's largest band (_rel_close, as the spectral grid's test)
         assert info["rel_err"][:3].max() <= 2e-6 and info["rel_err"][:3].max() > 0
         ctx.close()
         ctx0, _, _, _, _, _, band, cnt0 = _rgb_patch_mo(mpss, desired, exact_mo=0, mo_common_grid=0)

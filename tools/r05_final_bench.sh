@@ -1,6 +1,5 @@
 # round 5, final measurements on the final tree: kernel trace of the C2 bench; the default bench line
-# (C2, CPU baseline, reference-sampler secondary); rgbprofile and textured C2; C3 and C5 on one GPU;
-# kernel trace of the reference-sampler C2 frame.
+# (C2, CPU baseline, reference-sampler secondary); rgbprofile, textured and reference-sampler C2.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
@@ -15,6 +14,4 @@ run() {  # name, bench args
 }
 run c2_rgb --rgb-profile && \
 run c2_textured --scene scenes/skin_textured.pbrt && \
-run c2_replay --sampler reference && \
-bash tools/gpu.sh $T bench=c3 bench=c5 && \
-BENCH_ARGS="--sampler reference" bash tools/gpu.sh ${T}_ref kt
+run c2_replay --sampler reference
