@@ -333,7 +333,8 @@ def main(a):
                 "frac": None, "traffic": None, "avg_launch_ms": round(shade_launch_ms, 4),
                 "peak_source": "tools/microbench/l2_width.hip: per-lane group-row lookups (two 16-byte loads from "
                                "one 32-byte sector) from a per-XCD-resident table, 64 distinct lines per "
-                               "instruction (profiles/r05a_l2_width.json)",
+                               "instruction (profiles/r05a_l2_width.json); 0.99 L2 requests (TCP_TCC_READ_REQ) "
+                               "per lookup under PMC (profiles/r05k_l2_width_pmc.json)",
                 "algorithmic": {"achieved_gbs": round(mo_gbs, 1), "peak_gbs": HBM_PEAK_GBS,
                                 "frac": round(mo_gbs / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": mo_bytes_step / launches_per_step,
