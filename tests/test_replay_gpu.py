@@ -38,6 +38,22 @@ def _scene(name, lights=None, W=40, H=32, spp=4):
             a = 2 * np.pi * k / 24
             sc.lights.append(dict(center=np.array([5 * np.cos(a), -4 + 2 * np.sin(a), 3 + 0.1 * k], np.float32),
                                   radius=0.1, L=[40.0 + k, 40.0, 40.0 - k], nsamples=1 + k % 3))
+    elif lights == "edge geometry":
+        # the camera-ray candidate lists' edge cases (scene.h CameraBins): a strip crossing the camera
+        # plane (from behind the camera to in front of it: tested by every pixel), a wall behind the head
+        # larger than kCamBinMaxArea pixels (also every pixel), a triangle entirely behind the camera and
+        # one off the frame (in no list)
+        def tri_mesh(P, idx):
+            P = np.asarray(P, np.float32)
+            o2w = np.eye(4, dtype=np.float32)
+            return dict(P=P, N=None, S=None, uv=None, indices=np.asarray(idx, np.int32).reshape(-1, 3),
+                        o2w=o2w, w2o=o2w, reverse=False, material=0)
+        sc.meshes.append(tri_mesh([[-0.3, -7.0, -0.45], [0.3, -7.0, -0.45], [0.0, 2.0, -0.45]], [0, 1, 2]))
+        sc.meshes.append(tri_mesh([[-1.6, 1.5, -1.0], [1.6, 1.5, -1.0], [1.6, 1.5, 1.6], [-1.6, 1.5, 1.6]],
+                                  [0, 1, 2, 0, 2, 3]))
+        sc.meshes.append(tri_mesh([[0.0, -8.0, 1.0], [0.3, -8.0, 1.2], [0.0, -8.2, 1.3]], [0, 1, 2]))
+        sc.meshes.append(tri_mesh([[6.0, 0.0, 0.0], [6.3, 0.0, 0.2], [6.0, 0.2, 0.3]], [0, 1, 2]))
+        sc.integrator["minsampledistance"] = 0.05
     elif lights and lights.startswith("ns="):
         # the light's sample count (rounded up to a power of 2 by LDShuffleScrambled): the generator
         # keeps each sample's own shuffle in registers up to 8 values, in LDS past that
@@ -78,9 +94,10 @@ def _render(torch, ctx, sc, rects):
 
 @pytest.mark.parametrize("name,lights,cores", [("skin.pbrt", None, 8), ("skin.pbrt", "sky+area", 8),
                                                ("tissue.pbrt", None, 2), ("skin.pbrt", "24 spheres", 8),
-                                               ("skin.pbrt", "ns=5", 8), ("skin.pbrt", "ns=16", 8)])
+                                               ("skin.pbrt", "ns=5", 8), ("skin.pbrt", "ns=16", 8),
+                                               ("skin.pbrt", "edge geometry", 8)])
 def test_replay_table_bit_exact(mpss, oracle, name, lights, cores):
-    sc = _scene(name, lights)
+    sc = _scene(name, lights, W=128, H=96) if lights == "edge geometry" else _scene(name, lights)
     torch, ctx, o = _pair(mpss, sc, cores)
     got = ctx.replay_samples(sc.spp, sc.xres, sc.yres)
     ref = o.replay_table(sc.spp, cores=cores, li_draws=6)
