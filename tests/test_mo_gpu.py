@@ -244,8 +244,21 @@ def test_mo_common_grid_vs_oracle(oracle, mpss, torch_dev, skin_profile, cfg):
     assert info["l1_err"].max() <= 1e-7 and info["rel_err"].max() <= 2e-6
     _, _, cg, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
     _, _, band, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
-    ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
+    ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.1, counters=True)
     assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
+    # and unfloored, per query and band, from the grid's guarantee: every term's lookup within
+    # kCgRelTol (2e-6, 3e-6 here for a lerp between knots) of its value or kCgAbsTol (1e-13) of the
+    # band's peak; the fused lerp within a few ulp; each sum within (n - 1) u of its exact value (n:
+    # the records the reference visits, u = 2^-24). The terms are non-negative, so the relative parts
+    # scale the result, and the absolute part is at most 1e-13 peak_c times the E_c * area of all points
+    _, _, E, area = cloud
+    u = 2.0 ** -24
+    n = (nn + npt).astype(np.float64)[:, None]
+    peak = np.abs(table).max(axis=1).astype(np.float64)[None, :]
+    mass = (E.astype(np.float64) * area.astype(np.float64)[:, None]).sum(axis=0)[None, :]
+    bound = (3e-6 + 4 * u + 2 * n * u) * np.abs(ref) + 1e-13 * peak * mass
+    err = np.abs(cg.astype(np.float64) - ref)
+    assert np.all(err <= bound), (err / bound).max()
     if cfg.get("mo_band_dealing", 0) == 0:
         assert not np.array_equal(cg, band)  # the grid is in use (snake: its rows may lie past this cloud)
     if cfg.get("mo_work_stealing") == 0:
