@@ -33,6 +33,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 namespace mpss {
@@ -552,8 +553,14 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             if (c >= 0 && (!(host_rcp[c] > 0.f) || !std::isfinite(host_rcp[c])))
                 return false;  // no uniform grid to resample
         }
-    bool any = false;
-    for (int g = 0; g < kGroups; ++g) {
+    // The groups are independent (their own slots, LDS split, rows and errors): each is built on its
+    // own thread into its own row block, then the blocks are laid out in group order. (For the
+    // rgbprofile all groups hold the same three slots: one group is built and copied.)
+    std::vector<float4> hg[kGroups];
+    float relg[kGroups][4] = {}, l1g[kGroups][4] = {};
+    bool anyg[kGroups] = {}, failg[kGroups] = {};
+    auto build_group = [&](int g) {
+        std::vector<float4> &h = hg[g];
         float rg = INFINITY;
         int nfull = 0;
         for (int j = 0; j < 4; ++j)
@@ -561,13 +568,12 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 rg = std::min(rg, host_rcp[groups.band[g][j]]);
                 ++nfull;
             }
-        cg.row0[g] = (uint32_t)(h.size() / 2);
         if (nfull == 0) {  // an unused group: no wave ever walks it
             for (int j = 0; j < 4; ++j) {
                 cg.lrow[g][j] = (uint32_t)(2 * j);
                 cg.lcnt[g][j] = 2;
             }
-            continue;
+            return;
         }
         double r[4] = {0.0, 0.0, 0.0, 0.0}, rsum = 0.0;
         for (int j = 0; j < 4; ++j)
@@ -592,7 +598,10 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             if (total <= kLdsFloats || K0 <= 1) break;
             --K0;
         }
-        if (total > kLdsFloats) return false;
+        if (total > kLdsFloats) {
+            failg[g] = true;
+            return;
+        }
         uint32_t off = 0;
         double u0 = INFINITY;
         for (int j = 0; j < 4; ++j) {
@@ -720,8 +729,8 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                 if (kCgRelTol * sc >= kCgAbsTol * peak[j]) emax = std::max(emax, e / sc);
                 esum += e;
             }
-            cg_rel_err[c] = (float)emax;
-            cg_l1_err[c] = (float)(l1 > 0.0 ? esum / l1 : 0.0);
+            relg[g][j] = (float)emax;
+            l1g[g][j] = (float)(l1 > 0.0 ? esum / l1 : 0.0);
         }
         const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
         int64_t u1 = (int64_t)std::floor(ubad) - 1;
@@ -730,7 +739,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         cg.ubase[g] = (uint32_t)ubase;
         if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
             cg.u1lim[g] = cg.u1start[g] = u0f;
-            continue;
+            return;
         }
         cg.u1start[g] = (float)start;  // (u0f, or an integer below 2^24)
         cg.u1lim[g] = (float)u1;  // lanes with u < u1 read rows u0 <= u1 - 1 (values R(u0), R(u0 + 1))
@@ -743,7 +752,48 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             h.push_back(make_float4(v[0][0], v[0][1], v[1][0], v[1][1]));
             h.push_back(make_float4(v[2][0], v[2][1], v[3][0], v[3][1]));
         }
-        any = true;
+        anyg[g] = true;
+    };
+    bool same = rgb;  // (rgb: every group's slots are the same three profiles)
+    for (int g = 1; g < kGroups && same; ++g)
+        for (int j = 0; j < 4; ++j) same = same && groups.band[g][j] == groups.band[0][j];
+    if (same) {
+        build_group(0);
+        for (int g = 1; g < kGroups; ++g) {
+            hg[g] = hg[0];
+            for (int j = 0; j < 4; ++j) {
+                cg.lrow[g][j] = cg.lrow[0][j];
+                cg.lcnt[g][j] = cg.lcnt[0][j];
+                cg.tau[g][j] = cg.tau[0][j];
+                relg[g][j] = relg[0][j];
+                l1g[g][j] = l1g[0][j];
+            }
+            cg.u0lim[g] = cg.u0lim[0];
+            cg.rg[g] = cg.rg[0];
+            cg.lds_r2[g] = cg.lds_r2[0];
+            cg.ubase[g] = cg.ubase[0];
+            cg.u1start[g] = cg.u1start[0];
+            cg.u1lim[g] = cg.u1lim[0];
+            anyg[g] = anyg[0];
+            failg[g] = failg[0];
+        }
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < kGroups; ++g) th.emplace_back(build_group, g);
+        for (std::thread &t : th) t.join();
+    }
+    bool any = false;
+    for (int g = 0; g < kGroups; ++g) {
+        if (failg[g]) return false;
+        cg.row0[g] = (uint32_t)(h.size() / 2);
+        h.insert(h.end(), hg[g].begin(), hg[g].end());
+        any = any || anyg[g];
+        for (int j = 0; j < 4; ++j) {
+            const int c = groups.band[g][j];
+            if (c < 0) continue;
+            cg_rel_err[c] = std::max(cg_rel_err[c], relg[g][j]);
+            cg_l1_err[c] = std::max(cg_l1_err[c], l1g[g][j]);
+        }
     }
     cg.on = any ? 1 : 0;
     return any;
@@ -766,14 +816,23 @@ void DeviceProfile::set_rgb(const float *tab) {
 void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int lds_reserve, bool rgb) {
     ctab.release();
     ctab_half.release();
-    std::vector<float4> h;
-    if (build_common_grid(tab, L, host_rcp, slots, cg_half, h, cg_rel_err[1], cg_l1_err[1], 5088, lds_reserve, rgb)) {
-        ctab_half.upload(h.data(), h.size());
+    // the two LDS layouts' grids side by side (host work: each builds its groups on threads of its own)
+    std::vector<float4> hh, h;
+    bool ok_half = false;
+    std::thread half([&] {
+        ok_half = build_common_grid(tab, L, host_rcp, slots, cg_half, hh, cg_rel_err[1], cg_l1_err[1], 5088,
+                                    lds_reserve, rgb);
+    });
+    const bool ok = build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err[0], cg_l1_err[0], 10236,
+                                      lds_reserve, rgb);
+    half.join();
+    if (ok_half) {
+        ctab_half.upload(hh.data(), hh.size());
         cg_half.tab = ctab_half.ptr;
     } else {
         cg_half.on = 0;
     }
-    if (!build_common_grid(tab, L, host_rcp, slots, cg, h, cg_rel_err[0], cg_l1_err[0], 10236, lds_reserve, rgb)) {
+    if (!ok) {
         cg.on = 0;  // the per-band tables stay in use
         return;
     }
