@@ -70,11 +70,42 @@ CONFIGS = {
 }
 
 
-def kernel_source_hash():
+def _code_only(src):
+    """A C++ source without its comments and with whitespace runs collapsed: what the compiler sees,
+    so that editing a comment does not orphan the PMC summaries of unchanged code (string and char
+    literals are kept whole)."""
+    out, i, n = [], 0, len(src)
+    while i < n:
+        c = src[i]
+        if c in "\"'":
+            j = i + 1
+            while j < n and src[j] != c:
+                j += 2 if src[j] == "\\" else 1
+            out.append(src[i:j + 1])
+            i = j + 1
+        elif src.startswith("//", i):
+            j = src.find("\n", i)
+            i = n if j < 0 else j
+        elif src.startswith("/*", i):
+            j = src.find("*/", i + 2)
+            i = n if j < 0 else j + 2
+        else:
+            out.append(c)
+            i += 1
+    return " ".join("".join(out).split())
+
+
+def kernel_source_hash(read=None):
+    """Hash of the gather's sources (KERNEL_SOURCES) as code, comments and layout aside. read: a
+    function path -> text (default: the working tree)."""
     h = hashlib.sha256()
     for f in KERNEL_SOURCES:
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
+        if read is None:
+            with open(os.path.join(ROOT, f), encoding="utf-8") as fh:
+                txt = fh.read()
+        else:
+            txt = read(f)
+        h.update(_code_only(txt).encode())
     return h.hexdigest()[:16]
 
 

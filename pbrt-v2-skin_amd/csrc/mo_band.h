@@ -14,10 +14,11 @@
 // per group, so consecutive pre-order records share lines); only the table lookups are per-lane
 // gathers (one 8-byte load per band: the lerp pair).
 //
-// What bounds it: with the common grid (the default, CommonGrid below) VALU issue -- the record loop's
-// instruction count (SQ_ACTIVE_INST_VALU busy ~0.9 of the SIMDs' cycles, the measured
-// issue ceiling of this instruction mix in tools/microbench/valu_issue.hip); with the per-band tables
-// (mo_common_grid 0) the L2 request rate of the per-lane table gathers. The traversal is the UNION of
+// What bounds it: with the common grid (the default, CommonGrid below) two resources together -- the
+// vector-memory path's L2 request rate (0.84 of the rate tools/microbench/l2_width.hip sustains for the
+// grid's row loads) and VALU issue (0.80 of the rate tools/microbench/valu_issue.hip measures for this
+// record loop's instruction mix; SQ_ACTIVE_INST_VALU busy 0.82), DESIGN.md §4 "Round 5"; with the
+// per-band tables (mo_common_grid 0) the L2 request rate of the per-lane table gathers alone. The traversal is the UNION of
 // the wave's 64 pruned traversals, so the 64 queries of a wave should be neighbours: each 1024-query
 // chunk is sorted by a Morton key of the query position before queries are dealt to lanes
 // (mo_kernel.hip), and the per-record work below is kept to a few VALU on 32-bit table offsets.
