@@ -2,4 +2,4 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-bash tools/gpu.sh r05z tests smoke
+bash tools/gpu.sh r05zz tests smoke
