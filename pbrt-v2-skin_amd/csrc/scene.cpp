@@ -281,6 +281,7 @@ void build_camera_bins(const SceneData &s, CameraBins &b) {
     enum { kNone = 0, kBox = 1, kAll = 2 };
     const size_t n = s.tris.size();
     std::vector<int> box(4 * n), tag(n, kNone);
+    std::vector<double> q2(6 * n), parea(n, 0.0);  // projected vertices (raster x, y) and area
     for (size_t i = 0; i < n; ++i) {
         if (!ok) {
             tag[i] = kAll;
@@ -312,6 +313,7 @@ void build_camera_bins(const SceneData &s, CameraBins &b) {
             }
             for (int k = 0; k < 2; ++k) {
                 const double q = pr[k] / pr[3];
+                q2[6 * i + 2 * j + k] = q;
                 lo[k] = std::min(lo[k], q);
                 hi[k] = std::max(hi[k], q);
             }
@@ -331,25 +333,57 @@ void build_camera_bins(const SceneData &s, CameraBins &b) {
             continue;
         }
         tag[i] = kBox;
+        const double *q = &q2[6 * i];
+        parea[i] = 0.5 * ((q[2] - q[0]) * (q[5] - q[1]) - (q[4] - q[0]) * (q[3] - q[1]));
         box[4 * i] = ix0;
         box[4 * i + 1] = ix1;
         box[4 * i + 2] = iy0;
         box[4 * i + 3] = iy1;
     }
+    // Pixel (x, y) -- widened by kCamBinMargin -- against triangle i beyond its box: separated when all
+    // four corners lie strictly outside one of its projected edges (the separating-axis test of a
+    // triangle and a square; the box test is the square's own axes). Projections of (nearly) zero
+    // area keep the whole box.
+    auto meets = [&](size_t i, int x, int y) {
+        const double A = parea[i];
+        if (!(std::fabs(A) > 1e-6)) return true;
+        const double *q = &q2[6 * i];
+        const double sg = A > 0.0 ? 1.0 : -1.0;
+        const double cx[4] = {x - kCamBinMargin, x + 1 + kCamBinMargin, x - kCamBinMargin, x + 1 + kCamBinMargin};
+        const double cy[4] = {y - kCamBinMargin, y - kCamBinMargin, y + 1 + kCamBinMargin, y + 1 + kCamBinMargin};
+        for (int e = 0; e < 3; ++e) {
+            const double ax = q[2 * e], ay = q[2 * e + 1];
+            const double bx = q[2 * ((e + 1) % 3)], by = q[2 * ((e + 1) % 3) + 1];
+            bool all_out = true;
+            for (int k = 0; k < 4 && all_out; ++k)
+                all_out = sg * ((bx - ax) * (cy[k] - ay) - (by - ay) * (cx[k] - ax)) < 0.0;
+            if (all_out) return false;
+        }
+        return true;
+    };
     for (size_t i = 0; i < n; ++i) {
         if (tag[i] == kAll) b.all.push_back((int32_t)i);
         if (tag[i] != kBox) continue;
         for (int y = box[4 * i + 2]; y <= box[4 * i + 3]; ++y)
-            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x) ++b.off[(size_t)y * b.w + x + 1];
+            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x)
+                if (meets(i, x, y)) ++b.off[(size_t)y * b.w + x + 1];
     }
     for (size_t p = 1; p < b.off.size(); ++p) b.off[p] += b.off[p - 1];
     b.tri.resize(b.off.back());
     std::vector<uint32_t> cur(b.off.begin(), b.off.end() - 1);
-    for (size_t i = 0; i < n; ++i) {  // (in triangle order: each pixel's list ascending)
+    for (size_t i = 0; i < n; ++i) {
         if (tag[i] != kBox) continue;
         for (int y = box[4 * i + 2]; y <= box[4 * i + 3]; ++y)
-            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x) b.tri[cur[(size_t)y * b.w + x]++] = (int32_t)i;
+            for (int x = box[4 * i]; x <= box[4 * i + 1]; ++x)
+                if (meets(i, x, y)) b.tri[cur[(size_t)y * b.w + x]++] = (int32_t)i;
     }
+    // each pixel's list by projected area, largest first: a camera ray stops at its first hit, and the
+    // wave once every lane has one, so the triangles covering most of the pixel go first (the answer
+    // does not depend on the order)
+    for (size_t p = 0; p + 1 < b.off.size(); ++p)
+        if (b.off[p + 1] - b.off[p] > 1)
+            std::stable_sort(b.tri.begin() + b.off[p], b.tri.begin() + b.off[p + 1],
+                             [&](int32_t u, int32_t v) { return std::fabs(parea[u]) > std::fabs(parea[v]); });
 }
 
 }  // namespace mpss

@@ -75,9 +75,9 @@ void build_bvh(SceneData &s);
 // Candidate triangles per pixel for the reference sampler's camera rays (replay_gen.hip: whether a
 // camera ray hits anything decides how many Li draws its sample consumes). For each pixel of the
 // (xres + 1) x (yres + 1) sample extent (a sample's raster point lies in [x, x + 1) x [y, y + 1)):
-// the triangles (indices into SceneData::tris) whose raster projection's bounding box, widened by
-// kCamBinMargin pixels, meets it -- a ray through a point of the pixel can hit no other triangle in
-// front of the camera. Triangles with a vertex near or behind the camera plane, or whose box spans
+// the triangles (indices into SceneData::tris) whose raster projection, widened by kCamBinMargin
+// pixels, meets it (its box, then its edges) -- a ray through a point of the pixel can hit no other
+// triangle in front of the camera -- largest projected area first. Triangles with a vertex near or behind the camera plane, or whose box spans
 // more than kCamBinMaxArea pixels, go to `all` (tested for every pixel); triangles entirely behind
 // the camera or off the extent to neither list.
 struct CameraBins {
