@@ -439,6 +439,7 @@ def main(a):
                            "mo_common_grid": bool(ctx.gather_info(0)["common_grid"]) if sc.materials else False,
                            "mo_lane_records": {"rows": cnt["mo_row_lane_records"], "lds": cnt["mo_lds_lane_records"],
                                                   "tables": cnt["mo_table_lane_records"]},
+                           "mo_l2_footprint": l2_footprint(cnt),
                            "mo_visits": {"node": cnt["mo_nodes"], "point": cnt["mo_points"],
                                          "lookups_in_profile": cnt["mo_lookups"]}},
                 "roofline": roofline, "cpu_baseline": cpu}
@@ -455,6 +456,27 @@ def main(a):
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def l2_footprint(cnt):
+    """The count pass's L2 footprint of the gather's far lookups by path (mo_band.h kHist 7..12): per band
+    group, lane-records on the group rows / LDS / own tables, and for the rows and own tables the distinct
+    32-byte sectors and 128-byte lines their loads touch, summed over wave fetches (what the
+    vector-memory path asks of L2), and the wave fetches. Per SSS sample in "per_sss_sample"."""
+    ns = max(1, cnt["sss_samples"])
+    rec = cnt["group_path_records"]
+    out = {"per_group": [{"records": rec[g], "sectors": cnt["group_path_sectors"][g],
+                          "lines": cnt["group_path_lines"][g], "fetches": cnt["group_path_fetches"][g]}
+                         for g in range(8)]}
+    tot = {}
+    for i, path in enumerate(("rows", "tables")):
+        tot[path] = {k: int(sum(cnt["group_path_" + k][g][i] for g in range(8)))
+                     for k in ("sectors", "lines", "fetches")}
+        tot[path]["records"] = int(sum(rec[g][0 if i == 0 else 2] for g in range(8)))
+    tot["lds"] = {"records": int(sum(rec[g][1] for g in range(8)))}
+    out["total"] = tot
+    out["per_sss_sample"] = {p: {k: round(v / ns, 1) for k, v in d.items()} for p, d in tot.items()}
+    return out
 
 
 def c3_strong_secondary(a, rank, world, local):

@@ -334,6 +334,11 @@ typedef struct {
     int64_t n_tex;
     double ms_replay;     /* the reference sampler's values of each batch's window (replay_window) */
     int64_t n_replay;
+    /* count_traversal with the common grid, per band group: lane-records by path (group rows, LDS,
+     * own tables), and the L2 footprint of the row / own-table fetches -- distinct 32-byte sectors and
+     * 128-byte lines the active lanes' loads touch, summed over wave fetches -- and the wave fetches */
+    int64_t group_path_records[8][3];
+    int64_t group_path_sectors[8][2], group_path_lines[8][2], group_path_fetches[8][2];
 } mpss_render_stats;
 int mpss_get_render_stats(mpss_ctx *ctx, mpss_render_stats *out);
 /* Switch kernel_timing / count_traversal (0, 1 or 2, as mpss_config) after creation
@@ -403,7 +408,8 @@ int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, 
  * knots each band reads from the rows); *ok = 1 when some group has rows. */
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, int near_field, float *rows,
                           uint32_t *n_rows, int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start,
-                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, int *ok);
+                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, float *ua, float *hinv,
+                          int *ok);
 /* Octree build + pre-order export (sizes first with NULL outputs). */
 int mpss_host_octree_export(uint32_t n, const float *p, const float *nrm, const float *E, const float *area,
                             uint32_t *n_nodes, float *node_p, float *node_area, float *node_et, int32_t *depth,

@@ -27,37 +27,25 @@
 // minus subtrees that lie past the end of all of the group's profiles (they add +0 for these
 // bands), in pre-order, with the packet kernel's summation order. With the per-band tables the
 // results are bit-identical to mo_packet_traverse (one running sum per band, a leaf's points summed
-// first); the common grid resamples the far lookups (within kCgRelTol / kCgAbsTol per value) and, with
-// MPSS_MO_FUSED, forms each term with FMAs, so its sums are within the float-summation bound of the
-// reference (tests/test_mo_gpu.py) rather than bit-identical to it.
+// first); the common grid resamples the far lookups (within kCgRelTol / kCgAbsTol per value) and forms
+// each term with FMAs (cg_combine), so its sums are within the float-summation bound of the reference
+// (tests/test_mo_gpu.py) rather than bit-identical to it.
 #pragma once
 #include <cstdlib>
 
 #include "common.h"
 #include "octree.h"
 
-// MPSS_MO_FUSED (default 1): the common-grid gather forms each Rd as a + t (b - a) with one FMA and
-// accumulates Rd * (E * area) with one FMA per band (cg_combine) -- fewer and cheaper VALU
-// instructions on the record loop the gather's time is made of. 0: the reference's operation order,
-// (1 - t) a + t b and (Rd * E) * area, as the per-band gather keeps (for A/B builds).
-#ifndef MPSS_MO_FUSED
-#define MPSS_MO_FUSED 1
-#endif
-// MPSS_MO_TPATH (default 1, with MPSS_MO_FUSED): each path of the common-grid fetch forms its own lerp
-// parameters -- the rows one fract(u) for the four bands, the LDS and own-table lanes fract(d2 rcp_j)
-// per band -- so a wave whose lanes all read rows pays one fract instead of four (CgRec::f then holds t).
-#ifndef MPSS_MO_TPATH
-#define MPSS_MO_TPATH 1
-#endif
-// MPSS_MO_LAZYF (default 1, with MPSS_MO_TPATH): the per-band indices d2 * rcp_j are formed inside the
-// LDS and own-table steps that use them, so a wave whose lanes all read rows forms none.
-#ifndef MPSS_MO_LAZYF
-#define MPSS_MO_LAZYF 1
-#endif
-
 namespace mpss {
 
 constexpr int kGroups = 8;
+// Per-lane traversal counters of the instrumented (COUNT) gather, summed into mo_kernel.h's counts:
+// 0 table lookups inside the profile (lane x band), 1..3 those at entries < 4096, 8192, 16384;
+// common grid only: 4..6 lane-records by path (group rows, LDS near field, the bands' own tables);
+// 7..8 distinct 32-byte sectors and 9..10 distinct 128-byte lines the path's loads touch, summed
+// over wave fetches (rows, own tables: what the vector-memory path asks of L2); 11..12 wave fetches
+// with a lane on the path (rows, own tables).
+constexpr int kHist = 13;
 
 // Band -> (group, slot) assignment and per-group pruning scale.
 struct BandGroups {
@@ -113,26 +101,32 @@ inline bool same_groups(const BandGroups &a, const BandGroups &b) {
 // lookup of all <= 4 bands of the group past their LDS near fields from ONE interleaved table. The
 // group's tables are resampled onto the grid of its longest-reach band (rg = its rcpDsqSpacing, for
 // which the resampling is the identity), u = d2 * rg, and stored as 32-byte pair rows
-// {R_0(u), R_0(u+1), R_1(u), R_1(u+1)}, {R_2(u), R_2(u+1), R_3(u), R_3(u+1)}: a lookup is two 16-byte
-// loads from one 32-byte-aligned sector per lane instead of four 8-byte lerp pairs from four
-// unrelated offsets (the gather is bound by the L2 request rate of these per-lane loads, DESIGN.md
-// §4). Each lane takes one of three paths by u:
+// {R_0(u_k), R_0(u_k+1), R_1(u_k), R_1(u_k+1)}, {R_2(u_k), ...}: a lookup is two 16-byte loads from one
+// 32-byte-aligned sector per lane instead of four 8-byte lerp pairs from four unrelated offsets (the
+// gather is bound by the L2 request rate of these per-lane loads). Row k sits at u_k = k
+// below ua and at ua + H (k - ua) above it (H = 1, 2 or 4 per group): the lane's row coordinate is
+// v = min(u, fma(u, hinv, hc)), hc = ua (1 - hinv), its row floor(v) and its lerp parameter fract(v), so
+// a group's rows can reach its profile end inside kCgMaxRows where the tables are smooth enough for
+// the coarser steps. Each lane takes one of three paths by u:
 //   u < u0lim          every band's exact pair from its LDS near field (as the per-band gather);
-//   u1start <= u < u1lim the group rows -- only where the resampling is accurate: build_common
-//                      measures the error at every band's own grid knots and ends the range before
-//                      the first knot off by more than kCgRelTol of the band's local value (the
-//                      tables' far tails carry the MPC resampler's kinks and float noise a coarser
-//                      grid cannot follow); u1start = u0lim, or (bands of widely different reach,
-//                      the rgbprofile's R, G, B) past the end of the bands the grid cannot follow;
+//   u1start <= u < u1lim the group rows -- accurate wherever they are read: build_common measures the
+//                      error at every band's own knots, and a cell (row) holding a knot off by more
+//                      than the bound carries a NaN in its first value: its lanes read the bands' own
+//                      tables instead (cg_fix). The range is the one serving the most records from
+//                      good cells (the far tails of the longest-reach bands carry the MPC resampler's
+//                      float noise, which no coarser grid follows: there every cell is bad);
 //   otherwise          every band's exact pair from its own table in HBM/L2 (as the per-band gather).
 struct CommonGrid {
     const float4 *tab;          // pair rows, two float4 each; group g's row for u at 2 * (row0[g] + u - ubase[g])
     uint32_t row0[kGroups];     // group g's first pair row
-    uint32_t ubase[kGroups];    // the u of that row
+    uint32_t ubase[kGroups];    // the v (row coordinate) of that row
     float rg[kGroups];          // the group's grid: u = d2 * rg (its smallest rcp)
     float u0lim[kGroups];       // u < u0lim => every band's pair (s, s + 1) lies in its LDS near field
     float u1lim[kGroups];       // u1start <= u < u1lim: the pair rows (u1lim = u0lim: none)
     float u1start[kGroups];     // (u0lim, or past the end of the bands the rows cannot serve)
+    float ua[kGroups];          // rows one grid step apart below ua, H steps apart above (L: none)
+    float hinv[kGroups];        // 1 / H
+    float hc[kGroups];          // ua (1 - 1 / H): v = min(u, fma(u, hinv, hc)) (exact: ua a multiple of 64)
     float tau[kGroups][4];      // d2 >= tau <=> fl(d2 * rcp) >= L - 1: the band is past its profile end
     uint32_t lrow[kGroups][4];  // float offset of slot j's near-field row in LDS (entries 0..klim_j)
     int lcnt[kGroups][4];       // its length, klim_j + 1 floats (2 zeros for an empty slot)
@@ -234,7 +228,7 @@ __host__ __device__ constexpr int near_row() {
 // (how much a near-field copy of that many entries per band in LDS would absorb).
 // The fetch half: f per band and the four pair loads (issued, not consumed).
 template <bool COUNT, int KLDS>
-__device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float f[4], RdPair v[4], int hist[7]) {
+__device__ __forceinline__ void band_rd_fetch(const BandLane &b, float d2, float f[4], RdPair v[4], int hist[kHist]) {
     const f2v f01 = f2v{d2, d2} * f2v{b.rcp[0], b.rcp[1]};
     const f2v f23 = f2v{d2, d2} * f2v{b.rcp[2], b.rcp[3]};
     f[0] = f01.x;
@@ -346,7 +340,7 @@ __device__ __forceinline__ void from_rgb4(lds_float *rk, float R, float G, float
     }
 }
 
-// from_rgb4 for the common-grid gather (MPSS_MO_FUSED): rk holds the weights times .94, the LDS offsets of
+// from_rgb4 for the common-grid gather (cg_combine): rk holds the weights times .94, the LDS offsets of
 // the X and Y rows come from two selects each, and each band is .94 W min + .94 X (mid - min) + .94 Y
 // (max - mid) as one multiply and two FMAs (packed, two bands per instruction), clamped at 0 -- within an
 // ulp or two of FromRGB's own sum (the far values are a resampling already).
@@ -391,9 +385,10 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
 // ---- the common-grid gather (CommonGrid) ----
 // The lane's (wave-uniform) view of its group's grid.
 struct CgLane {
-    const float4 *tab;    // the pair rows, indexed by u0 + rowoff
+    const float4 *tab;    // the pair rows, indexed by floor(v) + rowoff
     uint32_t rowoff;      // row0 - ubase (mod 2^32)
     float rg, u0lim, u1lim, u1start;
+    float hinv, hc;       // v = min(u, fma(u, hinv, hc))
     float tau[4];
     float tau_min;        // the group's first profile end
     uint32_t lrow[4];     // LDS float offsets of the slots' exact near-field rows
@@ -417,7 +412,7 @@ typedef const __attribute__((address_space(1))) f4v gf4v;
 typedef const __attribute__((address_space(1))) f2v gf2v __attribute__((aligned(4)));
 
 template <bool COUNT>
-__device__ __forceinline__ void cg_count(const BandLane &b, const CgLane &c, float d2, int path, int hist[7]) {
+__device__ __forceinline__ void cg_count(const BandLane &b, const CgLane &c, float d2, int path, int hist[kHist]) {
     if (!COUNT) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -429,6 +424,30 @@ __device__ __forceinline__ void cg_count(const BandLane &b, const CgLane &c, flo
         hist[3] += s < 16384u;
     }
     hist[4 + path] += 1;  // 4: group rows, 5: LDS, 6: the bands' own tables
+}
+
+// COUNT: how many distinct keys (sector or line numbers) the active lanes hold, each lane holding k0 and,
+// if it differs, k1 (a load that straddles two) -- counted once per wave, by its first active lane.
+__device__ inline int wave_distinct(uint64_t k0, uint64_t k1) {
+    uint64_t m0 = __builtin_amdgcn_ballot_w64(true);
+    uint64_t m1 = __builtin_amdgcn_ballot_w64(k1 != k0);
+    int n = 0;
+    while (m0 | m1) {
+        const uint64_t m = m0 ? m0 : m1;
+        const int l = __builtin_ctzll(m);
+        const bool from0 = m0 != 0;
+        const uint64_t mine = from0 ? k0 : k1;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)mine, l);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(mine >> 32), l);
+        const uint64_t key = ((uint64_t)hi << 32) | lo;
+        m0 &= ~__builtin_amdgcn_ballot_w64(k0 == key);
+        m1 &= ~__builtin_amdgcn_ballot_w64(k1 == key);
+        ++n;
+    }
+    return n;
+}
+__device__ __forceinline__ bool first_active_lane() {
+    return (int)(threadIdx.x & 63) == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true));
 }
 
 __device__ __forceinline__ f2v lds_pair(const BandLane &b, uint32_t k) {
@@ -447,11 +466,60 @@ __device__ __forceinline__ void band_f(const BandLane &b, float d2, float f[4]) 
 }
 
 template <bool COUNT>
+__device__ __forceinline__ void cg_count_rows(uint64_t addr, int hist[kHist]) {
+    const int ns = wave_distinct(addr >> 5, addr >> 5), nl = wave_distinct(addr >> 7, addr >> 7);
+    if (first_active_lane()) {
+        hist[7] += ns;
+        hist[9] += nl;
+        hist[11] += 1;
+    }
+}
+template <bool COUNT>
+__device__ __forceinline__ void cg_count_own(const uint64_t addr[4], int hist[kHist]) {
+    int ns = 0, nl = 0;
+    for (int j = 0; j < 4; ++j) {  // one 8-byte load per band
+        ns += wave_distinct(addr[j] >> 5, (addr[j] + 7) >> 5);
+        nl += wave_distinct(addr[j] >> 7, (addr[j] + 7) >> 7);
+    }
+    if (first_active_lane()) {
+        hist[8] += ns;
+        hist[10] += nl;
+        hist[12] += 1;
+    }
+}
+
+// every band's exact pair from its own table (the u >= u1lim path, and cg_fix)
+template <bool COUNT>
+__device__ __forceinline__ void cg_own(const BandLane &b, const CgLane &c, const float *table, float d2, CgRec &r,
+                                       int hist[kHist]) {
+    band_f(b, d2, r.f);
+    uint32_t otp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
+        otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
+    }
+    const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
+    const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
+    const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
+    if (COUNT) {
+        const uint64_t ad[4] = {(uint64_t)(uintptr_t)table + otp[0], (uint64_t)(uintptr_t)table + otp[1],
+                                (uint64_t)(uintptr_t)table + otp[2], (uint64_t)(uintptr_t)table + otp[3]};
+        cg_count_own<COUNT>(ad, hist);
+    }
+    r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
+    r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
+}
+
+template <bool COUNT>
 __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, const float *table, float d2,
-                                          int hist[7]) {
+                                          int hist[kHist]) {
+    // Each path forms its own lerp parameters (CgRec::f holds t on return): the rows one fract(u) for
+    // the four bands, the LDS and own-table lanes fract(d2 rcp_j) per band, the per-band indices
+    // d2 * rcp_j only inside the steps that use them -- a wave whose lanes all read rows forms none.
     CgRec r;
-    constexpr bool lazy = MPSS_MO_FUSED && MPSS_MO_TPATH && MPSS_MO_LAZYF;
-    if (!lazy) band_f(b, d2, r.f);
     const float u = d2 * c.rg;
     // Three sequential masked steps, LDS first: a later step's loads may overwrite registers an
     // earlier step's loads target only once those have returned, and LDS returns first (the
@@ -466,18 +534,17 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // the row step's address up front, as a 32-bit byte offset from the (wave-uniform) grid base: one
     // VGPR, a global load in saddr form. (The own-table step's four addresses are formed in its branch:
     // with the gather VALU-bound, a wave whose lanes all take the rows or the LDS does not pay them.)
-    uint32_t orow = 32u * ((uint32_t)u + c.rowoff);
+    const float v = __builtin_fminf(u, __builtin_fmaf(u, c.hinv, c.hc));
+    uint32_t orow = 32u * ((uint32_t)v + c.rowoff);
     asm volatile("" : "+v"(orow));
     if (p_lds) {  // s_j < klim_j for every band: inside its LDS row
-        if (lazy) band_f(b, d2, r.f);
+        band_f(b, d2, r.f);
         const f2v q0 = lds_pair(b, c.lrow[0] + (uint32_t)r.f[0]), q1 = lds_pair(b, c.lrow[1] + (uint32_t)r.f[1]);
         const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
         r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
         r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
-#if MPSS_MO_FUSED && MPSS_MO_TPATH
 #pragma unroll
         for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
-#endif
     }
     // (keeps the LDS step ahead of the global ones: the compiler otherwise orders the three steps its
     // own way and puts the LDS step last)
@@ -486,34 +553,34 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
         gf4v *row = (gf4v *)((const __attribute__((address_space(1))) char *)c.tab + orow);
         r.p01 = row[0];
         r.p23 = row[1];
-#if MPSS_MO_FUSED && MPSS_MO_TPATH
-        const float t = __builtin_amdgcn_fractf(u);  // one lerp parameter for the four bands
-#else
-        const float t = u;
-#endif
+        if (COUNT) cg_count_rows<COUNT>((uint64_t)(uintptr_t)c.tab + orow, hist);
+        const float t = __builtin_amdgcn_fractf(v);  // one lerp parameter for the four bands
 #pragma unroll
         for (int j = 0; j < 4; ++j) r.f[j] = t;
     }
-    if (p_own) {
-        if (lazy) band_f(b, d2, r.f);
-        uint32_t otp[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
-            otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
-        }
-        const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
-        const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
-        const f2v q2 = *(gf2v *)(tb + otp[2]), q3 = *(gf2v *)(tb + otp[3]);
-        r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
-        r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
-#if MPSS_MO_FUSED && MPSS_MO_TPATH
-#pragma unroll
-        for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
-#endif
-    }
+    if (p_own) cg_own<COUNT>(b, c, table, d2, r, hist);
     cg_count<COUNT>(b, c, d2, path, hist);
     return r;
+}
+
+// A lane whose group row is flagged bad (a NaN first value: build_common_grid) reads every band's exact
+// pair from its own table instead -- after the row has arrived, so only waves with such a lane wait a
+// second round trip. Called for a record's (or a point pair's) fetches before they are combined. (The
+// tables hold no NaN, so a lane of the LDS or own-table path never takes it.)
+template <bool COUNT>
+__device__ __forceinline__ void cg_fix(const BandLane &b, const CgLane &c, const float *table, float d2, CgRec &r,
+                                       int hist[kHist]) {
+    const bool bad = r.p01.x != r.p01.x;
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 && bad) cg_own<COUNT>(b, c, table, d2, r, hist);
+}
+template <bool COUNT>
+__device__ __forceinline__ void cg_fix2(const BandLane &b, const CgLane &c, const float *table, float d2a,
+                                        CgRec &ra, float d2b, CgRec &rb, int hist[kHist]) {
+    const bool bad_a = ra.p01.x != ra.p01.x, bad_b = rb.p01.x != rb.p01.x;
+    if (__builtin_amdgcn_ballot_w64(bad_a || bad_b) != 0) {
+        if (bad_a) cg_own<COUNT>(b, c, table, d2a, ra, hist);
+        if (bad_b) cg_own<COUNT>(b, c, table, d2b, rb, hist);
+    }
 }
 
 // A record the caller has proven near for every lane (leaf_r2 < CommonGrid::lds_r2): LDS only.
@@ -529,10 +596,8 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
     const f2v q2 = lds_pair(b, c.lrow[2] + (uint32_t)r.f[2]), q3 = lds_pair(b, c.lrow[3] + (uint32_t)r.f[3]);
     r.p01 = f4v{q0.x, q0.y, q1.x, q1.y};
     r.p23 = f4v{q2.x, q2.y, q3.x, q3.y};
-#if MPSS_MO_FUSED && MPSS_MO_TPATH
 #pragma unroll
     for (int j = 0; j < 4; ++j) r.f[j] = __builtin_amdgcn_fractf(r.f[j]);
-#endif
     return r;
 }
 
@@ -540,53 +605,39 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 // gather's, the group rows' on the group grid -- then its range test (multipole.cpp:65-66) as
 // d2 >= tau: only lanes off the LDS path can be past a band's end, and only at the group's reach, so
 // the test runs when some lane of the wave is past the group's first end.
-// MPSS_MO_FUSED: e is E * area for a point (BandTree::band_ew) and Et for a node, w unused.
+// e is E * area for a point (BandTree::band_ew) and Et for a node, w unused.
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
                                            f2v acc[2], lds_float *rk = nullptr) {
     float rd[4];
     const RdPair v[4] = {{r.p01.x, r.p01.y}, {r.p01.z, r.p01.w}, {r.p23.x, r.p23.y}, {r.p23.z, r.p23.w}};
-#if MPSS_MO_FUSED
     // a + t (b - a), one rounding after the product: within an ulp or two of the reference's
     // (1 - t) a + t b (the far values are a resampling already)
     // (written out: packed, the four bands' (a, b) pairs would first be shuffled into (a0, a1), (b0, b1)
     // register pairs -- three v_mov per two bands, more than the packing saves)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float t = MPSS_MO_TPATH ? r.f[j] : __builtin_amdgcn_fractf(r.f[j]);  // (TPATH: fetched as t)
+        const float t = r.f[j];  // (cg_fetch returns t)
         float d;
         asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(v[j].b), "v"(v[j].a));
         asm("v_fma_f32 %0, %1, %2, %3" : "=v"(rd[j]) : "v"(t), "v"(d), "v"(v[j].a));
     }
-#else
-    band_rd_lerp(r.f, v, rd);
-#endif
     if (__builtin_amdgcn_ballot_w64(d2 >= c.tau_min) != 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
     }
     float o[4];
-    if (RGB) {  // slots 0..2: the R, G, B profiles on the grid
-#if MPSS_MO_FUSED
-        from_rgb4_fused(rk, rd[0], rd[1], rd[2], o);
-#else
-        from_rgb4(rk, rd[0], rd[1], rd[2], o);
-#endif
-    }
+    if (RGB) from_rgb4_fused(rk, rd[0], rd[1], rd[2], o);  // slots 0..2: the R, G, B profiles on the grid
     const float *x = RGB ? o : rd;
-#if MPSS_MO_FUSED
     (void)w;
 #pragma unroll
     for (int h = 0; h < 2; ++h)  // acc += Rd * (E area), one packed FMA per two bands
         acc[h] = __builtin_elementwise_fma(f2v{x[2 * h], x[2 * h + 1]}, f2v{e[2 * h], e[2 * h + 1]}, acc[h]);
-#else
-    band_rd_products<POINT>(x, e, w, acc);
-#endif
 }
 
 template <bool POINT, bool COUNT, int KLDS, bool RGB = false>
 __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, const float e[4], float w, f2v acc[2],
-                                                   int hist[7], lds_float *rk = nullptr) {
+                                                   int hist[kHist], lds_float *rk = nullptr) {
     float f[4];
     RdPair v[4];
     band_rd_fetch<COUNT, KLDS>(b, d2, f, v, hist);
@@ -594,26 +645,13 @@ __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, 
 }
 
 // sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d) (v_rcp_f32,
-// <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20 relative either way. (MPSS_MO_DWMUL = 1:
-// a against the products d * m (1 -+ 2^-20) instead -- a < fl(d m_lo) puts the true quotient below
-// m (1 - 2^-21), a > fl(d m_hi) above m (1 + 2^-21) -- two plain multiplies for v_rcp; measured equal,
-// profiles/r05g_dwmul_ab.txt.) The rare near-ties (and NaN / inf) take the exact division, so the decision
-// is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
-#ifndef MPSS_MO_DWMUL
-#define MPSS_MO_DWMUL 0
-#endif
+// <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20 relative either way (m_lo, m_hi). The
+// rare near-ties (and NaN / inf) take the exact division, so the decision is always that of
+// fl(sum_area / d2) < max_error (diffusionutil.h:182).
 __device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, float m_hi) {
-#if MPSS_MO_DWMUL
-    bool below = a < d * m_lo;
-    const bool sure = below || a > d * m_hi;
-#else
-    (void)m_lo;
-    (void)m_hi;
     const float r = a * __builtin_amdgcn_rcpf(d);
-    const float lo = m * (1.f - 0x1p-20f), hi = m * (1.f + 0x1p-20f);
-    bool below = r < lo;
-    const bool sure = below || r > hi;
-#endif
+    bool below = r < m_lo;
+    const bool sure = below || r > m_hi;
     if (!sure) below = (a / d) < m;
     return below;
 }
@@ -629,7 +667,7 @@ __device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, 
 template <bool COUNT, int KLDS, bool VROWS, bool CG = false, bool RGB = false>
 __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, float px, float py, float pz, bool valid,
                                                  float out[4], int &k_nodes, int &k_pts, int &w_nodes, int &w_pts,
-                                                 int hist[7], const float *lt) {
+                                                 int hist[kHist], const float *lt) {
     BandLane b;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -654,6 +692,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         cl.u0lim = a.cg.u0lim[grp];
         cl.u1lim = a.cg.u1lim[grp];
         cl.u1start = a.cg.u1start[grp];
+        cl.hinv = a.cg.hinv[grp];
+        cl.hc = a.cg.hc[grp];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             cl.tau[j] = a.cg.tau[grp][j];
@@ -673,7 +713,7 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     const float box_lim = a.prune_f / a.groups.rcp_min[grp];
     const cptr<float4> et_g = as_const(a.band_et + (size_t)grp * a.n_nodes);
     // (the common-grid gather's fused products read E * area)
-    const cptr<float4> e_g = as_const(((CG && MPSS_MO_FUSED) ? a.band_ew : a.band_e) + (size_t)grp * a.n_points);
+    const cptr<float4> e_g = as_const((CG ? a.band_ew : a.band_e) + (size_t)grp * a.n_points);
     const cptr<NodeHdr> nodes = as_const(a.nodes);
     const cptr<float4> pt_hdr = as_const(a.pt_hdr);
     int resume = valid ? 0 : 0x7fffffff;
@@ -710,7 +750,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float4 et = et_g[node];
                     const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
-                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        cg_fix<COUNT>(b, cl, a.table, d2, r, hist);
                         cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, rk);
                     } else {
                         band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, rk);
@@ -771,8 +812,9 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                         const float d2a = ax * ax + ay * ay + az * az;
                         const float d2b = bx2 * bx2 + by2 * by2 + bz2 * bz2;
                         if (CG) {
-                            const CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
-                            const CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
+                            CgRec ra = cg_fetch<COUNT>(b, cl, a.table, d2a, hist);
+                            CgRec rb = cg_fetch<COUNT>(b, cl, a.table, d2b, hist);
+                            cg_fix2<COUNT>(b, cl, a.table, d2a, ra, d2b, rb, hist);
                             const float e0[4] = {ea.x, ea.y, ea.z, ea.w}, e1[4] = {eb.x, eb.y, eb.z, eb.w};
                             cg_combine<true, RGB>(cl, ra, d2a, e0, pa.w, lacc, rk);
                             cg_combine<true, RGB>(cl, rb, d2b, e1, pb.w, lacc, rk);
@@ -802,7 +844,8 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     const float4 ev = e_g[kp];
                     const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
-                        const CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        cg_fix<COUNT>(b, cl, a.table, d2, r, hist);
                         cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, rk);
                     } else {
                         band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, rk);

@@ -86,7 +86,10 @@ struct DeviceProfile {
 // 0: gather 60.4 ms, unfloored image error 1.1e-6; 1e-13: 48.6 ms, 4.3e-6; 1e-10: 47.1 ms, 9.0e-5
 // (all three at values far below the film's resolution, 1e-16 of the frame's peak).
 constexpr double kCgRelTol = 2e-6;
-constexpr double kCgAbsTol = 1e-13;
+#ifndef MPSS_CG_ABS_TOL  // (A/B builds of the floor only)
+#define MPSS_CG_ABS_TOL 1e-13
+#endif
+constexpr double kCgAbsTol = MPSS_CG_ABS_TOL;
 
 // The host half of DeviceProfile::build_common: the layout (cg, without tab), the pair rows h (two
 // float4 per row, group by group from cg.row0) and the per-band errors; true (cg.on) when some group
@@ -134,8 +137,9 @@ void launch_mo_rgb(const DeviceOctree &t, const float *table3, const float *rcp3
 // point iterations (summed over waves; 64 x these / the visits = 1 / lane efficiency), 4 table
 // lookups inside the profile (lane x band), 5..7 those at entries < 4096, 8192, 16384; common grid
 // only: 8 lane-records read from the group rows (two 16-byte loads each), 9 from the LDS near field,
-// 10 from the bands' own tables (four 8-byte loads).
-constexpr int kStatStride = 11;
+// 10 from the bands' own tables (four 8-byte loads); 11..16 the L2 footprint of the row and own-table
+// fetches (mo_band.h kHist 7..12: distinct 32-B sectors, 128-B lines, wave fetches).
+constexpr int kStatStride = 4 + 13;
 
 // Spectrally sharded gather for the render path: queries4[i] = {p, *}, i < *count_dev (<= nq_max);
 // out4[i * 8 + g] = the 4 bands of group g (BandGroups::pos gives a band's float offset).

@@ -533,16 +533,24 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
 constexpr int kCgMaxRows = 65536;
-// (MPSS_CG_MAX_ROWS overrides the cap: the row-cap experiments of tools/x_ab_val.sh)
+// (a diagnostic build, -DMPSS_DIAGNOSTICS, lets MPSS_CG_MAX_ROWS override the cap: row-cap experiments)
 static int cg_max_rows() {
+#ifdef MPSS_DIAGNOSTICS
     const char *e = getenv("MPSS_CG_MAX_ROWS");
-    return e && atoi(e) > 0 ? atoi(e) : kCgMaxRows;
+    if (e && atoi(e) > 0) return atoi(e);
+#endif
+    return kCgMaxRows;
 }
 
 bool build_common_grid(const float *tab, int L, const float *host_rcp, const BandGroups &groups, CommonGrid &cg,
                        std::vector<float4> &h, float cg_rel_err[NB], float cg_l1_err[NB], int near_field,
                        int lds_reserve, bool rgb) {
     cg = CommonGrid{};
+    for (int g = 0; g < kGroups; ++g) {  // (one row per grid step unless the layout below says otherwise)
+        cg.hinv[g] = 1.f;
+        cg.hc[g] = 0.f;
+        cg.ua[g] = (float)L;
+    }
     h.clear();
     for (int c = 0; c < NB; ++c) cg_rel_err[c] = cg_l1_err[c] = 0.f;
     const int kLdsFloats = 4 * (near_field + 3) - lds_reserve;
@@ -645,14 +653,16 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             const float *T = tab + (size_t)c * L;
             return (float)((1.0 - t) * (double)T[sidx] + t * (double)T[sidx + 1]);
         };
-        // The row range: every band knot past the near field (s >= u0lim r_j - 1) whose rows value is
-        // off by more than kCgRelTol of |T[s]| and more than kCgAbsTol of the band's peak is "bad";
-        // the rows serve the longest stretch of u between bad knots, a grid cell of margin either
-        // side (the rows' error inside a cell is bounded by that at the knots in it), capped at
-        // kCgMaxRows rows. Usually the first stretch, from the near field's end; for bands of widely
-        // different reach (the rgbprofile's R, G, B: the shortest reach's knots are much denser than
-        // the grid, so it is off from the start) one past its end -- there tau's range test makes it
-        // exactly 0, as its rows hold.
+        // The row layout. Rows are indexed by v, a piecewise-linear map of u: v = u below ua (one row per
+        // grid step), v = ua + (u - ua) / H above it (one row per H steps, H = 1, 2 or 4) -- on the lane
+        // v = min(u, fma(u, hinv, hc)), hc = ua (1 - hinv). A cell (rows k, k + 1) is "bad" when some band
+        // knot in it is off by more than max(kCgRelTol scale, kCgAbsTol peak) on the rows (the error of
+        // two piecewise-linear functions peaks at a knot of one or the other, and at the row positions R is
+        // the band's own lerp, rounded once); a bad cell's row carries a NaN in slot 0's first value and
+        // its lanes read the bands' own tables instead (cg_fix), so every served value is within the bound.
+        // The range [u1start, u1lim), ua and H are chosen to maximise the record weight served by good
+        // cells (records per unit u fall off as 1 / u past the near field: the octree's aggregated nodes
+        // grow with distance), a bad cell counting against it, within kCgMaxRows rows (+ one pad row).
         double peak[4] = {0.0, 0.0, 0.0, 0.0};  // each band's largest |T|
         for (int j = 0; j < 4; ++j)
             if (groups.band[g][j] >= 0) {
@@ -680,49 +690,157 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             }
             return v;
         };
-        auto knot_err = [&](int j, int k) -> double {  // |rows - T| at band j's knot k, inf = bad
+        // |rows - T| at band j's knot k on a grid of H steps (cells [H m, H (m + 1))), inf = bad
+        auto knot_err = [&](int j, int k, int H) -> double {
             const float *T = tab + (size_t)groups.band[g][j] * L;
             const double u = (double)k / r[j];
-            const int64_t ui = (int64_t)std::floor(u);
-            const double t = u - (double)ui;
-            const double approx = (1.0 - t) * R(j, ui) + t * R(j, ui + 1);
+            const int64_t m = (int64_t)std::floor(u / H);
+            const double t = (u - (double)(H * m)) / H;
+            const double approx = (1.0 - t) * R(j, H * m) + t * R(j, H * (m + 1));
             const double err = std::fabs(approx - (double)T[k]);
             return err > std::max(kCgRelTol * scale(j, k), kCgAbsTol * peak[j]) ? INFINITY : err;
         };
-        std::vector<double> bad;
+        static constexpr int kH[3] = {1, 2, 4};
+        const int ncell = L + 2;  // cells of the fine grid (u < L); coarse grids: ncell / H + 1
+        std::vector<uint8_t> bad[3];
+        for (int hi = 0; hi < 3; ++hi) bad[hi].assign((size_t)ncell / kH[hi] + 2, 0);
+        std::vector<double> fine_bad;  // u of the fine grid's bad knots (the candidate range starts)
         for (int j = 0; j < 4; ++j) {
             if (groups.band[g][j] < 0) continue;
-            for (int k = std::max(0, (int)std::floor((double)u0f * r[j]) - 1); k < L - 1; ++k)
-                if (knot_err(j, k) == INFINITY) bad.push_back((double)k / r[j]);
-        }
-        bad.push_back((double)(L - 1));
-        std::sort(bad.begin(), bad.end());
-        double start = u0f, ubad = u0f, best = -1.0;
-        {
-            double from = u0f;  // the current stretch's first servable u
-            for (const double ub : bad) {
-                if (ub >= from) {
-                    const double len = std::min(std::floor(ub) - 1.0, from + (double)cg_max_rows()) - from;
-                    if (len > best) {
-                        best = len;
-                        start = from;
-                        ubad = ub;
+            for (int k = std::max(0, (int)std::floor((double)u0f * r[j]) - 1); k < L - 1; ++k) {
+                const double u = (double)k / r[j];
+                for (int hi = 0; hi < 3; ++hi)
+                    if (knot_err(j, k, kH[hi]) == INFINITY) {
+                        bad[hi][(size_t)std::floor(u / kH[hi])] = 1;
+                        if (hi == 0) fine_bad.push_back(u);
                     }
-                }
-                from = std::max(from, std::floor(ub) + 2.0);
             }
         }
-        for (int j = 0; j < 4; ++j) {  // the error over the knots the rows serve
+        std::sort(fine_bad.begin(), fine_bad.end());
+        // prefix scores per grid: a good cell +w, a bad one -w, w = the cell's share of records (~ H / u)
+        std::vector<double> P[3];
+        for (int hi = 0; hi < 3; ++hi) {
+            const int H = kH[hi];
+            const size_t n = bad[hi].size();
+            P[hi].assign(n + 1, 0.0);
+            for (size_t m = 0; m < n; ++m) {
+                const double w = (double)H / std::max(1.0, (double)H * ((double)m + 0.5));
+                P[hi][m + 1] = P[hi][m] + (bad[hi][m] ? -w : w);
+            }
+        }
+        // argmax of P over an index range (sparse table per grid)
+        std::vector<std::vector<uint32_t>> sp[3];
+        for (int hi = 0; hi < 3; ++hi) {
+            const size_t n = P[hi].size();
+            sp[hi].push_back(std::vector<uint32_t>(n));
+            for (size_t i = 0; i < n; ++i) sp[hi][0][i] = (uint32_t)i;
+            for (size_t lv = 1; ((size_t)1 << lv) <= n; ++lv) {
+                const std::vector<uint32_t> &a = sp[hi][lv - 1];
+                std::vector<uint32_t> b(n - ((size_t)1 << lv) + 1);
+                for (size_t i = 0; i < b.size(); ++i) {
+                    const uint32_t x = a[i], y = a[i + ((size_t)1 << (lv - 1))];
+                    b[i] = P[hi][y] > P[hi][x] ? y : x;
+                }
+                sp[hi].push_back(std::move(b));
+            }
+        }
+        auto argmax = [&](int hi, size_t lo, size_t hi_incl) -> size_t {  // first index of the max
+            size_t lv = 0;
+            while (((size_t)2 << lv) <= hi_incl - lo + 1) ++lv;
+            const uint32_t x = sp[hi][lv][lo], y = sp[hi][lv][hi_incl + 1 - ((size_t)1 << lv)];
+            return P[hi][y] > P[hi][x] ? y : x;
+        };
+        const int64_t cap = cg_max_rows();
+        const int64_t uend = (int64_t)L - 1;  // the rows serve u < u1lim <= L - 1
+        // candidate starts: the near field's end, and just past each of the first bad fine knots
+        std::vector<double> starts{(double)u0f};
+        for (const double b : fine_bad) {
+            if (starts.size() >= 64) break;
+            const double st = std::floor(b) + 2.0;
+            if (st > starts.back() && st < (double)uend) starts.push_back(st);
+        }
+        double best = 0.0, bstart = u0f;
+        int64_t bua = 0, bu1 = 0;
+        int bh = 0;
+        for (const double st : starts) {
+            const int64_t sb = (int64_t)std::floor(st), vbase = std::max<int64_t>(0, sb - 1);
+            // H = 1: fine rows only, [st, u1)
+            {
+                const int64_t hiu = std::min<int64_t>(uend, vbase + cap);
+                if (hiu > sb) {
+                    const size_t e = argmax(0, (size_t)sb + 1, (size_t)hiu);
+                    const double sc = P[0][e] - P[0][sb];
+                    if (sc > best) {
+                        best = sc, bstart = st, bua = (int64_t)e, bu1 = (int64_t)e, bh = 0;
+                    }
+                }
+            }
+            // H = 2, 4: fine rows [st, ua), coarse rows [ua, u1), ua a multiple of 64 (so hc is exact)
+            for (int hi = 1; hi < 3; ++hi) {
+                const int H = kH[hi];
+                for (int64_t ua = ((sb + 64) / 64) * 64; ua < uend; ua += 64) {
+                    const int64_t left = cap - (ua - vbase);
+                    if (left < 2) break;
+                    const double sf = P[0][ua] - P[0][sb];
+                    const int64_t m0 = ua / H;
+                    const int64_t mhi = std::min<int64_t>(m0 + left, uend / H);
+                    if (mhi <= m0) continue;
+                    const size_t e = argmax(hi, (size_t)m0 + 1, (size_t)mhi);
+                    const double sc = sf + P[hi][e] - P[hi][m0];
+                    if (sc > best) best = sc, bstart = st, bua = ua, bu1 = (int64_t)e * H, bh = hi;
+                }
+            }
+        }
+        const int H = kH[bh];
+        cg.hinv[g] = 1.f;
+        cg.hc[g] = 0.f;
+        cg.ua[g] = (float)L;
+        if (!(best > 0.0) || bu1 <= (int64_t)bstart + 1) {  // no accurate range: the exact tables past the near field
+            cg.u1lim[g] = cg.u1start[g] = u0f;
+            cg.ubase[g] = 0;
+            return;
+        }
+        const int64_t ua = bh ? bua : bu1;  // (H = 1: every row fine)
+        if (bh) {
+            cg.hinv[g] = 1.f / (float)H;
+            cg.hc[g] = (float)((double)ua * (1.0 - 1.0 / H));  // exact: ua a multiple of 64
+            cg.ua[g] = (float)ua;
+        }
+        const int64_t vbase = std::max<int64_t>(0, (int64_t)std::floor(bstart) - 1);
+        const int64_t v1 = ua + (bu1 - ua) / H;  // v(u1); lanes read rows <= v1 (v may round up to v1)
+        auto upos = [&](int64_t v) -> int64_t { return v <= ua ? v : ua + (int64_t)H * (v - ua); };
+        auto cell_bad = [&](int64_t v) -> bool {
+            const int64_t u = upos(v);
+            return v < ua ? bad[0][(size_t)u] != 0 : bad[bh][(size_t)(u / H)] != 0;
+        };
+        cg.ubase[g] = (uint32_t)vbase;
+        cg.u1start[g] = (float)bstart;  // (u0f, or an integer below 2^24)
+        cg.u1lim[g] = (float)bu1;
+        for (int64_t v = vbase; v <= v1; ++v) {
+            const int64_t u = upos(v), un = upos(v + 1);
+            float vv[4][2];
+            for (int j = 0; j < 4; ++j) {
+                vv[j][0] = R(j, u);
+                vv[j][1] = R(j, un);
+            }
+            if (cell_bad(v)) vv[0][0] = NAN;  // its lanes read the bands' own tables (cg_fix)
+            h.push_back(make_float4(vv[0][0], vv[0][1], vv[1][0], vv[1][1]));
+            h.push_back(make_float4(vv[2][0], vv[2][1], vv[3][0], vv[3][1]));
+        }
+        for (int j = 0; j < 4; ++j) {  // the error over the knots the good rows serve
             const int c = groups.band[g][j];
             if (c < 0) continue;
             const float *T = tab + (size_t)c * L;
             double l1 = 0.0, emax = 0.0, esum = 0.0;
             for (int k = 0; k < L; ++k) l1 += std::fabs(T[k]);
-            for (int k = std::max(0, (int)std::floor(start * r[j]) - 1); k < L - 1; ++k) {
+            for (int k = std::max(0, (int)std::floor(bstart * r[j]) - 1); k < L - 1; ++k) {
                 const double u = (double)k / r[j];
-                if (u < start) continue;
-                if (u >= ubad) break;
-                const double e = knot_err(j, k);
+                if (u < bstart) continue;
+                if (u >= (double)bu1) break;
+                const int Hk = u < (double)ua ? 1 : H;
+                const int64_t v = u < (double)ua ? (int64_t)std::floor(u) : ua + (int64_t)std::floor((u - ua) / H);
+                if (cell_bad(v)) continue;
+                const double e = knot_err(j, k, Hk);
                 // (relative error -- to scale(): the band's own value, or the largest of R, G, B -- where
                 // the relative bound governs: scale >= kCgAbsTol / kCgRelTol of the peak)
                 const double sc = scale(j, k);
@@ -731,26 +849,6 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             }
             relg[g][j] = (float)emax;
             l1g[g][j] = (float)(l1 > 0.0 ? esum / l1 : 0.0);
-        }
-        const int64_t ubase = std::max<int64_t>(0, (int64_t)std::floor(start) - 1);
-        int64_t u1 = (int64_t)std::floor(ubad) - 1;
-        u1 = std::min<int64_t>(u1, ubase + cg_max_rows());
-        u1 = std::min<int64_t>(u1, (int64_t)L - 1);
-        cg.ubase[g] = (uint32_t)ubase;
-        if (u1 <= (int64_t)start + 1) {  // no accurate range: the exact tables past the near field
-            cg.u1lim[g] = cg.u1start[g] = u0f;
-            return;
-        }
-        cg.u1start[g] = (float)start;  // (u0f, or an integer below 2^24)
-        cg.u1lim[g] = (float)u1;  // lanes with u < u1 read rows u0 <= u1 - 1 (values R(u0), R(u0 + 1))
-        for (int64_t u = ubase; u < u1; ++u) {
-            float v[4][2];
-            for (int j = 0; j < 4; ++j) {
-                v[j][0] = R(j, u);
-                v[j][1] = R(j, u + 1);
-            }
-            h.push_back(make_float4(v[0][0], v[0][1], v[1][0], v[1][1]));
-            h.push_back(make_float4(v[2][0], v[2][1], v[3][0], v[3][1]));
         }
         anyg[g] = true;
     };
@@ -774,6 +872,9 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             cg.ubase[g] = cg.ubase[0];
             cg.u1start[g] = cg.u1start[0];
             cg.u1lim[g] = cg.u1lim[0];
+            cg.ua[g] = cg.ua[0];
+            cg.hinv[g] = cg.hinv[0];
+            cg.hc[g] = cg.hc[0];
             anyg[g] = anyg[0];
             failg[g] = failg[0];
         }

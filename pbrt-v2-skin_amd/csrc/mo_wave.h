@@ -119,7 +119,7 @@ void mo_band_wave_kernel(BandArgs a) {
         }
     }
     // (the common-grid gather's fused FromRGB takes the weights with FromRGB's .94 folded in: from_rgb4_fused)
-    if (RGB && tid < 28) lt[4 * ROWF - 28 + tid] = (&a.t.rgb_k[grp].w[0])[tid] * ((CG && MPSS_MO_FUSED) ? .94f : 1.f);
+    if (RGB && tid < 28) lt[4 * ROWF - 28 + tid] = (&a.t.rgb_k[grp].w[0])[tid] * (CG ? .94f : 1.f);
     __syncthreads();  // the near field is read-only from here on
     for (;;) {
         int u = 0;
@@ -131,7 +131,7 @@ void mo_band_wave_kernel(BandArgs a) {
         float px = 0.f, py = 0.f, pz = 0.f;
         const bool live = q >= 0 && band_query(a, q, px, py, pz);
         float acc[4];
-        int kn = 0, kp = 0, wn = 0, wp = 0, hist[7] = {0, 0, 0, 0, 0, 0, 0};
+        int kn = 0, kp = 0, wn = 0, wp = 0, hist[kHist] = {};
         mo_band_traverse<COUNT, KLDS, VROWS && !CG, CG, RGB>(a.t, grp, px, py, pz, live, acc, kn, kp, wn, wp, hist,
                                                             lt);
         if (live) {
@@ -158,7 +158,7 @@ void mo_band_wave_kernel(BandArgs a) {
                     atomicAdd(&a.counts[kStatStride * grp + 3], (unsigned long long)wp);
                 }
 #pragma unroll
-                for (int k = 0; k < 7; ++k)
+                for (int k = 0; k < kHist; ++k)
                     if (hist[k]) atomicAdd(&a.counts[kStatStride * grp + 4 + k], (unsigned long long)hist[k]);
             }
         }

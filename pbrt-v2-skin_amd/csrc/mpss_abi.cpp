@@ -43,7 +43,7 @@ void require(bool ok, const char *msg) {
 
 extern "C" {
 
-int mpss_abi_version(void) { return 12; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
+int mpss_abi_version(void) { return 13; }  // 2: poisson point finder, infinite lights; 3: imagemap textures;
                                           // 4: tile costs, wave-iteration stats, thread-safe calls;
                                           // 5: reference-sampler replay, dipole materials;
                                           // 6: GPU octree build (octree_on_host), mpss_octree_export;
@@ -58,6 +58,9 @@ int mpss_abi_version(void) { return 12; }  // 2: poisson point finder, infinite 
                                           //     grid), mpss_host_common_grid u1start / rgb mode
                                           // 12: LayeredSkin genprofile / showirradiancepoints /
                                           //     irradiancepointsize; mpss_host_common_grid near_field
+                                          // 13: per-group, per-path L2 footprint in mpss_render_stats;
+                                          //     common-grid rows H steps apart past ua, bad cells
+                                          //     flagged (mpss_host_common_grid ua / hinv)
 const char *mpss_last_error(void) { return g_last_error.c_str(); }
 
 void mpss_config_defaults(mpss_config *c) {
@@ -190,7 +193,8 @@ int mpss_get_material_tables(mpss_ctx *c, uint32_t id, float *rd, uint32_t *len,
 
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, int near_field, float *rows,
                           uint32_t *n_rows, int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start,
-                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, int *ok) {
+                          uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, float *ua, float *hinv,
+                          int *ok) {
     return guarded([&] {
         require(table && rcp && ok, "mpss_host_common_grid: null argument");
         require(L >= 2 && L < (1u << 24), "mpss_host_common_grid: L out of range");
@@ -218,6 +222,8 @@ int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int 
             if (u1start) u1start[k] = cg.u1start[k];
             if (row0) row0[k] = cg.row0[k];
             if (ubase) ubase[k] = cg.ubase[k];
+            if (ua) ua[k] = cg.ua[k];
+            if (hinv) hinv[k] = cg.hinv[k];
         }
         for (int c = 0; c < NB; ++c) {
             if (rel_err) rel_err[c] = rel[c];

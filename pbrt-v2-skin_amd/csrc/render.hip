@@ -539,7 +539,9 @@ __global__ __launch_bounds__(256) void poisson_walk_kernel(RenderScene sc, Poiss
             const ShadingFrame fr = tri_shading(mesh.view, lt, p, 1.f - h.b1 - h.b2, h.b1, h.b2);
             nn = faceforward(fr.ng, -d);
             eps = 1e-3f * h.t;
-            if (depth >= 3 && mesh.material < (uint32_t)sc.nmaterials && sc.materials[mesh.material].has_bssrdf) {
+            // every mesh material is a LayeredSkin, whose GetBSSRDF is never NULL (layeredskin.cpp:170-177;
+            // surfacepoints.cpp:202) -- genprofile false included: its points are candidates too
+            if (depth >= 3 && mesh.material < (uint32_t)sc.nmaterials) {
                 // dgs = Bump(hitGeometry, dgShading); without N and S the shading geometry is dg itself
                 // (its nn already faceforwarded); no ray differentials (GetBSSRDF(RayDifferential(ray)))
                 V3 sn = (!mesh.view.N && !mesh.view.S) ? nn : fr.nn;

@@ -1058,6 +1058,12 @@ mpss_render_stats Context::render_stats() {
             out.mo_row_lane_records += (int64_t)c[kStatStride * g2 + 8];
             out.mo_lds_lane_records += (int64_t)c[kStatStride * g2 + 9];
             out.mo_table_lane_records += (int64_t)c[kStatStride * g2 + 10];
+            for (int k = 0; k < 3; ++k) out.group_path_records[g2][k] = (int64_t)c[kStatStride * g2 + 8 + k];
+            for (int k = 0; k < 2; ++k) {
+                out.group_path_sectors[g2][k] = (int64_t)c[kStatStride * g2 + 11 + k];
+                out.group_path_lines[g2][k] = (int64_t)c[kStatStride * g2 + 13 + k];
+                out.group_path_fetches[g2][k] = (int64_t)c[kStatStride * g2 + 15 + k];
+            }
         }
     }
     return out;

@@ -242,7 +242,8 @@ __device__ ReplayArray replay_array(const RenderScene &sc, int spp, int nmax, ui
     return ReplayArray{adraw + off, aidx + (size_t)a * spp, asig + (size_t)a * spp * nmax, n, hdr, col};
 }
 
-// skip: a diagnostic only (MPSS_REPLAY_SKIP, launch_replay_window; the values are then wrong): bit 0
+// skip: 0, except in a diagnostic build (-DMPSS_DIAGNOSTICS: MPSS_REPLAY_SKIP, launch_replay_window; the
+// values are then wrong): bit 0
 // the per-sample own shuffles and the block shuffles' partners, 1 the block swaps, 2 the camera rays'
 // hit tests, 3 the light arrays' values, 4 the draws' copies (the stream still advances) -- the cost of each
 // section of the pixel loop, measured by leaving it out.
@@ -487,7 +488,11 @@ void launch_replay_window(const RenderScene &sc, const ReplayWindow &w, hipStrea
     if (lds > 64 * 1024)
         MPSS_HIP(hipFuncSetAttribute((const void *)replay_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds));
+#ifdef MPSS_DIAGNOSTICS  // (a diagnostic build only: a release library always generates every value)
     static const int skip = getenv("MPSS_REPLAY_SKIP") ? atoi(getenv("MPSS_REPLAY_SKIP")) : 0;
+#else
+    constexpr int skip = 0;
+#endif
     hipLaunchKernelGGL(replay_window_kernel, dim3((unsigned)((nw + nwv - 1) / nwv)), dim3(64 * nwv), lds, stream, sc,
                        w, words, skip);
     MPSS_HIP(hipGetLastError());

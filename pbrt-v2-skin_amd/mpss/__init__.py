@@ -59,7 +59,9 @@ class RenderStats(C.Structure):
                 ("n_direct", C.c_int64), ("mo_wave_node_iters", C.c_int64), ("mo_wave_point_iters", C.c_int64),
                 ("mo_lookups", C.c_int64), ("mo_lookups_near", C.c_int64 * 3), ("mo_row_lane_records", C.c_int64),
                 ("mo_lds_lane_records", C.c_int64), ("mo_table_lane_records", C.c_int64), ("ms_tex", C.c_double),
-                ("n_tex", C.c_int64), ("ms_replay", C.c_double), ("n_replay", C.c_int64)]
+                ("n_tex", C.c_int64), ("ms_replay", C.c_double), ("n_replay", C.c_int64),
+                ("group_path_records", (C.c_int64 * 3) * 8), ("group_path_sectors", (C.c_int64 * 2) * 8),
+                ("group_path_lines", (C.c_int64 * 2) * 8), ("group_path_fetches", (C.c_int64 * 2) * 8)]
 
 
 class LayeredSkin(C.Structure):
@@ -139,7 +141,7 @@ _sig("mpss_host_imagemap_lookup", C.c_int, [C.POINTER(Imagemap), u32, f32p, f32p
 _sig("mpss_host_skin_layers", C.c_int, [C.POINTER(LayeredSkin), f32p, f32p, f32p, f32p])
 _sig("mpss_host_build_profile", C.c_int, [f32p, f32p, f32p, f32p, C.c_int, C.c_int, vp, u32p, vp, vp])
 _sig("mpss_host_rho_table", C.c_int, [C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, f32p, C.POINTER(C.c_float)])
-_sig("mpss_host_common_grid", C.c_int, [f32p, u32, f32p, C.c_int, C.c_int, vp, u32p] + [vp] * 9 + [C.POINTER(C.c_int)])
+_sig("mpss_host_common_grid", C.c_int, [f32p, u32, f32p, C.c_int, C.c_int, vp, u32p] + [vp] * 11 + [C.POINTER(C.c_int)])
 _sig("mpss_host_octree_export", C.c_int, [u32, f32p, f32p, f32p, f32p, u32p] + [vp] * 8)
 
 
@@ -319,16 +321,18 @@ def host_common_grid(table, rcp, snake=False, rgb=False, near_field=5088):
     L = table.shape[1]
     mode = 2 if rgb else int(snake)
     n = C.c_uint32(0)
-    nul = [None] * 9
+    nul = [None] * 11
     ok = C.c_int()
     check(_lib.mpss_host_common_grid(table, L, rcp, mode, int(near_field), None, C.byref(n), *nul, C.byref(ok)))
     out = dict(rows=np.zeros((n.value, 8), np.float32), bands=np.zeros((8, 4), np.int32),
                rg=np.zeros(8, np.float32), u0lim=np.zeros(8, np.float32), u1lim=np.zeros(8, np.float32),
                u1start=np.zeros(8, np.float32), row0=np.zeros(8, np.uint32), ubase=np.zeros(8, np.uint32),
-               rel_err=np.zeros(NB, np.float32), l1_err=np.zeros(NB, np.float32))
+               rel_err=np.zeros(NB, np.float32), l1_err=np.zeros(NB, np.float32), ua=np.zeros(8, np.float32),
+               hinv=np.zeros(8, np.float32))
     check(_lib.mpss_host_common_grid(table, L, rcp, mode, int(near_field), out["rows"].ctypes.data, C.byref(n),
                                      *[out[k].ctypes.data for k in ("bands", "rg", "u0lim", "u1lim", "u1start", "row0",
-                                                                    "ubase", "rel_err", "l1_err")], C.byref(ok)))
+                                                                    "ubase", "rel_err", "l1_err", "ua", "hinv")],
+                                     C.byref(ok)))
     out["ok"] = bool(ok.value)
     return out
 
@@ -523,7 +527,7 @@ class Context:
         out = {}
         for k, _ in RenderStats._fields_:
             v = getattr(st, k)
-            out[k] = [list(x) for x in v] if k == "group_bands" else (
+            out[k] = [list(x) for x in v] if k == "group_bands" or k.startswith("group_path") else (
                 list(v) if k.startswith("group_") or k == "mo_lookups_near" else v)
         return out
 

@@ -16,7 +16,7 @@ def test_library_exports_header_symbols(mpss):
 
 
 def test_abi_version_and_errors(mpss):
-    assert mpss.lib().mpss_abi_version() == 12
+    assert mpss.lib().mpss_abi_version() == 13
     # a null-argument call must fail with a message, not crash
     rc = mpss.lib().mpss_create(None, None)
     assert rc == -1

@@ -112,3 +112,25 @@ def test_material_showirradiancepoints(mpss, oracle, size):
     assert (ref[..., 1] > 0).mean() > 0.03
     ctx.close()
     o.close()
+
+
+def test_poisson_finder_keeps_genprofile_false_surfaces(mpss, oracle):
+    """FindPoissonPointDistribution picks candidates by GetBSSRDF != NULL (surfacepoints.cpp:202), which a
+    LayeredSkin always returns (layeredskin.cpp:170-177) -- genprofile false included. With half the head
+    genprofile false, the Poisson points cover both halves, equal to the oracle's (o_poisson_points)."""
+    sc = _split_two_materials(_scene(), dict(gen_profile=0))
+    sc.integrator["usepoissonpointfinder"] = "true"
+    sc.integrator["minsampledistance"] = 0.02
+    from mpss import pbrtscene
+    ctx = pbrtscene.build_context(sc)
+    ctx.preprocess(seed=5)
+    got = ctx.surface_points()
+    o = orr.OracleScene(sc, orr.tables_from_oracle(sc), ctx.cfg, mpss)
+    ref = o.poisson_points(5)
+    assert len(got) == len(ref) and len(got) > 100
+    assert set(np.unique(got["material"])) == {0, 1}
+    assert np.array_equal(got["p"], ref["p"])
+    for k in ("u", "v", "material", "area", "ray_eps"):
+        assert np.array_equal(got[k], ref[k]), k
+    ctx.close()
+    o.close()

@@ -157,9 +157,31 @@ def test_layeredskin_material_on_device(oracle, mpss, torch_dev):
     assert np.array_equal(rho, hd_o)
 
 
-def _rel_close(got, ref, tol):
-    scale = np.maximum(np.abs(ref), np.abs(ref).max(axis=1, keepdims=True) * 1e-3)
-    return np.all(np.abs(got - ref) <= tol * scale + 1e-30)
+U = 2.0 ** -24
+
+
+def _sum_bound(ref, nn, npt):
+    """Per query and band, unfloored: the fast kernels form the reference's terms exactly and sum them in
+    another order (a leaf's points first, one running sum per band), so each sum lies within 2 (n - 1) u
+    of the exact one (n: the records the reference visits, u = 2^-24); the terms are non-negative."""
+    n = (nn + npt).astype(np.float64)[:, None]
+    return (4 * U + 2 * n * U) * np.abs(ref)
+
+
+def _grid_bound(ref, nn, npt, table, cloud):
+    """_sum_bound for the common-grid gather: every term's lookup within kCgRelTol (2e-6, 3e-6 here for a
+    lerp between knots) of its value or kCgAbsTol (1e-13) of the band's peak (a bad cell's lanes read the
+    exact tables), the fused lerp within a few ulp. The relative parts scale the result, and the absolute
+    part is at most 1e-13 peak_c times the E_c * area of all points."""
+    _, _, E, area = cloud
+    peak = np.abs(table).max(axis=1).astype(np.float64)[None, :]
+    mass = (E.astype(np.float64) * area.astype(np.float64)[:, None]).sum(axis=0)[None, :]
+    return 3e-6 * np.abs(ref) + _sum_bound(ref, nn, npt) + 1e-13 * peak * mass
+
+
+def _within(got, ref, bound):
+    err = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    return bool(np.all(err <= bound)), float((err / np.maximum(bound, 1e-300)).max())
 
 
 @pytest.mark.parametrize("max_error", [0.05, 0.1])
@@ -172,9 +194,10 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
                                           mo_common_grid=0)
         cg, cnt_g, plain_g, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, mode=0)
         exact, cnt_e, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, max_error, exact=True)
-        ref = oracle.Octree(*cloud).mo(q, table, rcp, max_error)
+        ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, max_error, counters=True)
         assert np.array_equal(exact, ref)
-        assert _rel_close(fast, ref, 2e-5), np.abs(fast - ref).max()
+        ok, worst = _within(fast, ref, _sum_bound(ref, nn, npt))
+        assert ok, worst
         assert np.array_equal(cnt_f[:, 2:], cnt_e[:, 2:])  # same pruned traversal per query
         assert np.array_equal(fast == 0, ref == 0)
         # spectral sharding: same terms, same order per band -> bit-identical to the packet kernel
@@ -183,7 +206,8 @@ def test_mo_packet_matches_reference_order(oracle, mpss, torch_dev, skin_profile
         assert np.all(cnt_b[:, 2] <= 8 * cnt_f[:, 2]) and np.all(cnt_b[:, 2] > 0)
         # the common grid: the same traversal, its far lookups resampled
         assert np.array_equal(cnt_g, cnt_b) and np.array_equal(plain_g, cg)
-        assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
+        ok, worst = _within(cg, ref, _grid_bound(ref, nn, npt, table, cloud))
+        assert ok, worst
         assert np.array_equal(cg == 0, ref == 0)
 
 
@@ -197,10 +221,10 @@ def test_mo_packet_edge_cases(oracle, mpss, torch_dev, wide_profile):
         fast, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=2)
         band, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0, mo_common_grid=0)
         cg, _, _, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.05, mode=0)
-        ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.05)
-        assert _rel_close(fast, ref, 2e-5), npts
+        ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.05, counters=True)
+        assert _within(fast, ref, _sum_bound(ref, nn, npt))[0], npts
         assert np.array_equal(band, fast), npts
-        assert _rel_close(cg, ref, 2e-5), npts
+        assert _within(cg, ref, _grid_bound(ref, nn, npt, table, cloud))[0], npts
 
 
 @pytest.mark.parametrize("cfg", [dict(mo_band_dealing=1), dict(mo_work_stealing=0), dict(mo_near_field=10236),
@@ -219,8 +243,9 @@ def test_mo_gather_choices_are_bit_identical(oracle, mpss, torch_dev, skin_profi
     _, _, alt, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
     assert np.array_equal(base, alt)
     assert np.array_equal(base, packet)  # one running sum per band, the packet kernel's order
-    ref = oracle.Octree(*cloud).mo(q, table, rcp, 0.1)
-    assert _rel_close(base, ref, 2e-5), np.abs(base - ref).max()
+    ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.1, counters=True)
+    ok, worst = _within(base, ref, _sum_bound(ref, nn, npt))
+    assert ok, worst
     assert np.any(ref > 0)
 
 
@@ -245,20 +270,9 @@ def test_mo_common_grid_vs_oracle(oracle, mpss, torch_dev, skin_profile, cfg):
     _, _, cg, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, **cfg)
     _, _, band, _ = run_gpu(mpss, torch_dev, cloud, table, rcp, q, 0.1, mode=0, mo_common_grid=0, **cfg)
     ref, nn, npt = oracle.Octree(*cloud).mo(q, table, rcp, 0.1, counters=True)
-    assert _rel_close(cg, ref, 2e-5), np.abs(cg - ref).max()
-    # and unfloored, per query and band, from the grid's guarantee: every term's lookup within
-    # kCgRelTol (2e-6, 3e-6 here for a lerp between knots) of its value or kCgAbsTol (1e-13) of the
-    # band's peak; the fused lerp within a few ulp; each sum within (n - 1) u of its exact value (n:
-    # the records the reference visits, u = 2^-24). The terms are non-negative, so the relative parts
-    # scale the result, and the absolute part is at most 1e-13 peak_c times the E_c * area of all points
-    _, _, E, area = cloud
-    u = 2.0 ** -24
-    n = (nn + npt).astype(np.float64)[:, None]
-    peak = np.abs(table).max(axis=1).astype(np.float64)[None, :]
-    mass = (E.astype(np.float64) * area.astype(np.float64)[:, None]).sum(axis=0)[None, :]
-    bound = (3e-6 + 4 * u + 2 * n * u) * np.abs(ref) + 1e-13 * peak * mass
-    err = np.abs(cg.astype(np.float64) - ref)
-    assert np.all(err <= bound), (err / bound).max()
+    # unfloored, per query and band, from the grid's guarantee (_grid_bound)
+    ok, worst = _within(cg, ref, _grid_bound(ref, nn, npt, table, cloud))
+    assert ok, worst
     if cfg.get("mo_band_dealing", 0) == 0:
         assert not np.array_equal(cg, band)  # the grid is in use (snake: its rows may lie past this cloud)
     if cfg.get("mo_work_stealing") == 0:

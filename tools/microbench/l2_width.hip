@@ -26,11 +26,16 @@ constexpr int kLog = 19;  // 2^19 floats = 2 MB per group
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-enum { W4 = 0, W8, W16, ROW32, PAIRS4, W16X4, V_COUNT };
+enum { W4 = 0, W8, W16, ROW32, PAIRS4, W16X4, ROW16X2, ROW64, ROW16X2_S, ROW16X2_H, ROW16X2_L, V_COUNT };
 static const char *kNames[V_COUNT] = {"dword (4 B)", "dwordx2 (8 B)", "dwordx4 (16 B)",
                                       "2 x dwordx4, one 32-B sector (group row pair)",
-                                      "4 x dwordx2, four lines (per-band pairs)", "4 x dwordx4, four lines"};
-static const int kInsts[V_COUNT] = {1, 1, 1, 2, 4, 4};
+                                      "4 x dwordx2, four lines (per-band pairs)", "4 x dwordx4, four lines",
+                                      "2 x dwordx4, 32 contiguous bytes at 16-B alignment (16-B rows u, u + 1)",
+                                      "4 x dwordx4, one 64-B segment (8-band row)",
+                                      "2 x dwordx4 at 16 and 32 mod 64 (two sectors of one 64-B half)",
+                                      "2 x dwordx4 at 48 and 64 mod 128 (the two 64-B halves of one line)",
+                                      "2 x dwordx4 at 112 mod 128 and the next line"};
+static const int kInsts[V_COUNT] = {1, 1, 1, 2, 4, 4, 2, 4, 2, 2, 2};
 
 __device__ __forceinline__ uint32_t lcg(uint32_t &s) {
     s = s * 1664525u + 1013904223u;
@@ -64,6 +69,23 @@ __global__ __launch_bounds__(1024) void width_kernel(const float *__restrict__ t
             for (int j = 0; j < 4; ++j) v[j] = *(const f2 *)(t + ((lcg(s) >> (32 - kLog)) & ~1u));
             acc.x += v[0].x + v[1].x + v[2].x + v[3].x;
             acc.y += v[0].y + v[1].y + v[2].y + v[3].y;
+        } else if (V == ROW16X2) {
+            const uint32_t o = (lcg(s) >> (32 - kLog)) & ~3u;
+            const uint32_t o2 = o + 4 < (1u << kLog) ? o + 4 : o;
+            const f4 a = *(const f4 *)(t + o), b = *(const f4 *)(t + o2);
+            acc += a + b;
+        } else if (V == ROW16X2_S || V == ROW16X2_H || V == ROW16X2_L) {
+            // the first load at a fixed offset in its 128-B line: 16 B (sectors 0, 1), 48 (halves), 112 (lines)
+            const uint32_t in = V == ROW16X2_S ? 4u : (V == ROW16X2_H ? 12u : 28u);
+            const uint32_t o = (((lcg(s) >> (32 - kLog)) & ~31u) + in) & ((1u << kLog) - 8u);
+            const uint32_t o2 = o + 4;
+            const f4 a = *(const f4 *)(t + o), b = *(const f4 *)(t + o2);
+            acc += a + b;
+        } else if (V == ROW64) {
+            const uint32_t o = (lcg(s) >> (32 - kLog)) & ~15u;
+            const f4 a = *(const f4 *)(t + o), b = *(const f4 *)(t + o + 4);
+            const f4 c = *(const f4 *)(t + o + 8), d = *(const f4 *)(t + o + 12);
+            acc += (a + b) + (c + d);
         } else {
             f4 v[4];
 #pragma unroll
@@ -81,6 +103,7 @@ void launch(int blocks, const float *d, int steps, float *o) {
 
 int main(int argc, char **argv) {
     const int steps = argc > 1 ? atoi(argv[1]) : 256;
+    const int only = argc > 2 ? atoi(argv[2]) : -1;  // one variant (the PMC passes), or all
     std::vector<float> h((size_t)8 << kLog);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (float)(i % 1000) * 1e-3f;
     float *d, *o;
@@ -94,9 +117,11 @@ int main(int argc, char **argv) {
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     void (*fn[V_COUNT])(int, const float *, int, float *) = {launch<0>, launch<1>, launch<2>,
-                                                                launch<3>, launch<4>, launch<5>};
+                                                                launch<3>, launch<4>, launch<5>, launch<6>, launch<7>,
+                                                                launch<8>, launch<9>, launch<10>};
     printf("{\"cus\": %d, \"blocks\": %d, \"steps\": %d, \"results\": [\n", prop.multiProcessorCount, blocks, steps);
     for (int v = 0; v < V_COUNT; ++v) {
+        if (only >= 0 && v != only) continue;
         fn[v](blocks, d, 16, o);  // warm L2
         CHECK(hipEventRecord(a));
         fn[v](blocks, d, steps, o);
@@ -109,7 +134,7 @@ int main(int argc, char **argv) {
         const double insts = lane_steps * kInsts[v] / 64;
         printf("%s{\"variant\": \"%s\", \"ms\": %.3f, \"lane_lookups_per_s\": %.4g, "
                "\"cu_cycles_per_wave_inst\": %.1f, \"cu_cycles_per_lane_lookup_x64\": %.1f}",
-               v ? ",\n" : "", kNames[v], ms, lane_steps / (ms * 1e-3),
+               (only < 0 ? v : 0) ? ",\n" : "", kNames[v], ms, lane_steps / (ms * 1e-3),
                (ms * 1e-3) * 2.4e9 * prop.multiProcessorCount / insts,
                (ms * 1e-3) * 2.4e9 * prop.multiProcessorCount / (lane_steps / 64));
     }
