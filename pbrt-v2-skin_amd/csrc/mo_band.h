@@ -109,21 +109,24 @@ inline bool same_groups(const BandGroups &a, const BandGroups &b) {
 // a group's rows can reach its profile end inside kCgMaxRows where the tables are smooth enough for
 // the coarser steps. Each lane takes one of three paths by u:
 //   u < u0lim          every band's exact pair from its LDS near field (as the per-band gather);
-//   u1start <= u < u1lim the group rows -- accurate wherever they are read: build_common measures the
+//   u0lim <= u < u1lim the group rows -- accurate wherever they are read: build_common measures the
 //                      error at every band's own knots, and a cell (row) holding a knot off by more
 //                      than the bound carries a NaN in its first value: its lanes read the bands' own
-//                      tables instead (cg_fix). The range is the one serving the most records from
-//                      good cells (the far tails of the longest-reach bands carry the MPC resampler's
-//                      float noise, which no coarser grid follows: there every cell is bad);
-//   otherwise          every band's exact pair from its own table in HBM/L2 (as the per-band gather).
+//                      tables instead (cg_fix). So does a cell within a step of a band's profile end
+//                      (sampleProfile's exact cutoff, multipole.cpp:65-66, is the own path's) and one
+//                      before the stretch the rows serve (u1start). The range is the one serving the
+//                      most records from good cells (the far tails of the longest-reach bands carry
+//                      the MPC resampler's float noise, which no coarser grid follows: every cell bad);
+//   otherwise          every band's exact pair from its own table in HBM/L2 (as the per-band gather),
+//                      a band past its profile end from the table's trailing zero pair.
 struct CommonGrid {
     const float4 *tab;          // pair rows, two float4 each; group g's row for u at 2 * (row0[g] + u - ubase[g])
     uint32_t row0[kGroups];     // group g's first pair row
     uint32_t ubase[kGroups];    // the v (row coordinate) of that row
     float rg[kGroups];          // the group's grid: u = d2 * rg (its smallest rcp)
     float u0lim[kGroups];       // u < u0lim => every band's pair (s, s + 1) lies in its LDS near field
-    float u1lim[kGroups];       // u1start <= u < u1lim: the pair rows (u1lim = u0lim: none)
-    float u1start[kGroups];     // (u0lim, or past the end of the bands the rows cannot serve)
+    float u1lim[kGroups];       // u0lim <= u < u1lim: the pair rows (u1lim = u0lim: none)
+    float u1start[kGroups];     // the rows' cells below it are flagged (bands the rows cannot serve)
     float ua[kGroups];          // rows one grid step apart below ua, H steps apart above (L: none)
     float hinv[kGroups];        // 1 / H
     float hc[kGroups];          // ua (1 - 1 / H): v = min(u, fma(u, hinv, hc)) (exact: ua a multiple of 64)
@@ -282,6 +285,14 @@ __device__ __forceinline__ const float *in_vgprs(const float *p) {
     return (const float *)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
+// A wave-uniform float held in a VGPR (an operand that would otherwise need a v_mov per use beside
+// another SGPR operand).
+__device__ __forceinline__ float in_vgpr(float x) {
+    float v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
+
 // The Mo() products and the running sums of one record's four Rd values: acc += (Rd * e) (* w).
 template <bool POINT>
 __device__ __forceinline__ void band_rd_products(const float rd[4], const float e[4], float w, f2v acc[2]) {
@@ -387,13 +398,12 @@ __device__ __forceinline__ void band_rd_combine(const float f[4], const RdPair v
 struct CgLane {
     const float4 *tab;    // the pair rows, indexed by floor(v) + rowoff
     uint32_t rowoff;      // row0 - ubase (mod 2^32)
-    float rg, u0lim, u1lim, u1start;
-    float hinv, hc;       // v = min(u, fma(u, hinv, hc))
-    float tau[4];
-    float tau_min;        // the group's first profile end
+    float rg, u0lim, u1lim;
+    float hinv, hc;       // v = min(u, fma(u, hinv, hc)) (hinv in a VGPR: one SGPR operand per fma)
     uint32_t lrow[4];     // LDS float offsets of the slots' exact near-field rows
     uint32_t off[4];      // c_j * L: the bands' own tables (the u >= u1lim path)
-    uint32_t lm2;         // L - 2: the last pair of a band's table
+    uint32_t lm1;         // L - 1: sampleProfile's range end
+    uint32_t zoff;        // byte offset of the table's trailing zero pair (NB * L floats in)
 };
 
 // One record's lookups: band j's pair (T[s], T[s + 1]) -- or (R(u0), R(u0 + 1)) on the group rows --
@@ -416,8 +426,8 @@ __device__ __forceinline__ void cg_count(const BandLane &b, const CgLane &c, flo
     if (!COUNT) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        if (!(b.rcp[j] > 0.f) || !(d2 < c.tau[j])) continue;
         const uint32_t s = (uint32_t)(d2 * b.rcp[j]);
+        if (!(b.rcp[j] > 0.f) || s >= c.lm1) continue;
         ++hist[0];
         hist[1] += s < 4096u;
         hist[2] += s < 8192u;
@@ -496,8 +506,10 @@ __device__ __forceinline__ void cg_own(const BandLane &b, const CgLane &c, const
     uint32_t otp[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint32_t sj = (uint32_t)r.f[j];  // past the end: any in-range pair, the range test gives 0
-        otp[j] = 4u * (c.off[j] + (sj < c.lm2 ? sj : c.lm2));
+        // sampleProfile's range test (multipole.cpp:65-66): s >= L - 1 <=> fl(d2 rcp) >= L - 1 (the saturating
+        // convert takes f >= 2^32 there too): the zero pair, so the term is exactly +0
+        const uint32_t sj = (uint32_t)r.f[j];
+        otp[j] = sj < c.lm1 ? 4u * (c.off[j] + sj) : c.zoff;
     }
     const __attribute__((address_space(1))) char *tb = (const __attribute__((address_space(1))) char *)table;
     const f2v q0 = *(gf2v *)(tb + otp[0]), q1 = *(gf2v *)(tb + otp[1]);
@@ -525,10 +537,9 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // earlier step's loads target only once those have returned, and LDS returns first (the
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
     // issue order (vector memory returns in order), so the second does not wait for the first.
-    // The paths as lane masks (two compares and scalar mask logic; u1start >= u0lim, so a lane on
-    // the rows is never on the LDS path)
+    // The paths as lane masks (two compares and scalar mask logic)
     const bool p_lds = u < c.u0lim;
-    const bool p_row = u >= c.u1start && u < c.u1lim;
+    const bool p_row = !p_lds && u < c.u1lim;
     const bool p_own = !(p_lds || p_row);
     const int path = p_lds ? 1 : (p_row ? 0 : 2);  // (COUNT only)
     // the row step's address up front, as a 32-bit byte offset from the (wave-uniform) grid base: one
@@ -602,9 +613,9 @@ __device__ __forceinline__ CgRec cg_fetch_near(const BandLane &b, const CgLane &
 }
 
 // sampleProfile's lerp with t = fract(f[j]) -- the LDS and own-table paths' exactly as the per-band
-// gather's, the group rows' on the group grid -- then its range test (multipole.cpp:65-66) as
-// d2 >= tau: only lanes off the LDS path can be past a band's end, and only at the group's reach, so
-// the test runs when some lane of the wave is past the group's first end.
+// gather's, the group rows' on the group grid. Its range test (multipole.cpp:65-66) is already in the
+// pairs: an LDS lane is never past a band's end, an own-table lane past it read the zero pair, and a row
+// cell within a step of a band's end is flagged (its lanes took the own path), past it the rows are 0.
 // e is E * area for a point (BandTree::band_ew) and Et for a node, w unused.
 template <bool POINT, bool RGB = false>
 __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, float d2, const float e[4], float w,
@@ -622,10 +633,7 @@ __device__ __forceinline__ void cg_combine(const CgLane &c, const CgRec &r, floa
         asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(v[j].b), "v"(v[j].a));
         asm("v_fma_f32 %0, %1, %2, %3" : "=v"(rd[j]) : "v"(t), "v"(d), "v"(v[j].a));
     }
-    if (__builtin_amdgcn_ballot_w64(d2 >= c.tau_min) != 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rd[j] = d2 < c.tau[j] ? rd[j] : 0.f;
-    }
+    (void)d2;
     float o[4];
     if (RGB) from_rgb4_fused(rk, rd[0], rd[1], rd[2], o);  // slots 0..2: the R, G, B profiles on the grid
     const float *x = RGB ? o : rd;
@@ -691,17 +699,15 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
         cl.rg = a.cg.rg[grp];
         cl.u0lim = a.cg.u0lim[grp];
         cl.u1lim = a.cg.u1lim[grp];
-        cl.u1start = a.cg.u1start[grp];
-        cl.hinv = a.cg.hinv[grp];
+        cl.hinv = in_vgpr(a.cg.hinv[grp]);
         cl.hc = a.cg.hc[grp];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            cl.tau[j] = a.cg.tau[grp][j];
             cl.lrow[j] = a.cg.lrow[grp][j];
             cl.off[j] = b.off[j];
         }
-        cl.lm2 = (uint32_t)a.L - 2u;
-        cl.tau_min = fminf(fminf(cl.tau[0], cl.tau[1]), fminf(cl.tau[2], cl.tau[3]));
+        cl.lm1 = (uint32_t)a.L - 1u;
+        cl.zoff = 4u * (uint32_t)NB * (uint32_t)a.L;
     }
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     // a leaf whose points all lie within the near field of every band of the group, for any query that

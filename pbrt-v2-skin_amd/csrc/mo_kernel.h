@@ -81,13 +81,15 @@ struct DeviceProfile {
 // The common grid's bound on the resampling error of a lookup: kCgRelTol of the band's own value
 // there, or kCgAbsTol of the band's peak where that is larger (the far tails, whose values fall to
 // 1e-11 of the peak and carry under 1 % of a band's mass on C2's profile: there the bound is
-// absolute). DeviceProfile::build_common; the group rows cover only the range where every band is
-// within it. The floor is chosen on the full C2 frame against the oracle (profiles/r04p_abstol.txt):
-// 0: gather 60.4 ms, unfloored image error 1.1e-6; 1e-13: 48.6 ms, 4.3e-6; 1e-10: 47.1 ms, 9.0e-5
-// (all three at values far below the film's resolution, 1e-16 of the frame's peak).
+// absolute). DeviceProfile::build_common; a group row (cell) holding a knot off by more is flagged and
+// its lanes read the exact tables. The floor is chosen on the full C2 frame against the oracle, same
+// box (profiles/r06_grid_ab.txt, rows H steps apart with flagged cells): 1e-13: gather 43.4 ms,
+// unfloored image error 3.3e-5; 1e-14: 43.9 ms, 1.5e-6; 1e-15: 45.1 ms, 1.1e-6 -- the worst values at
+// 1e-16 of the frame's peak, far below the film's resolution (round 4, one stretch of rows per group,
+// profiles/r04p_abstol.txt: none 60.4 ms, 1.1e-6; 1e-13 48.6 ms, 4.3e-6; 1e-10 47.1 ms, 9.0e-5).
 constexpr double kCgRelTol = 2e-6;
 #ifndef MPSS_CG_ABS_TOL  // (A/B builds of the floor only)
-#define MPSS_CG_ABS_TOL 1e-13
+#define MPSS_CG_ABS_TOL 1e-14
 #endif
 constexpr double kCgAbsTol = MPSS_CG_ABS_TOL;
 

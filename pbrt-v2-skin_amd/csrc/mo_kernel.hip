@@ -532,7 +532,10 @@ void DeviceProfile::upload(const float *tab, int len, const float *rcp_, bool sn
 //     the rgbprofile's R, G, B (rgb) of the largest of the three at that distance instead of |T[s]|;
 //   * at most kCgMaxRows rows per group (32 B each: a group's rows stay well inside its XCD's 4 MB L2);
 //   * tau_j = the smallest float d2 with fl(d2 * rcp_j) >= L - 1 (sampleProfile's range test).
-constexpr int kCgMaxRows = 65536;
+#ifndef MPSS_CG_MAX_ROWS_DEFAULT  // (A/B builds of the cap only)
+#define MPSS_CG_MAX_ROWS_DEFAULT 49152
+#endif
+constexpr int kCgMaxRows = MPSS_CG_MAX_ROWS_DEFAULT;
 // (a diagnostic build, -DMPSS_DIAGNOSTICS, lets MPSS_CG_MAX_ROWS override the cap: row-cap experiments)
 static int cg_max_rows() {
 #ifdef MPSS_DIAGNOSTICS
@@ -717,8 +720,23 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             }
         }
         std::sort(fine_bad.begin(), fine_bad.end());
+        // a cell within a step of a band's profile end (u_end = (L - 1) / r_j) is flagged too: there the
+        // lanes take the own path, whose pairs carry sampleProfile's exact cutoff (multipole.cpp:65-66);
+        // past it the band's rows are exactly 0 (R is 0 from u_end + 1 on), before it every lane's f_j is
+        // at least one table step below L - 1 -- so the combine needs no range test
+        for (int j = 0; j < 4; ++j) {
+            if (groups.band[g][j] < 0) continue;
+            const double ue = (double)(L - 1) / r[j];
+            for (int hi = 0; hi < 3; ++hi) {
+                const int H = kH[hi];
+                const int64_t m0 = std::max<int64_t>(0, (int64_t)std::floor((ue - 1.0) / H));
+                const int64_t m1 = (int64_t)std::floor((ue + 2.0) / H);
+                for (int64_t m = m0; m <= m1 && m < (int64_t)bad[hi].size(); ++m) bad[hi][(size_t)m] = 1;
+            }
+        }
         // prefix scores per grid: a good cell +w, a bad one -w, w = the cell's share of records (~ H / u)
-        std::vector<double> P[3];
+        std::vector<double> P[3], W0(bad[0].size() + 1, 0.0);  // (W0: the fine cells' weights, unsigned)
+        for (size_t m = 0; m < bad[0].size(); ++m) W0[m + 1] = W0[m] + 1.0 / std::max(1.0, (double)m + 0.5);
         for (int hi = 0; hi < 3; ++hi) {
             const int H = kH[hi];
             const size_t n = bad[hi].size();
@@ -762,14 +780,19 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
         double best = 0.0, bstart = u0f;
         int64_t bua = 0, bu1 = 0;
         int bh = 0;
+        // (the rows always begin at the near field's end, so that a lane's row path is u0lim <= u < u1lim:
+        // one compare; the cells before the chosen start st are flagged)
+        const int64_t vbase = std::max<int64_t>(0, (int64_t)std::floor((double)u0f) - 1);
+        const int64_t c0 = (int64_t)std::floor((double)u0f);
         for (const double st : starts) {
-            const int64_t sb = (int64_t)std::floor(st), vbase = std::max<int64_t>(0, sb - 1);
+            const int64_t sb = (int64_t)std::floor(st);
+            const double pre = W0[(size_t)sb] - W0[(size_t)c0];  // the flagged cells before st
             // H = 1: fine rows only, [st, u1)
             {
                 const int64_t hiu = std::min<int64_t>(uend, vbase + cap);
                 if (hiu > sb) {
                     const size_t e = argmax(0, (size_t)sb + 1, (size_t)hiu);
-                    const double sc = P[0][e] - P[0][sb];
+                    const double sc = P[0][e] - P[0][sb] - pre;
                     if (sc > best) {
                         best = sc, bstart = st, bua = (int64_t)e, bu1 = (int64_t)e, bh = 0;
                     }
@@ -786,7 +809,7 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
                     const int64_t mhi = std::min<int64_t>(m0 + left, uend / H);
                     if (mhi <= m0) continue;
                     const size_t e = argmax(hi, (size_t)m0 + 1, (size_t)mhi);
-                    const double sc = sf + P[hi][e] - P[hi][m0];
+                    const double sc = sf + P[hi][e] - P[hi][m0] - pre;
                     if (sc > best) best = sc, bstart = st, bua = ua, bu1 = (int64_t)e * H, bh = hi;
                 }
             }
@@ -806,11 +829,12 @@ bool build_common_grid(const float *tab, int L, const float *host_rcp, const Ban
             cg.hc[g] = (float)((double)ua * (1.0 - 1.0 / H));  // exact: ua a multiple of 64
             cg.ua[g] = (float)ua;
         }
-        const int64_t vbase = std::max<int64_t>(0, (int64_t)std::floor(bstart) - 1);
         const int64_t v1 = ua + (bu1 - ua) / H;  // v(u1); lanes read rows <= v1 (v may round up to v1)
         auto upos = [&](int64_t v) -> int64_t { return v <= ua ? v : ua + (int64_t)H * (v - ua); };
+        const int64_t sfirst = (int64_t)std::floor(bstart);  // the first cell the chosen stretch serves
         auto cell_bad = [&](int64_t v) -> bool {
             const int64_t u = upos(v);
+            if (u < sfirst && u >= c0) return true;  // (the row below c0 is never read)
             return v < ua ? bad[0][(size_t)u] != 0 : bad[bh][(size_t)(u / H)] != 0;
         };
         cg.ubase[g] = (uint32_t)vbase;

@@ -1,7 +1,7 @@
 """The common grid of the sharded Mo() gather (mpss_config.mo_common_grid; mo_band.h CommonGrid),
 host half, on the CPU: the LDS split, the resampled pair rows and the range they serve, against a
 numpy restatement of multipole.cpp:60-73's sampleProfile (every served knot within 2e-6 of the
-band's own value, or 1e-13 of the band's peak in the far tails).
+band's own value, or 1e-14 of the band's peak in the far tails).
 
 The gather itself (LDS and own-table lanes bit-identical to the per-band gather, row lanes within
 the bound) is checked on the GPU by tests/test_mo_gpu.py and the image tests."""
@@ -13,7 +13,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.npz")
 NEAR_FIELDS = (5088, 10236)  # mpss_config.mo_near_field: the default layout and the one-workgroup one
-ABS_TOL = 1e-13  # mo_kernel.h kCgAbsTol
+ABS_TOL = 1e-14  # mo_kernel.h kCgAbsTol
 
 
 def _groups(rcp):
@@ -62,9 +62,9 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None, near_field=5088, rgb=Fals
         u0, u1, ub, r0 = cg["u0lim"][g], cg["u1lim"][g], int(cg["ubase"][g]), int(cg["row0"][g])
         if u1 <= u0:
             continue
-        us = cg["u1start"][g]  # the rows serve u in [u1start, u1lim)
+        us = cg["u1start"][g]  # the rows serve u in [u1start, u1lim); they begin at the near field's end
         assert us >= u0 and us < u1
-        assert ub == max(0, int(np.floor(us)) - 1)
+        assert ub == max(0, int(np.floor(u0)) - 1)
         # row coordinate v: u below ua, ua + (u - ua) / H above it (H = 1 / hinv, ua a multiple of 64)
         H = int(round(1.0 / cg["hinv"][g]))
         assert H in (1, 2, 4) and np.float32(1.0 / H) == cg["hinv"][g]
@@ -77,7 +77,17 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None, near_field=5088, rgb=Fals
         v = np.arange(ub, ub + n + 1, dtype=np.int64)
         upos = np.where(v <= ua, v, ua + H * (v - ua)).astype(np.float64)
         bad = np.isnan(rows[:, 0])
-        served_bad = np.zeros(n, bool)  # cells with a knot off by more than the bound
+        # cells with a knot off by more than the bound, before u1start, or within a step of a band's end
+        # (must: the cells meeting [u_end - 1, u_end + 2]; may: with a rounding margin either way)
+        served_bad = upos[1:] <= np.floor(us)
+        must = np.zeros(n, bool)
+        for j, c in enumerate(slots):
+            if c >= 0:
+                ue = (L - 1) / r[j]
+                served_bad |= (upos[1:] > ue - 1 - 1e-6) & (upos[:-1] <= ue + 2 + 1e-6)
+                must |= (upos[1:] > ue - 1 + 1e-6) & (upos[:-1] <= ue + 2 - 1e-6)
+        # every cell within a step of a band's end is flagged (the combine has no range test)
+        assert np.all(bad[must & (upos[:-1] >= np.floor(us))]), g
         for j, c in enumerate(slots):
             if c < 0:
                 assert np.all(rows[:, 2 * j:2 * j + 2] == 0)
@@ -99,7 +109,7 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None, near_field=5088, rgb=Fals
             t = vk - np.floor(vk)
             approx = (1 - t) * want0[ci].astype(np.float64) + t * want1[ci].astype(np.float64)
             err = np.abs(approx - T64[c, k])
-            # kCgRelTol of the band's value (rgb: of the largest of R, G, B there), or kCgAbsTol = 1e-13
+            # kCgRelTol of the band's value (rgb: of the largest of R, G, B there), or kCgAbsTol = 1e-14
             # of its peak where that is larger
             scale = np.abs(T64[c, k])
             if rgb:
@@ -111,7 +121,7 @@ def _check_layout(tab, rcp, cg, tol=2e-6, groups=None, near_field=5088, rgb=Fals
             # every knot off by more than the bound lies in a flagged cell (its lanes read the exact tables)
             assert np.all(bad[ci[over]]), (g, c, (err[served & ~bad[ci]] / bound[served & ~bad[ci]]).max())
             served_bad[ci[err > bound * (1 - 1e-9)]] = True
-        # and a flagged cell holds such a knot (the flags are not spent on good cells; the pad row's cell
+        # and a flagged cell is one of those (the flags are not spent on good cells; the pad row's cell
         # lies past u1lim)
         assert np.all(served_bad[:-1][bad[:-1]]), (g, np.flatnonzero(bad[:-1] & ~served_bad[:-1])[:5])
 

@@ -170,13 +170,13 @@ def _sum_bound(ref, nn, npt):
 
 def _grid_bound(ref, nn, npt, table, cloud):
     """_sum_bound for the common-grid gather: every term's lookup within kCgRelTol (2e-6, 3e-6 here for a
-    lerp between knots) of its value or kCgAbsTol (1e-13) of the band's peak (a bad cell's lanes read the
+    lerp between knots) of its value or kCgAbsTol (1e-14) of the band's peak (a bad cell's lanes read the
     exact tables), the fused lerp within a few ulp. The relative parts scale the result, and the absolute
-    part is at most 1e-13 peak_c times the E_c * area of all points."""
+    part is at most 1e-14 peak_c times the E_c * area of all points."""
     _, _, E, area = cloud
     peak = np.abs(table).max(axis=1).astype(np.float64)[None, :]
     mass = (E.astype(np.float64) * area.astype(np.float64)[:, None]).sum(axis=0)[None, :]
-    return 3e-6 * np.abs(ref) + _sum_bound(ref, nn, npt) + 1e-13 * peak * mass
+    return 3e-6 * np.abs(ref) + _sum_bound(ref, nn, npt) + 1e-14 * peak * mass
 
 
 def _within(got, ref, bound):

@@ -90,10 +90,10 @@ def test_rgb_mo_vs_oracle(mpss, exact_mo, common_grid):
     else:
         # the common grid of the three profiles: the same traversal and order as the sharded gather
         # without it (its counters equal), each far R, G, B lookup off by <= 2e-6 of the largest of the
-        # three at that distance, or 1e-13 of its peak (gather_info; build_common_grid's rgb scale; a bad
+        # three at that distance, or 1e-14 of its peak (gather_info; build_common_grid's rgb scale; a bad
         # cell's lanes read the exact tables). FromRGB's output is .94 (W min + X (mid - min) + Y (max -
         # mid)), weights <= 1.1, so each term's error is <= 6 x that, and max(R, G, B) <= R + G + B:
-        # unfloored, per query and band, |got - band| <= 6 (2e-6 S_c + 1e-13 peak mass_c) + the fused
+        # unfloored, per query and band, |got - band| <= 6 (2e-6 S_c + 1e-14 peak mass_c) + the fused
         # FMAs' few ulp of |band|, S_c = sum over the records of (R + G + B)(d2) E_c area -- the reference
         # traversal with each profile in every band (the records do not depend on the table)
         assert info["rel_err"][:3].max() <= 2e-6 and info["rel_err"][:3].max() > 0
@@ -106,7 +106,7 @@ def test_rgb_mo_vs_oracle(mpss, exact_mo, common_grid):
         S = sum(oc.mo(q, np.ascontiguousarray(np.repeat(tab[k:k + 1], 30, 0)), np.full(30, rcp[k], np.float32),
                       max_error).astype(np.float64) for k in range(3))
         mass = (E.astype(np.float64) * area.astype(np.float64)[:, None]).sum(axis=0)[None, :]
-        bound = 6 * (2e-6 * S + 1e-13 * np.abs(tab[:3]).max() * mass) + 8 * 2.0 ** -24 * np.abs(band)
+        bound = 6 * (2e-6 * S + 1e-14 * np.abs(tab[:3]).max() * mass) + 8 * 2.0 ** -24 * np.abs(band)
         err = np.abs(got.astype(np.float64) - band)
         assert np.all(err <= bound), (err / bound).max()
         assert np.array_equal(got == 0, ref == 0)
