@@ -46,7 +46,8 @@ REF_RECORD_BYTES = 12 + 4 + 4 * 30  # position, area / sumArea, 30-ba
 # lookups/s, 158.6 CU cycles per 64 lane lookups; per-lane 8-byte gathers: 2.53e11, and 2.69e11 in
 # their best load form, profiles/r03_l2_policy.json).
 L2_GATHER_CEILING_REQ_S = 2.48e11
-# The gather's binding resource since the common grid (round 4): VALU issue. Its ceiling is measured, not
+# The gather's other ceiling, VALU issue (the headline names whichever of the two runs at the larger
+# fraction: bench.headline_bound; round 5 ended L2-request-bound, round 6 VALU-bound). It is measured, not
 # assumed: tools/microbench/valu_issue.hip runs the record loop's instruction mix (with its SALU) at the
 # gather's occupancy (two 1024-thread workgroups per CU, 8 waves per SIMD) and reports wave64 VALU
 # instructions per second over the chip. Plain f32 add / mul / fma issue every ~2.3 cycles per SIMD there,
@@ -397,7 +398,10 @@ def main(a):
     if world > 1 and a.config == "c2" and not a.no_secondary:
         secondary = c3_strong_secondary(a, rank, world, local)
     if world == 1 and a.config == "c2" and a.sampler == "hash" and not a.no_secondary:
+        # pbrt's own sampler on the same frame, and C3's frame on this one GPU: the N = 1 anchor of the
+        # c3_strong series the N > 1 lines carry
         secondary = reference_sampler_secondary(a, local)
+        secondary.update(c3_strong_secondary(a, rank, world, local))
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

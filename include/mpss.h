@@ -399,13 +399,14 @@ int mpss_host_rho_table(float roughness, float eta, int double_ref_sslf, int n, 
  * table [30][L], rcp [30]; snake as mpss_config.mo_band_dealing (0, 1), or 2: an rgbprofile table
  * (rows 0..2 = R, G, B, read in slots 0..2 of every group); near_field as mpss_config.mo_near_field
  * (5088 or 10236: the LDS split the grid is built for). Outputs (each nullable): rows
- * [n_rows][8] (the groups' pair rows: group g's row for u is row0[g] + u - ubase[g], holding
- * R_0(u), R_0(u+1), ..., R_3(u), R_3(u+1)); *n_rows (call with rows NULL to size it); bands [8][4]
- * (band of each group slot, -1 empty); rg [8] (each group's grid: u = d2 * rg); u0lim / u1lim /
- * u1start [8] (lanes with u < u0lim read the exact LDS near field, u1start <= u < u1lim the rows, any
- * other u the bands' own tables; u1start = u0lim unless the rows begin past the end of bands the grid
- * cannot follow); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over the
- * knots each band reads from the rows); *ok = 1 when some group has rows. */
+ * [n_rows][8] (the groups' pair rows: group g's row for row coordinate v = u below ua[g], ua + (u - ua)
+ * hinv above it, is row0[g] + floor(v) - ubase[g], holding R_j(u_k), R_j(u_k+1) for slots j = 0..3, u_k
+ * the row's position; a NaN first value flags a cell whose lanes read the exact tables);
+ * *n_rows (call with rows NULL to size it); bands [8][4] (band of each group slot, -1 empty); rg [8]
+ * (each group's grid: u = d2 * rg); u0lim / u1lim / u1start [8] (lanes with u < u0lim read the exact
+ * LDS near field, u0lim <= u < u1lim the rows, any other u the bands' own tables; the rows' cells below
+ * u1start are flagged); row0 / ubase [8]; rel_err / l1_err [30] (the measured resampling error over the
+ * knots each band reads from the rows); ua / hinv [8]; *ok = 1 when some group has rows. */
 int mpss_host_common_grid(const float *table, uint32_t L, const float *rcp, int snake, int near_field, float *rows,
                           uint32_t *n_rows, int32_t *bands, float *rg, float *u0lim, float *u1lim, float *u1start,
                           uint32_t *row0, uint32_t *ubase, float *rel_err, float *l1_err, float *ua, float *hinv,

@@ -56,6 +56,7 @@ enum {
     V_MAX3,     // v_max3_f32
     V_RCP,      // v_rcp_f32
     V_MIX5,     // the round-5 fused record (one group-row lookup + one LDS lookup), VALU + SALU
+    V_MIX6,     // the round-6 record (one group-row lookup + one LDS lookup), VALU + SALU
     V_COUNT
 };
 static const char *kNames[V_COUNT] = {"v_fma_f32",      "v_add_f32",    "v_pk_mul_f32",   "v_pk_add_f32",
@@ -63,11 +64,12 @@ static const char *kNames[V_COUNT] = {"v_fma_f32",      "v_add_f32",    "v_pk_mu
                                       "v_lshl_add_u32", "gather mix (VALU)", "gather mix (VALU + SALU)",
                                       "v_add_u32",      "v_min_u32",    "v_min_f32",      "v_mov_b32",
                                       "v_cmp_gt_f32 (e64)", "v_mul_f32", "v_max3_f32",   "v_rcp_f32",
-                                      "gather mix r05 (fused: row + LDS record, VALU + SALU)"};
+                                      "gather mix r05 (fused: row + LDS record, VALU + SALU)",
+                                      "gather mix r06 (row + LDS record, VALU + SALU)"};
 // wave64 VALU instructions per loop step, and SALU
 static const int kValu[V_COUNT] = {32, 32, 32, 32, 32, 32, 32, 32, 32, 94, 94,  // mix: 2 records x 47
-                                   32, 32, 32, 32, 32, 32, 32, 32, 64};
-static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48, 0, 0, 0, 0, 0, 0, 0, 0, 24};
+                                   32, 32, 32, 32, 32, 32, 32, 32, 64, 68};
+static const int kSalu[V_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 48, 0, 0, 0, 0, 0, 0, 0, 0, 24, 24};
 
 #define R8(X) X X X X X X X X
 #define R4(X) X X X X
@@ -251,6 +253,55 @@ __device__ __forceinline__ void step_mix5(float (&a)[8], f2v (&p)[8], float x, f
     }
 }
 
+// The round-6 record (mo_band.h cg_fetch / cg_fix / cg_combine, counted from the hipcc -S of
+// mo_wave_cg.hip): the common head -- d2 (4 plain + 2 packed), u, the row coordinate v (fma, min), its
+// cvt and row offset, the three path compares (14 VALU) -- then a group-row record: fract(v) and three
+// moves, the flagged-cell compare, the lerp (4 sub + 4 fma), two packed FMAs (29 VALU); and an LDS
+// record: 2 packed muls, 4 cvt, 4 LDS addresses, 4 fract, the flagged-cell compare, lerp, products (39
+// VALU); with the exec-mask SALU of the path steps (12 per record).
+__device__ __forceinline__ void step_mix6(float (&a)[8], f2v (&p)[8], float x, f2v xv, uint32_t &s0, uint32_t &s1) {
+    float &d = a[0], &u = a[1], &t = a[2], &w = a[3], &e = a[4], &g = a[5], &h = a[6], &k = a[7];
+    f2v &pa = p[0], &pb = p[1], &pc = p[2], &pd = p[3];
+    uint64_t m;
+#pragma unroll
+    for (int rec = 0; rec < 2; ++rec) {
+        asm volatile("v_subrev_f32 %0, %1, %0" : "+v"(d) : "v"(x));
+        asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(pa) : "v"(xv));
+        asm volatile("v_mul_f32 %0, %0, %0" : "+v"(d));
+        asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(pa));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        asm volatile("v_add_f32 %0, %0, %1" : "+v"(d) : "v"(x));
+        asm volatile("v_mul_f32 %0, %1, %0" : "+v"(u) : "v"(x));
+        asm volatile("v_fma_f32 %0, %1, %0, %2" : "+v"(g) : "v"(u), "v"(x));
+        asm volatile("v_min_f32 %0, %0, %1" : "+v"(g) : "v"(u));
+        asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(w));
+        asm volatile("v_add_lshl_u32 %0, %0, %1, 5" : "+v"(w) : "v"(x));
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_cmp_le_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(x), "v"(u));
+        if (rec == 0) {  // group rows
+            asm volatile("v_fract_f32 %0, %0" : "+v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(e) : "v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(g) : "v"(t));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(h) : "v"(t));
+        } else {  // LDS
+            asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pb) : "v"(xv));
+            asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(pc) : "v"(xv));
+            R4(asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(k));)
+            R4(asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(k) : "v"(x));)
+            R4(asm volatile("v_fract_f32 %0, %0" : "+v"(t));)
+        }
+        asm volatile("v_cmp_u_f32_e64 %0, %1, %2" : "=s"(m) : "v"(e), "v"(e));
+        R4(asm volatile("v_sub_f32 %0, %0, %1" : "+v"(e) : "v"(x));)
+        R4(asm volatile("v_fma_f32 %0, %1, %0, %2" : "+v"(g) : "v"(t), "v"(x));)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(pd) : "v"(pb), "v"(xv));
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(pa) : "v"(pc), "v"(xv));
+        R4(asm volatile("s_add_u32 %0, %0, 32\n s_addc_u32 %1, %1, 0" : "+s"(s0), "+s"(s1) ::"scc");)
+        R4(asm volatile("s_mov_b32 %0, %1\n s_or_b32 %1, %1, %0" : "+s"(s0), "+s"(s1) ::"scc");)
+        R4(asm volatile("s_cmp_ge_i32 %0, %1\n s_cselect_b32 %0, %0, %1" : "+s"(s0) : "s"(s1) : "scc");)
+    }
+}
+
 template <int V>
 __global__ __launch_bounds__(1024) void issue_kernel(int steps, float *out, unsigned long long *span) {
     const float x = 1.0f + threadIdx.x * 1e-7f, y = 1e-3f;
@@ -274,6 +325,8 @@ __global__ __launch_bounds__(1024) void issue_kernel(int steps, float *out, unsi
             step_mix<true>(a, p, x, xv, s0, s1);
         else if (V == V_MIX5)
             step_mix5(a, p, x, xv, s0, s1);
+        else if (V == V_MIX6)
+            step_mix6(a, p, x, xv, s0, s1);
         else
             step<V>(a, x, y);
     }
@@ -317,7 +370,7 @@ int main(int argc, char **argv) {
     void (*fn[V_COUNT])(int, int, size_t, int, float *, unsigned long long *) = {
         launch<0>,  launch<1>,  launch<2>,  launch<3>,  launch<4>,  launch<5>,  launch<6>,
         launch<7>,  launch<8>,  launch<9>,  launch<10>, launch<11>, launch<12>, launch<13>,
-        launch<14>, launch<15>, launch<16>, launch<17>, launch<18>, launch<19>};
+        launch<14>, launch<15>, launch<16>, launch<17>, launch<18>, launch<19>, launch<20>};
     const int ws[4] = {1, 2, 4, 8};
     printf("{\"cus\": %d, \"clock_khz\": %d, \"steps\": %d, \"results\": [\n", cus, prop.clockRate, steps);
     bool first = true;
