@@ -52,9 +52,11 @@ L2_GATHER_CEILING_REQ_S = 2.48e11
 # gather's occupancy (two 1024-thread workgroups per CU, 8 waves per SIMD) and reports wave64 VALU
 # instructions per second over the chip. Plain f32 add / mul / fma issue every ~2.3 cycles per SIMD there,
 # packed f32, conversions, compares, selects and integer shifts every ~4.2, v_rcp every ~8.2
-# (profiles/r05c_valu_issue.json, r05e_valu_issue.json), so the ceiling is the mix's, not a per-instruction constant.
-VALU_CEILING_JSON = "profiles/r05e_valu_issue.json"
-VALU_CEILING_VARIANT = "gather mix r05 (fused: row + LDS record, VALU + SALU)"
+# (profiles/r05c_valu_issue.json, r05e_valu_issue.json, r06m_valu_issue.json), so the ceiling is the mix's, not a
+# per-instruction constant: round 6's record (the row coordinate, the flagged-cell compare, no range test)
+# issues at 6.19e11/s there.
+VALU_CEILING_JSON = "profiles/r06m_valu_issue.json"
+VALU_CEILING_VARIANT = "gather mix r06 (row + LDS record, VALU + SALU)"
 # sources whose code the PMC summary's counters describe (profiles/*_pmc.json "source_hash")
 KERNEL_SOURCES = ("pbrt-v2-skin_amd/csrc/mo_kernel.hip", "pbrt-v2-skin_amd/csrc/mo_band.h",
                   "pbrt-v2-skin_amd/csrc/mo_wave.h", "pbrt-v2-skin_amd/csrc/octree.h")
