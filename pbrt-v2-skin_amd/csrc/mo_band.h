@@ -652,14 +652,15 @@ __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, 
     band_rd_combine<POINT, RGB>(f, v, e, w, acc, rk);
 }
 
-// sum_area / d2 < max_error decided without an IEEE division in the common case: a * rcp(d) (v_rcp_f32,
-// <= 1 ulp; product <= ~2.5 ulp) trusted when it clears m by 2^-20 relative either way (m_lo, m_hi). The
-// rare near-ties (and NaN / inf) take the exact division, so the decision is always that of
-// fl(sum_area / d2) < max_error (diffusionutil.h:182).
+// sum_area / d2 < max_error decided without an IEEE division in the common case: a against the products
+// d m_lo and d m_hi (m_lo, m_hi = m (1 -+ 2^-20)): a < fl(d m_lo) puts the true quotient below m (1 - 2^-21),
+// a > fl(d m_hi) above m (1 + 2^-21) -- two plain multiplies and compares (a v_rcp_f32 issues at a quarter of
+// a multiply's rate: the multiplies measured 0.7 % faster once the gather was VALU-bound,
+// profiles/r06_grid_ab.txt r06n). The rare near-ties (and NaN / inf) take the exact division, so the
+// decision is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
 __device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, float m_hi) {
-    const float r = a * __builtin_amdgcn_rcpf(d);
-    bool below = r < m_lo;
-    const bool sure = below || r > m_hi;
+    bool below = a < d * m_lo;
+    const bool sure = below || a > d * m_hi;
     if (!sure) below = (a / d) < m;
     return below;
 }
