@@ -363,6 +363,10 @@ def _skin_params(ps, textures):
         if k in ps:
             v = ps.one(k)
             p[dst] = int(v in (True, "true", 1))
+    if p.get("gen_profile", 1) == 0:
+        import warnings
+        warnings.warn("LayeredSkin genprofile false: no Mo() term on this material (the reference would dereference "
+                      "its NULL MultipoleBSSRDFData, layeredskin.cpp:184; DESIGN.md section 2)")
     return p
 
 

@@ -11,6 +11,10 @@ layeredskin.cpp:246-255; the constructor's branches at :70-122):
 
 Each renders a small skin.pbrt frame through the production path and the oracle (its own tables:
 tables_from_oracle, its own irradiance and octree); tests/parity.py's criterion.
+
+genprofile false is parity unpinned: the reference would dereference its NULL MultipoleBSSRDFData
+(layeredskin.cpp:184, multipole.cpp rho()/albedo()), so the meaning above is this package's and the
+oracle's, and these tests check the two restatements against each other.
 """
 import os
 
