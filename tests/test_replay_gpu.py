@@ -53,6 +53,11 @@ def _scene(name, lights=None, W=40, H=32, spp=4):
                                   [0, 1, 2, 0, 2, 3]))
         sc.meshes.append(tri_mesh([[0.0, -8.0, 1.0], [0.3, -8.0, 1.2], [0.0, -8.2, 1.3]], [0, 1, 2]))
         sc.meshes.append(tri_mesh([[6.0, 0.0, 0.0], [6.3, 0.0, 0.2], [6.0, 0.2, 0.3]], [0, 1, 2]))
+        # an axis-aligned quad (a zero-thickness box: the slab test's most fragile case) whose edges lie
+        # inside the frame, between the camera and the head, so its edges and diagonal cut through pixel
+        # samples (the candidate lists and the oracle both take a hit iff some triangle is met)
+        sc.meshes.append(tri_mesh([[-0.22, -0.9, 0.05], [0.18, -0.9, 0.05], [0.18, -0.9, 0.41], [-0.22, -0.9, 0.41]],
+                                  [0, 1, 2, 0, 2, 3]))
         sc.integrator["minsampledistance"] = 0.05
     elif lights and lights.startswith("ns="):
         # the light's sample count (rounded up to a power of 2 by LDShuffleScrambled): the generator
