@@ -15,7 +15,8 @@
 #   kt[=CFG]          rocprofv3 --kernel-trace --stats of the bench -> gpurun_out/prof_TAG[_CFG]/kt
 #   pmc[=CFG]         rocprofv3 --pmc passes of the bench (one counter set per run, $PMC_SETS
 #                     overrides the default sets, one per line)   -> gpurun_out/prof_TAG[_CFG]/pmc_i
-# $BENCH_ARGS: extra bench.py arguments for kt and pmc (e.g. "--rgb-profile").
+# $BENCH_ARGS: extra bench.py arguments for kt and pmc (e.g. "--rgb-profile"). The gather's full counter sets:
+#   PMC_SETS="$(cat tools/pmc_sets_gather.txt)" (tools/pmc_sets_replay.txt for the replay generator).
 # Afterwards `python tools/summarize_prof.py TAG` writes profiles/TAG_kernel_stats.csv + TAG_pmc.json.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
