@@ -536,7 +536,11 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // Three sequential masked steps, LDS first: a later step's loads may overwrite registers an
     // earlier step's loads target only once those have returned, and LDS returns first (the
     // opposite order made every LDS lane wait for the global loads). The two global steps write in
-    // issue order (vector memory returns in order), so the second does not wait for the first.
+    // issue order (vector memory returns in order), so the second does not wait for the first. The
+    // own-table step goes before the row step: its address arithmetic reuses the record's registers
+    // as temporaries, which, behind the row step, waited for the row loads in flight to them (and,
+    // for a pair's second point, for the first point's loads too) -- the row step's only VALU work
+    // writes CgRec::f, which no load targets (C2 gather 42.8 -> 41.5 ms, profiles/r06_grid_ab.txt r06s).
     // The paths as lane masks (two compares and scalar mask logic)
     const bool p_lds = u < c.u0lim;
     const bool p_row = !p_lds && u < c.u1lim;
@@ -560,6 +564,8 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // (keeps the LDS step ahead of the global ones: the compiler otherwise orders the three steps its
     // own way and puts the LDS step last)
     asm volatile("" : "+v"(r.p01), "+v"(r.p23)::"memory");
+    if (p_own) cg_own<COUNT>(b, c, table, d2, r, hist);
+    asm volatile("" ::: "memory");  // (an order barrier only: an operand would wait for the loads)
     if (p_row) {
         gf4v *row = (gf4v *)((const __attribute__((address_space(1))) char *)c.tab + orow);
         r.p01 = row[0];
@@ -569,7 +575,6 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
 #pragma unroll
         for (int j = 0; j < 4; ++j) r.f[j] = t;
     }
-    if (p_own) cg_own<COUNT>(b, c, table, d2, r, hist);
     cg_count<COUNT>(b, c, d2, path, hist);
     return r;
 }
@@ -754,13 +759,19 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                 const bool inside = fmaxf(fmaxf(bx, by), bz) == 0.f;
                 if (dw_below(h.sum_area, d2, a.max_error, m_lo, m_hi) && !inside) {
                     resume = skip;
-                    const float4 et = et_g[node];
-                    const float e[4] = {et.x, et.y, et.z, et.w};
                     if (CG) {
                         CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        // Et's scalar load issued behind the record's table loads: issued before them,
+                        // the wait for the LDS step's reads (lgkmcnt) would wait for it too
+                        int nd = node;
+                        asm volatile("" : "+s"(nd)::"memory");
+                        const float4 et = et_g[nd];
+                        const float e[4] = {et.x, et.y, et.z, et.w};
                         cg_fix<COUNT>(b, cl, a.table, d2, r, hist);
                         cg_combine<false, RGB>(cl, r, d2, e, 1.f, acc, rk);
                     } else {
+                        const float4 et = et_g[node];
+                        const float e[4] = {et.x, et.y, et.z, et.w};
                         band_rd_accumulate<false, COUNT, KLDS, RGB>(b, d2, e, 1.f, acc, hist, rk);
                     }
                 } else {
