@@ -156,7 +156,8 @@ struct BandTree {
     BandGroups groups;
     float grcp[kGroups][4];              // rcpDsqSpacing of each group slot (0 for an empty slot)
     float grcp_max[kGroups];             // the largest of a group's rcp (its shortest reach)
-    const float *leaf_r2;                // DeviceOctree::leaf_r2 (nullable: no LDS-only point loops)
+    const float *leaf_r2;                // DeviceOctree::leaf_r2, non-null when its leaf codes (NodeHdr::pad's
+                                         // high half) hold for max_error (null: no LDS-only point loops)
     int L, n_nodes, n_points;
     float max_error, prune_f;
     CommonGrid cg;       // the grid the launch uses (launch_band: cg_half for the 5088 layout)
@@ -541,10 +542,13 @@ __device__ __forceinline__ CgRec cg_fetch(const BandLane &b, const CgLane &c, co
     // as temporaries, which, behind the row step, waited for the row loads in flight to them (and,
     // for a pair's second point, for the first point's loads too) -- the row step's only VALU work
     // writes CgRec::f, which no load targets (C2 gather 42.8 -> 41.5 ms, profiles/r06_grid_ab.txt r06s).
-    // The paths as lane masks (two compares and scalar mask logic)
-    const bool p_lds = u < c.u0lim;
-    const bool p_row = !p_lds && u < c.u1lim;
-    const bool p_own = !(p_lds || p_row);
+    // The paths as lane masks: two compares, the rest scalar mask logic (written as plain bools, the
+    // negation of a compare becomes a third compare)
+    const uint64_t m_lds = __builtin_amdgcn_ballot_w64(u < c.u0lim);
+    const uint64_t m_in = __builtin_amdgcn_ballot_w64(u < c.u1lim);
+    const bool p_lds = __builtin_amdgcn_inverse_ballot_w64(m_lds);
+    const bool p_row = __builtin_amdgcn_inverse_ballot_w64(m_in & ~m_lds);
+    const bool p_own = __builtin_amdgcn_inverse_ballot_w64(~(m_in | m_lds));
     const int path = p_lds ? 1 : (p_row ? 0 : 2);  // (COUNT only)
     // the row step's address up front, as a 32-bit byte offset from the (wave-uniform) grid base: one
     // VGPR, a global load in saddr form. (The own-table step's four addresses are formed in its branch:
@@ -664,9 +668,11 @@ __device__ __forceinline__ void band_rd_accumulate(const BandLane &b, float d2, 
 // profiles/r06_grid_ab.txt r06n). The rare near-ties (and NaN / inf) take the exact division, so the
 // decision is always that of fl(sum_area / d2) < max_error (diffusionutil.h:182).
 __device__ __forceinline__ bool dw_below(float a, float d, float m, float m_lo, float m_hi) {
-    bool below = a < d * m_lo;
-    const bool sure = below || a > d * m_hi;
-    if (!sure) below = (a / d) < m;
+    // (the masks as ballots: two compares, the rest scalar mask logic)
+    const uint64_t m_below = __builtin_amdgcn_ballot_w64(a < d * m_lo);
+    const uint64_t m_above = __builtin_amdgcn_ballot_w64(a > d * m_hi);
+    bool below = __builtin_amdgcn_inverse_ballot_w64(m_below);
+    if (__builtin_amdgcn_inverse_ballot_w64(~(m_below | m_above))) below = (a / d) < m;
     return below;
 }
 
@@ -718,8 +724,11 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
     f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
     // a leaf whose points all lie within the near field of every band of the group, for any query that
     // opens it: leaf_r2 * rcp_max < klim (with a 1e-5 margin for the roundings of d2 and f)
-    const float lds_r2_lim = CG ? a.cg.lds_r2[grp] : (float)b.klim / (a.grcp_max[grp] * 1.00001f);
-    const cptr<float> leaf_r2 = as_const(a.leaf_r2);
+    const float lds_r2_lim = !a.leaf_r2 ? 0.f : CG ? a.cg.lds_r2[grp] : (float)b.klim / (a.grcp_max[grp] * 1.00001f);
+    // as a leaf code (NodeHdr::pad's high half, DeviceOctree::ensure_leaf_r2: leaf_r2's high 16 bits
+    // rounded up): code < lim_code => leaf_r2 < lds_r2_lim (a leaf within a rounding of the limit
+    // takes the general loop)
+    const uint32_t lds_code = __float_as_uint(lds_r2_lim) >> 16;
     // box2 * rcp_min >= prune_f as one compare: prune_f carries a 1e-4 margin over the profile end,
     // far above the rounding of the quotient (rcp_min 0: pruning off, INF)
     const float box_lim = a.prune_f / a.groups.rcp_min[grp];
@@ -784,10 +793,10 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
             if (any_open) {
                 // the leaf's non-black points only (DeviceOctree::upload puts them first, h.pad)
                 f2v lacc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
-                const int live = (int)h.pad;
+                const int live = (int)(h.pad & 0xffffu);
                 if (COUNT) w_pts += live;
                 int i0 = 0;
-                if (!COUNT && KLDS > 0 && a.leaf_r2 && leaf_r2[node] < lds_r2_lim) {
+                if (!COUNT && KLDS > 0 && (h.pad >> 16) < lds_code) {
                     for (; i0 + 1 < live; i0 += 2) {
                         const int ka = h.leaf_first + i0, kb = ka + 1;
                         const float4 pa = pt_hdr[ka], pb = pt_hdr[kb];
@@ -859,13 +868,17 @@ __device__ __forceinline__ void mo_band_traverse(const BandTree &a, int grp, flo
                     if (COUNT) ++k_pts;
                     const float ex = px - ph.x, ey = py - ph.y, ez = pz - ph.z;
                     const float d2 = ex * ex + ey * ey + ez * ez;
-                    const float4 ev = e_g[kp];
-                    const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                     if (CG) {
                         CgRec r = cg_fetch<COUNT>(b, cl, a.table, d2, hist);
+                        int kq = kp;  // (E's scalar load behind the table loads, as Et's)
+                        asm volatile("" : "+s"(kq)::"memory");
+                        const float4 ev = e_g[kq];
+                        const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                         cg_fix<COUNT>(b, cl, a.table, d2, r, hist);
                         cg_combine<true, RGB>(cl, r, d2, e, ph.w, lacc, rk);
                     } else {
+                        const float4 ev = e_g[kp];
+                        const float e[4] = {ev.x, ev.y, ev.z, ev.w};
                         band_rd_accumulate<true, COUNT, KLDS, RGB>(b, d2, e, ph.w, lacc, hist, rk);
                     }
                 }

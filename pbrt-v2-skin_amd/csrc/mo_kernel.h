@@ -33,7 +33,8 @@ struct DeviceOctree {
     // maxError, or the query inside the leaf's box): max(sqrt(sumArea / maxError), diag) + diag,
     // squared, rounded up; +inf for interior nodes and leaves without a finite centroid. Lets the
     // sharded gather prove a leaf's point lookups lie in its LDS near field. Valid for
-    // leaf_r2_error == the gather's max_error.
+    // leaf_r2_error == the gather's max_error. The gather reads it as a 16-bit code in the node's
+    // header (NodeHdr::pad's high half, rounded up; ensure_leaf_r2 writes both).
     DevBuf<float> leaf_r2;
     float leaf_r2_error = -1.f;
     void ensure_leaf_r2(float max_error);  // synchronous

@@ -464,7 +464,8 @@ void launch_exact(const MoArgs &a, int max_depth, bool count, hipStream_t s) {
 
 // The device copy moves each leaf's black points (E == 0: every kernel skips them, they add
 // nothing) behind its other points, keeping the others' order, and records the count of the
-// rest in NodeHdr::pad, so the sharded gather's leaf loop needs no per-point test.
+// rest in NodeHdr::pad's low half (a leaf holds at most 8 points), so the sharded gather's leaf loop
+// needs no per-point test. (The high half: ensure_leaf_r2's leaf code.)
 void DeviceOctree::upload(const FlatOctree &t) {
     std::vector<NodeHdr> hdr = t.hdr;
     std::vector<float> ph(t.pt_hdr.size()), pe(t.pt_e.size());
@@ -966,7 +967,10 @@ void DeviceProfile::build_common(const float *tab, const BandGroups &slots, int 
 }
 
 namespace {
-__global__ void leaf_r2_kernel(const NodeHdr *__restrict__ nodes, int n, float max_error, float *__restrict__ r2) {
+// Also writes the bound's leaf code into NodeHdr::pad's high half (its low half is the live point count):
+// the bound's high 16 bits rounded up, so code < (lim's high 16 bits) => bound < lim -- the sharded
+// gather's LDS-only leaf test is then one scalar compare on the header it has loaded anyway.
+__global__ void leaf_r2_kernel(NodeHdr *__restrict__ nodes, int n, float max_error, float *__restrict__ r2) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (i >= n) return;
     const NodeHdr h = nodes[i];
@@ -988,6 +992,8 @@ __global__ void leaf_r2_kernel(const NodeHdr *__restrict__ nodes, int n, float m
         out = (float)(R * R * (1.0 + 1e-6));
     }
     r2[i] = out;
+    const uint32_t code = (__float_as_uint(out) + 0xffffu) >> 16;  // (out > 0; INF -> 0x7f80)
+    nodes[i].pad = (h.pad & 0xffffu) | (code << 16);
 }
 }  // namespace
 

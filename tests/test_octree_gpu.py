@@ -82,12 +82,47 @@ def test_gpu_build_matches_oracle(mpss, oracle):
     for f, c in zip(o["leaf_first"][leaf], o["leaf_count"][leaf]):
         ids = o["order"][f:f + c]
         want[f:f + c] = np.concatenate([ids[~black[ids]], ids[black[ids]]])
-        assert nodes["pad"][nodes["leaf_first"] == f].max() == (~black[ids]).sum()
+        assert (nodes["pad"][nodes["leaf_first"] == f] & 0xffff).max() == (~black[ids]).sum()
     assert np.array_equal(g["pt_index"], want)
     assert np.array_equal(g["pt_hdr"][:, :3], p[want])
     assert np.array_equal(np.signbit(g["pt_hdr"][:, 3]), black[want])
     assert np.array_equal(np.abs(g["pt_hdr"][:, 3]), area[want])
     assert np.array_equal(g["pt_e"][:, :30], E[want])
+
+
+def _leaf_code_bounds(nodes, max_error):
+    """ensure_leaf_r2's bound (mo_kernel.hip leaf_r2_kernel, in double) as the leaf code the gather
+    compares: its float's high 16 bits rounded up -- with a 1e-6 margin either way for the device's
+    double sqrt. Interior nodes and leaves without area: +inf (code 0x7f80)."""
+    b0, b1 = nodes["bmin"].astype(np.float64), nodes["bmax"].astype(np.float64)
+    c = nodes["p"].astype(np.float64)
+    diag = np.sqrt(((b1 - b0) ** 2).sum(axis=1))
+    corner = np.sqrt((np.maximum(np.abs(c - b0), np.abs(c - b1)) ** 2).sum(axis=1))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        opn = np.sqrt(nodes["sum_area"].astype(np.float64) / max_error) * (1 + 1e-6)
+    R = np.maximum(opn + corner, diag)
+    live = (nodes["leaf_first"] >= 0) & (nodes["sum_area"] > 0) & np.isfinite(c).all(axis=1)
+    r2 = np.where(live, R * R * (1 + 1e-6), np.inf)
+
+    def code(x):
+        return (x.astype(np.float32).view(np.uint32).astype(np.uint64) + 0xffff) >> 16
+    return code(r2 * (1 - 1e-6)), code(r2 * (1 + 1e-6))
+
+
+def test_leaf_codes_in_node_headers(mpss):
+    """NodeHdr::pad's high half (ensure_leaf_r2): the leaf's near-field bound as the 16-bit code the
+    sharded gather's LDS-only leaf test compares (code < lim's code => bound < lim), next to the
+    live-point count in the low half."""
+    p, n, E, area = synth.ellipsoid_cloud(40000, seed=23, black_frac=0.05)
+    ctx = mpss.Context()
+    ctx.set_irradiance_points(p, n, E, area)
+    nodes = ctx.octree_export()["nodes"].view(NODE).reshape(-1)
+    got = (nodes["pad"] >> 16).astype(np.uint64)
+    lo, hi = _leaf_code_bounds(nodes, float(ctx.cfg.max_error))
+    assert np.all((got >= lo) & (got <= hi))
+    assert np.all(got[nodes["leaf_first"] < 0] == 0x7f80)
+    leaf = nodes["leaf_first"] >= 0
+    assert np.all((nodes["pad"][leaf] & 0xffff) <= 8) and np.all(got[leaf] < 0x7f80)
 
 
 def test_gpu_build_rejects_coincident_points(mpss):
